@@ -1,0 +1,217 @@
+#!/usr/bin/env python3
+"""Benchmark of the stitch hot path: stitched MPix/s on a synthetic 4 x 1920x1080 rig.
+
+One "step" = one launch of the gather kernel over a batch of --frames rig captures that are
+already resident in HBM (4 camera frames each), producing --frames mosaics.  This is the work of
+Stitcher.stitch (PostScripts/Stitcher/StitcherClass.py:114-136) for each capture: bilinear
+warpPerspective of cameras 2..4 + overwrite paste of the growing mosaic, bit-exact to the CPU
+oracle (checked on frame 0 every run: "max_abs_diff").
+
+Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one process per GPU, each
+stitching its own captures (rig frames are independent: weak scaling, no data-path collective);
+barrier + synchronize around the timed region, time = max over ranks.
+
+Extra fields: "roofline" (HBM-bound gather; algorithmic bytes = mosaic bytes written + source
+bytes the mosaic actually reads, per launch, over the kernel's average duration measured with HIP
+events on its stream) and "cpu_baseline" (the reference-structured C restatement of the cascade,
+oracle/mcs_oracle.c, on the host cores, rank 0 only, bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--frames", type=int, default=32, help="rig captures per launch (per GPU)")
+    ap.add_argument("--cams", type=int, default=4)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--channels", type=int, default=3)
+    ap.add_argument("--interp", choices=["linear", "nearest"], default="linear")
+    ap.add_argument("--super-mode", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    from multicamera_stitching_amd import rig, _capi
+    from multicamera_stitching_amd.StitcherClass import _stage_desc
+
+    interp = _capi.MCS_INTER_LINEAR if args.interp == "linear" else _capi.MCS_INTER_NEAREST
+    st, images, _ = rig.calibrated_stitcher(args.cams, args.width, args.height, args.channels,
+                                            super_mode=args.super_mode, seed=0)
+    cams = [images[label] for label in st.img_labels]
+    descs = [_stage_desc(sb) for sb in st.stitchers]
+    plan = _capi.Plan(descs, args.width, args.height, args.channels, interp,
+                      device=torch.cuda.current_device())
+    C = args.channels
+    F = args.frames
+    out_w, out_h = plan.out_w, plan.out_h
+
+    # device-resident inputs: F captures per camera (frame f = camera texture rolled by f rows)
+    d_cams = []
+    for c in cams:
+        base = torch.from_numpy(c).to(dev)
+        d_cams.append(torch.stack([torch.roll(base, shifts=(rank * F + f) % c.shape[0], dims=0)
+                                   for f in range(F)]).contiguous())
+    pitch = (out_w * C + 255) // 256 * 256
+    d_out = torch.empty((F, out_h, pitch), dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream()
+
+    def step():
+        plan.stitch_device([t.data_ptr() for t in d_cams], [t[0].numel() for t in d_cams],
+                           d_out.data_ptr(), pitch, d_out[0].numel(), F, stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        step()
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    launch_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if world > 1:
+        t = torch.tensor([elapsed, launch_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, launch_ms = float(t[0]), float(t[1])
+
+    mpix_per_launch = F * out_w * out_h / 1e6
+    value = world * mpix_per_launch * args.steps / elapsed
+
+    # algorithmic bytes per launch: mosaic written once + the source pixels it reads, once
+    fp = plan.footprint()
+    bytes_per_frame = out_w * out_h * C + sum(fp) * C
+    bytes_per_launch = F * bytes_per_frame
+    achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
+    traffic = None
+    workload = f"{args.cams}x{args.width}x{args.height}x{C}-{args.interp}-super{int(args.super_mode)}-F{F}"
+    try:
+        pm = json.load(open(args.pmc_json))
+        if pm.get("workload") == workload:
+            traffic = pm.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+
+    result = None
+    if rank == 0:
+        frame0 = d_out[0, :, :out_w * C].reshape(out_h, out_w, C).cpu().numpy()
+        cpu = None
+        max_abs = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu, max_abs = cpu_baseline(st, cams, frame0, args, interp, out_w, out_h)
+        result = {
+            "metric": "stitched MPix/sec (4-cam 1080p rig)",
+            "value": round(value, 3),
+            "unit": "MPix/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic",
+            "config": {
+                "workload": ("C2 rig: %d x %dx%d BGR cameras, precomputed homographies, "
+                             "%s warpPerspective + overwrite paste (reference StitcherClass "
+                             "semantics, no blend)" % (args.cams, args.width, args.height,
+                                                       args.interp)),
+                "mosaic": [out_h, out_w, C],
+                "frames_per_step": F,
+                "super_mode": bool(args.super_mode),
+                "parallelism": f"frames sharded over {world} GPU(s)",
+            },
+            "max_abs_diff": max_abs,
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "stitch_gather",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "algorithmic_bytes_per_launch": bytes_per_launch,
+                "kernel_ms_per_launch": round(launch_ms, 4),
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return result
+
+
+def cpu_baseline(st, cams, frame0, args, interp, out_w, out_h):
+    """Reference-structured cascade on host cores (oracle/mcs_oracle.c), bounded sample."""
+    from oracle import oracle
+    threads = min(16, os.cpu_count() or 1)
+    oracle.set_threads(threads)
+    stages = [dict(H=np.asarray(sb.cachedAH), canvas_w=sb.ABSize[0], canvas_h=sb.ABSize[1],
+                   bx=sb.Bpts[0][0], by=sb.Bpts[0][1], super_mode=sb.super_mode,
+                   x_limits=sb.x_limits, y_limits=sb.y_limits) for sb in st.stitchers]
+    want = oracle.cascade_stitch(stages, cams, interp)
+    max_abs = int(np.abs(want.astype(np.int16) - frame0.astype(np.int16)).max())
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        oracle.cascade_stitch(stages, cams, interp)
+        n += 1
+        dt = time.perf_counter() - t0
+        if dt >= args.cpu_seconds or n >= 30:
+            break
+    return {
+        "value": round(n * out_w * out_h / 1e6 / dt, 3),
+        "unit": "MPix/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{n} captures of the same rig through the cascaded per-stage "
+                  f"warpPerspective+paste C restatement, {dt:.1f} s, OpenMP {threads} threads",
+    }, max_abs
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,121 @@
+/*
+ * mcs.h -- C ABI of libmcs.so, the MI355X (gfx950) multi-camera stitch hot path.
+ *
+ * The reference (kiwicampus/multicamera_stitching) is Python 2 glue around OpenCV; it has no
+ * FFI of its own.  Its per-frame hot path is
+ *     Stitcher.stitch(images_dic)                PostScripts/Stitcher/StitcherClass.py:114-136
+ *       -> N-1 x StitcherBase.stitch((B, A))                                    :211-256
+ *            cv2.warpPerspective(A, cachedAH, ABSize)                            :239
+ *            dst[By:By+hB, Bx:Bx+wB] = B                                         :240-241
+ *            dst = dst[y_limits[0]:y_limits[1], x_limits[0]:x_limits[1]]  (super) :248-251
+ * The entry points below replace exactly that chain: the Python drop-in
+ * (multicamera_stitching_amd/StitcherClass.py, module name `StitcherClass`) marshals the
+ * calibrated StitcherBase fields into mcs_stage_desc[] once, and each Stitcher.stitch call
+ * becomes one mcs_stitch_host (or mcs_stitch_device) call.  The ctypes binding a maintainer
+ * adds on the reference side is shown in INTEGRATION.md.
+ *
+ * Conventions: plain pointers and sizes only; every function returns an int status
+ * (MCS_OK = 0, negative = error) and never throws; mcs_last_error() returns a thread-local
+ * message for the last failure on the calling thread.  A plan is bound to one device and is
+ * not re-entrant (callers serialise per plan; distinct plans are independent).
+ */
+#ifndef MCS_H_
+#define MCS_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MCS_ABI_VERSION 1
+
+enum {
+    MCS_OK = 0,
+    MCS_E_INVALID = -1,     /* bad argument / null pointer */
+    MCS_E_HIP = -2,         /* HIP runtime failure (no device, launch error, ...) */
+    MCS_E_NOMEM = -3,       /* host or device allocation failed */
+    MCS_E_SHAPE = -4,       /* stage geometry inconsistent (reference would resize / raise) */
+    MCS_E_UNSUPPORTED = -5  /* channels / stage count outside what the kernels handle */
+};
+
+enum { MCS_INTER_NEAREST = 0, MCS_INTER_LINEAR = 1 };
+
+#define MCS_MAX_STAGES 15
+#define MCS_MAX_CAMS (MCS_MAX_STAGES + 1)
+
+/* One StitcherBase of the chain, in sorted-label order (StitcherClass.py:61-75). */
+typedef struct mcs_stage_desc {
+    double H[9];        /* cachedAH, row-major, FORWARD (A -> canvas) exactly as handed to
+                           cv2.warpPerspective (:239); inverted inside like OpenCV (LU, n=3) */
+    int calibrated;     /* cachedAH is not None (:223); 0 -> stage passes B through (:255-256) */
+    int canvas_w;       /* ABSize[0] (:238) */
+    int canvas_h;       /* ABSize[1] */
+    int b_x, b_y;       /* int(Bpts[0][0]), int(Bpts[0][1]) (:237) */
+    int b_w, b_h;       /* BimgSize[1], BimgSize[0]: calibrated size of B (:226) */
+    int a_w, a_h;       /* AimgSize[1], AimgSize[0]: calibrated size of A (:230) */
+    int super_mode;     /* (:248) */
+    int x_lim0, x_lim1; /* x_limits (:251), Python-slice semantics */
+    int y_lim0, y_lim1; /* y_limits (:250) */
+} mcs_stage_desc;
+
+/* Flattened geometry of a plan (what the single-pass gather kernel consumes). */
+typedef struct mcs_flat_stage {
+    double minv[9];     /* OpenCV-inverted H (cv::invert DECOMP_LU closed form) */
+    int rect[4];        /* B paste rect of this stage in OUTPUT coords: x0, y0, x1, y1 */
+    int off_x, off_y;   /* output coords -> this stage's canvas coords */
+    int bw0;            /* OpenCV WarpPerspectiveInvoker block width of the canvas */
+    int cam;            /* camera index (sorted-label order) warped by this stage */
+} mcs_flat_stage;
+
+typedef struct mcs_flat_desc {
+    int n_stages;                  /* calibrated stages only, innermost first */
+    int out_w, out_h, channels, interp;
+    int cam0_off_x, cam0_off_y;    /* output coords -> camera-0 coords */
+    int n_cams;
+    int cam_w[MCS_MAX_CAMS], cam_h[MCS_MAX_CAMS];
+    mcs_flat_stage st[MCS_MAX_STAGES];
+} mcs_flat_desc;
+
+typedef struct mcs_plan mcs_plan;
+
+/* Library / device info. */
+const char *mcs_version(void);
+int mcs_abi_version(void);
+const char *mcs_last_error(void);
+int mcs_device_count(int *n);
+/* The HIP runtime libmcs bound to (it links none: it uses the process's, e.g. PyTorch's). */
+const char *mcs_hip_runtime(void);
+
+/* Build a plan from the calibrated chain (replaces the per-stage state the reference keeps in
+ * StitcherBase, :190-209).  cam0_w/cam0_h: calibrated size of the first camera (B of stage 0).
+ * channels: 1..4 (interleaved u8, e.g. BGR = 3).  interp: MCS_INTER_LINEAR is the reference
+ * default (:239); MCS_INTER_NEAREST is the north-star C1 variant.  device: HIP ordinal.
+ * Host-side only: no device memory is touched until the first stitch call. */
+int mcs_plan_create(const mcs_stage_desc *stages, int n_stages, int cam0_w, int cam0_h,
+                    int channels, int interp, int device, mcs_plan **out);
+int mcs_plan_destroy(mcs_plan *plan);
+int mcs_plan_out_shape(const mcs_plan *plan, int *w, int *h, int *channels);
+int mcs_plan_describe(const mcs_plan *plan, mcs_flat_desc *out);
+
+/* Stitcher.stitch on host arrays (drop-in path, :114-136): cams[i] is the i-th camera in
+ * sorted-label order, dense HxWxC u8 of the calibrated size; out is a dense out_h x out_w x C
+ * buffer.  Synchronous: H2D -> kernel -> D2H on the plan's stream. */
+int mcs_stitch_host(mcs_plan *plan, const uint8_t *const *cams, uint8_t *out);
+
+/* Device-resident batch: n_frames rigs.  d_cams[i] + f*cam_frame_stride[i] is frame f of camera
+ * i (dense rows, pitch = w*C); d_out + f*out_frame_stride + y*out_pitch is output row y of frame
+ * f.  Enqueued on `stream` (a hipStream_t; NULL = plan stream); does not synchronise. */
+int mcs_stitch_device(mcs_plan *plan, const uint8_t *const *d_cams,
+                      const int64_t *cam_frame_stride, uint8_t *d_out, int64_t out_pitch,
+                      int64_t out_frame_stride, int n_frames, void *stream);
+
+/* Source pixels each camera actually contributes to the mosaic (for the roofline's algorithmic
+ * byte count): touched_px[i] for i < n_cams.  Runs a one-off marking kernel. */
+int mcs_plan_footprint(mcs_plan *plan, int64_t *touched_px, int n_cams);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MCS_H_ */

@@ -1,0 +1,266 @@
+"""ctypes binding of libmcs.so (include/mcs.h).
+
+This is the only route to pixels in the product path: there is no CPU fallback.  If the HIP
+library is missing the import of the drop-in fails loudly with instructions to build it.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("MCS_LIBRARY", os.path.join(_HERE, "libmcs.so"))
+
+MCS_OK = 0
+MCS_E_INVALID = -1
+MCS_E_HIP = -2
+MCS_E_NOMEM = -3
+MCS_E_SHAPE = -4
+MCS_E_UNSUPPORTED = -5
+MCS_INTER_NEAREST = 0
+MCS_INTER_LINEAR = 1
+MCS_MAX_STAGES = 15
+MCS_MAX_CAMS = MCS_MAX_STAGES + 1
+ABI_VERSION = 1
+
+# every symbol include/mcs.h declares (checked by tests/test_capi_exports.py)
+EXPORTS = (
+    "mcs_version", "mcs_abi_version", "mcs_last_error", "mcs_device_count", "mcs_hip_runtime",
+    "mcs_plan_create", "mcs_plan_destroy", "mcs_plan_out_shape", "mcs_plan_describe",
+    "mcs_stitch_host", "mcs_stitch_device", "mcs_plan_footprint",
+)
+
+
+class McsError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"libmcs error {code}: {msg}")
+        self.code = code
+
+
+class StageDesc(ctypes.Structure):
+    _fields_ = [
+        ("H", ctypes.c_double * 9),
+        ("calibrated", ctypes.c_int),
+        ("canvas_w", ctypes.c_int),
+        ("canvas_h", ctypes.c_int),
+        ("b_x", ctypes.c_int),
+        ("b_y", ctypes.c_int),
+        ("b_w", ctypes.c_int),
+        ("b_h", ctypes.c_int),
+        ("a_w", ctypes.c_int),
+        ("a_h", ctypes.c_int),
+        ("super_mode", ctypes.c_int),
+        ("x_lim0", ctypes.c_int),
+        ("x_lim1", ctypes.c_int),
+        ("y_lim0", ctypes.c_int),
+        ("y_lim1", ctypes.c_int),
+    ]
+
+
+class FlatStage(ctypes.Structure):
+    _fields_ = [
+        ("minv", ctypes.c_double * 9),
+        ("rect", ctypes.c_int * 4),
+        ("off_x", ctypes.c_int),
+        ("off_y", ctypes.c_int),
+        ("bw0", ctypes.c_int),
+        ("cam", ctypes.c_int),
+    ]
+
+
+class FlatDesc(ctypes.Structure):
+    _fields_ = [
+        ("n_stages", ctypes.c_int),
+        ("out_w", ctypes.c_int),
+        ("out_h", ctypes.c_int),
+        ("channels", ctypes.c_int),
+        ("interp", ctypes.c_int),
+        ("cam0_off_x", ctypes.c_int),
+        ("cam0_off_y", ctypes.c_int),
+        ("n_cams", ctypes.c_int),
+        ("cam_w", ctypes.c_int * MCS_MAX_CAMS),
+        ("cam_h", ctypes.c_int * MCS_MAX_CAMS),
+        ("st", FlatStage * MCS_MAX_STAGES),
+    ]
+
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def _preload_hip_runtime():
+    """Make sure the process will hold ONE HIP runtime, shared with PyTorch when it is installed.
+
+    libmcs links no HIP runtime; it binds to the libamdhip64 already in the process.  PyTorch-ROCm
+    bundles its own (torch/lib/libamdhip64.so); a second runtime (ROCm's libamdhip64.so.7) in the
+    same process fails to initialise.  So when torch is installed its runtime is loaded first
+    (without importing torch); torch, if imported later, then reuses it.  $MCS_HIP_RUNTIME
+    overrides the choice (handled inside libmcs).
+    """
+    if os.environ.get("MCS_HIP_RUNTIME"):
+        return
+    try:
+        import importlib.util
+        spec = importlib.util.find_spec("torch")
+    except (ImportError, ValueError):
+        spec = None
+    if spec is None or not spec.submodule_search_locations:
+        return
+    for loc in spec.submodule_search_locations:
+        cand = os.path.join(loc, "lib", "libamdhip64.so")
+        if os.path.exists(cand):
+            ctypes.CDLL(cand, mode=ctypes.RTLD_GLOBAL)
+            return
+
+
+def load() -> ctypes.CDLL:
+    """Load libmcs.so once.  Raises ImportError (loudly) when it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"libmcs.so not found at {LIB_PATH}: the MI355X stitch path has no CPU fallback. "
+                "Build it with `python -m multicamera_stitching_amd.build` (hipcc, gfx950).")
+        _preload_hip_runtime()
+        L = ctypes.CDLL(LIB_PATH)
+        P = ctypes.c_void_p
+        I = ctypes.c_int
+        L.mcs_version.restype = ctypes.c_char_p
+        L.mcs_version.argtypes = []
+        L.mcs_abi_version.restype = I
+        L.mcs_abi_version.argtypes = []
+        L.mcs_hip_runtime.restype = ctypes.c_char_p
+        L.mcs_hip_runtime.argtypes = []
+        L.mcs_last_error.restype = ctypes.c_char_p
+        L.mcs_last_error.argtypes = []
+        L.mcs_device_count.argtypes = [ctypes.POINTER(I)]
+        L.mcs_device_count.restype = I
+        L.mcs_plan_create.argtypes = [ctypes.POINTER(StageDesc), I, I, I, I, I, I,
+                                      ctypes.POINTER(P)]
+        L.mcs_plan_create.restype = I
+        L.mcs_plan_destroy.argtypes = [P]
+        L.mcs_plan_destroy.restype = I
+        L.mcs_plan_out_shape.argtypes = [P, ctypes.POINTER(I), ctypes.POINTER(I),
+                                         ctypes.POINTER(I)]
+        L.mcs_plan_out_shape.restype = I
+        L.mcs_plan_describe.argtypes = [P, ctypes.POINTER(FlatDesc)]
+        L.mcs_plan_describe.restype = I
+        L.mcs_stitch_host.argtypes = [P, ctypes.POINTER(P), P]
+        L.mcs_stitch_host.restype = I
+        L.mcs_stitch_device.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_int64), P,
+                                        ctypes.c_int64, ctypes.c_int64, I, P]
+        L.mcs_stitch_device.restype = I
+        L.mcs_plan_footprint.argtypes = [P, ctypes.POINTER(ctypes.c_int64), I]
+        L.mcs_plan_footprint.restype = I
+        if L.mcs_abi_version() != ABI_VERSION:
+            raise ImportError(f"libmcs ABI {L.mcs_abi_version()} != expected {ABI_VERSION}")
+        _lib = L
+    return _lib
+
+
+def check(rc: int):
+    if rc != MCS_OK:
+        msg = load().mcs_last_error()
+        raise McsError(rc, msg.decode() if msg else "")
+
+
+def hip_runtime() -> str:
+    return load().mcs_hip_runtime().decode()
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    rc = load().mcs_device_count(ctypes.byref(n))
+    return n.value if rc == MCS_OK else 0
+
+
+class Plan:
+    """Owning handle of an mcs_plan (flattened geometry of one calibrated chain)."""
+
+    def __init__(self, stages, cam0_w: int, cam0_h: int, channels: int,
+                 interp: int = MCS_INTER_LINEAR, device: int = 0):
+        L = load()
+        arr = (StageDesc * max(1, len(stages)))()
+        for i, s in enumerate(stages):
+            arr[i] = s
+        h = ctypes.c_void_p()
+        check(L.mcs_plan_create(arr, len(stages), int(cam0_w), int(cam0_h), int(channels),
+                                int(interp), int(device), ctypes.byref(h)))
+        self._h = h
+        self._lib = L
+        w, hh, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        check(L.mcs_plan_out_shape(h, ctypes.byref(w), ctypes.byref(hh), ctypes.byref(c)))
+        self.out_w, self.out_h, self.channels = w.value, hh.value, c.value
+        self.interp = int(interp)
+        self.device = int(device)
+        fd = FlatDesc()
+        check(L.mcs_plan_describe(h, ctypes.byref(fd)))
+        self.flat = fd
+        self.n_cams = fd.n_cams
+        self.cam_shapes = [(fd.cam_h[i], fd.cam_w[i]) for i in range(fd.n_cams)]
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._lib.mcs_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def out_shape(self):
+        if self.channels == 1:
+            return (self.out_h, self.out_w)
+        return (self.out_h, self.out_w, self.channels)
+
+    def describe(self) -> dict:
+        fd = self.flat
+        n = fd.n_stages
+        return {
+            "n_stages": n,
+            "out_w": fd.out_w, "out_h": fd.out_h, "channels": fd.channels,
+            "off_x": [fd.st[j].off_x for j in range(n)] + [fd.cam0_off_x],
+            "off_y": [fd.st[j].off_y for j in range(n)] + [fd.cam0_off_y],
+            "rect": [list(fd.st[j].rect) for j in range(n)],
+            "minv": [list(fd.st[j].minv) for j in range(n)],
+            "bw0": [fd.st[j].bw0 for j in range(n)],
+            "cam": [fd.st[j].cam for j in range(n)],
+            "cam_w": [fd.cam_w[i] for i in range(fd.n_cams)],
+            "cam_h": [fd.cam_h[i] for i in range(fd.n_cams)],
+        }
+
+    def stitch_host(self, cams) -> np.ndarray:
+        """cams: list of dense u8 arrays of the calibrated shapes (sorted-label order)."""
+        cams = [np.ascontiguousarray(c, dtype=np.uint8) for c in cams]
+        out = np.empty(self.out_shape(), np.uint8)
+        ptrs = (ctypes.c_void_p * len(cams))(*[c.ctypes.data for c in cams])
+        check(self._lib.mcs_stitch_host(self._h, ptrs, out.ctypes.data_as(ctypes.c_void_p)))
+        return out
+
+    def stitch_device(self, cam_ptrs, cam_frame_strides, out_ptr: int, out_pitch: int,
+                      out_frame_stride: int, n_frames: int, stream: int = 0):
+        """Device-resident batch (raw device pointers, e.g. torch tensor data_ptr())."""
+        n = len(cam_ptrs)
+        ptrs = (ctypes.c_void_p * n)(*[int(p) for p in cam_ptrs])
+        strides = (ctypes.c_int64 * n)(*[int(s) for s in cam_frame_strides])
+        check(self._lib.mcs_stitch_device(self._h, ptrs, strides, ctypes.c_void_p(int(out_ptr)),
+                                          int(out_pitch), int(out_frame_stride), int(n_frames),
+                                          ctypes.c_void_p(int(stream))))
+
+    def footprint(self):
+        arr = (ctypes.c_int64 * MCS_MAX_CAMS)()
+        check(self._lib.mcs_plan_footprint(self._h, arr, MCS_MAX_CAMS))
+        return [int(arr[i]) for i in range(self.n_cams)]

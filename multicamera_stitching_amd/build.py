@@ -1,0 +1,84 @@
+"""Builds libmcs.so in-tree.
+
+Two steps:
+  1. hipcc compiles csrc/mcs_kernels.hip device-only for gfx950 into a code object
+     (mcs_kernels.gfx950.hsaco);
+  2. g++ compiles the host side (plan builder, HIP runtime binding, C ABI) and embeds that code
+     object (.incbin) into libmcs.so.  libmcs links no HIP runtime: it binds to the one the process
+     already has (PyTorch's) or to ROCm's (csrc/hip_rt.h explains why).
+
+The library is the product path: the Python drop-in refuses to run without it.
+Usage: python -m multicamera_stitching_amd.build [--force]
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "libmcs.so")
+ARCH = os.environ.get("MCS_OFFLOAD_ARCH", "gfx950")
+HSACO = os.path.join(HERE, f"mcs_kernels.{ARCH}.hsaco")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+HIPCC = os.environ.get("HIPCC", os.path.join(ROCM, "bin", "hipcc"))
+CXX = os.environ.get("CXX", "g++")
+DEVICE_SRC = "mcs_kernels.hip"
+HOST_SRC = ["mcs_plan.cpp", "hip_rt.cpp", "mcs_capi.cpp"]
+HEADERS = ["mcs_kparams.h", "mcs_common.h", "hip_rt.h"]
+INC = ["-I" + os.path.join(ROOT, "include"), "-I" + CSRC]
+
+DEVICE_FLAGS = [
+    f"--offload-arch={ARCH}", "--offload-device-only", "--no-gpu-bundle-output",
+    "-O3", "-std=c++17",
+    # bit-exact OpenCV arithmetic: no FMA contraction of the FP64 coordinate map
+    "-ffp-contract=off", "-fno-fast-math", "-Wall",
+]
+HOST_FLAGS = [
+    "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wextra", "-Wno-unused-parameter",
+    # cv::invert must be bit-identical: no FMA contraction on the host either
+    "-ffp-contract=off", "-fno-fast-math",
+    "-D__HIP_PLATFORM_AMD__", "-I" + os.path.join(ROCM, "include"),
+]
+
+
+def _stale() -> bool:
+    if not (os.path.exists(LIB) and os.path.exists(HSACO)):
+        return True
+    t = min(os.path.getmtime(LIB), os.path.getmtime(HSACO))
+    deps = [os.path.join(CSRC, s) for s in [DEVICE_SRC, *HOST_SRC, *HEADERS]]
+    deps += [os.path.join(ROOT, "include", "mcs.h"), __file__]
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd, verbose):
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.check_call(cmd)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not _stale():
+        return LIB
+    _run([HIPCC, *DEVICE_FLAGS, *INC, "-o", HSACO + ".tmp", os.path.join(CSRC, DEVICE_SRC)],
+         verbose)
+    os.replace(HSACO + ".tmp", HSACO)
+    blob = os.path.join(HERE, "mcs_blob.S")
+    with open(blob, "w") as f:
+        f.write('    .section .rodata\n    .balign 4096\n    .globl mcs_hsaco_start\n'
+                'mcs_hsaco_start:\n    .incbin "%s"\n    .globl mcs_hsaco_end\n'
+                'mcs_hsaco_end:\n    .byte 0\n    .section .note.GNU-stack,"",@progbits\n'
+                % HSACO)
+    try:
+        _run([CXX, *HOST_FLAGS, *INC, "-o", LIB + ".tmp",
+              *[os.path.join(CSRC, s) for s in HOST_SRC], blob, "-ldl", "-lpthread"], verbose)
+    finally:
+        os.remove(blob)
+    os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

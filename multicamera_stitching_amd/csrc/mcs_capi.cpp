@@ -1,0 +1,354 @@
+// mcs_capi.cpp -- the extern "C" boundary of libmcs.so (declared in include/mcs.h).
+//
+// Replaces, for a calibrated chain, the per-frame work of Stitcher.stitch
+// (PostScripts/Stitcher/StitcherClass.py:114-136).  No exception crosses this boundary: every
+// entry point returns an MCS_* status and leaves a message in mcs_last_error().
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+
+#include "hip_rt.h"
+#include "mcs_common.h"
+
+// gfx950 code object of mcs_kernels.hip, embedded by the build (mcs_blob.S)
+extern "C" const unsigned char mcs_hsaco_start[];
+extern "C" const unsigned char mcs_hsaco_end[];
+
+struct mcs_plan {
+    mcs_flat_desc fd;
+    mcs::KParams kp;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    // device buffers for the host-array path (allocated on first use)
+    uint8_t *d_cams[MCS_MAX_CAMS] = {};
+    uint8_t *d_out = nullptr;
+    int64_t out_pitch = 0;
+};
+
+#define MCS_VERSION_STRING "mcs 0.1.0 (gfx950 code object, HIP module launch)"
+
+#define HIP_TRY(expr)                                                                          \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess)                                                                  \
+            return mcs::fail(MCS_E_HIP, "%s failed: %s", #expr, A->hipGetErrorString(e_));   \
+    } while (0)
+
+namespace {
+
+using mcs::rt::Api;
+
+constexpr int kMaxDevices = 64;
+
+struct Kernels {
+    hipModule_t mod = nullptr;
+    hipFunction_t stitch[5][2] = {};   // [channels][interp]
+    hipFunction_t footprint[2] = {};
+};
+Kernels g_k[kMaxDevices];
+std::mutex g_k_mu;
+
+// Loads the embedded code object on the current device (once per device).
+int kernels(const Api *A, int device, const Kernels **out)
+{
+    if (device < 0 || device >= kMaxDevices) return mcs::fail(MCS_E_INVALID, "device %d", device);
+    std::lock_guard<std::mutex> lk(g_k_mu);
+    Kernels &k = g_k[device];
+    if (!k.mod) {
+        hipModule_t m = nullptr;
+        HIP_TRY(A->hipModuleLoadData(&m, mcs_hsaco_start));
+        char name[64];
+        for (int c = 1; c <= 4; c++)
+            for (int i = 0; i < 2; i++) {
+                snprintf(name, sizeof(name), "mcs_stitch_c%d_i%d", c, i);
+                HIP_TRY(A->hipModuleGetFunction(&k.stitch[c][i], m, name));
+            }
+        HIP_TRY(A->hipModuleGetFunction(&k.footprint[0], m, "mcs_footprint_i0"));
+        HIP_TRY(A->hipModuleGetFunction(&k.footprint[1], m, "mcs_footprint_i1"));
+        k.mod = m;
+    }
+    *out = &k;
+    return MCS_OK;
+}
+
+// Makes the plan's device current for the duration of a call and restores the caller's.
+struct DeviceGuard {
+    const Api *A;
+    int prev = -1;
+    hipError_t err = hipSuccess;
+    DeviceGuard(const Api *a, int dev) : A(a)
+    {
+        err = A->hipGetDevice(&prev);
+        if (err == hipSuccess && prev != dev) err = A->hipSetDevice(dev);
+    }
+    ~DeviceGuard()
+    {
+        if (prev >= 0) (void)A->hipSetDevice(prev);
+    }
+};
+
+int ensure_stream(const Api *A, mcs_plan *p)
+{
+    if (!p->stream) HIP_TRY(A->hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
+    return MCS_OK;
+}
+
+int ensure_host_buffers(const Api *A, mcs_plan *p)
+{
+    const int C = p->fd.channels;
+    for (int i = 0; i < p->fd.n_cams; i++) {
+        if (p->d_cams[i]) continue;
+        const size_t bytes = (size_t)p->fd.cam_w[i] * p->fd.cam_h[i] * C;
+        HIP_TRY(A->hipMalloc((void **)&p->d_cams[i], bytes > 0 ? bytes : 1));
+    }
+    if (!p->d_out && p->fd.out_w > 0 && p->fd.out_h > 0) {
+        p->out_pitch = ((int64_t)p->fd.out_w * C + 63) / 64 * 64;
+        HIP_TRY(A->hipMalloc((void **)&p->d_out, (size_t)p->out_pitch * p->fd.out_h));
+    }
+    return MCS_OK;
+}
+
+int launch_stitch(const Api *A, const mcs_plan *p, const mcs::KParams &kp, int n_frames,
+                  hipStream_t s)
+{
+    if (kp.out_w <= 0 || kp.out_h <= 0 || n_frames <= 0) return MCS_OK;
+    const Kernels *k = nullptr;
+    int rc = kernels(A, p->device, &k);
+    if (rc) return rc;
+    size_t sz = sizeof(kp);
+    void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, (void *)&kp, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz,
+                   HIP_LAUNCH_PARAM_END};
+    const unsigned gx = (kp.out_w + mcs::kTileW - 1) / mcs::kTileW;
+    const unsigned gy = (kp.out_h + mcs::kRows - 1) / mcs::kRows;
+    HIP_TRY(A->hipModuleLaunchKernel(k->stitch[p->fd.channels][p->fd.interp], gx, gy,
+                                     (unsigned)n_frames, mcs::kWave, mcs::kWavesPerBlock, 1, 0, s,
+                                     nullptr, cfg));
+    return MCS_OK;
+}
+
+void need_mask(const mcs_flat_desc &fd, bool *need)
+{
+    for (int i = 0; i < MCS_MAX_CAMS; i++) need[i] = false;
+    need[0] = true;
+    for (int j = 0; j < fd.n_stages; j++) need[fd.st[j].cam] = true;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *mcs_version(void) { return MCS_VERSION_STRING; }
+
+int mcs_abi_version(void) { return MCS_ABI_VERSION; }
+
+const char *mcs_hip_runtime(void)
+{
+    (void)mcs::rt::api();
+    return mcs::rt::runtime_name();
+}
+
+const char *mcs_last_error(void) { return mcs::last_error(); }
+
+int mcs_device_count(int *n)
+{
+    if (!n) return mcs::fail(MCS_E_INVALID, "n is NULL");
+    *n = 0;
+    const Api *A = mcs::rt::api();
+    if (!A) return MCS_E_HIP;
+    int c = 0;
+    hipError_t e = A->hipGetDeviceCount(&c);
+    if (e != hipSuccess)
+        return mcs::fail(MCS_E_HIP, "hipGetDeviceCount: %s", A->hipGetErrorString(e));
+    *n = c;
+    return MCS_OK;
+}
+
+int mcs_plan_create(const mcs_stage_desc *stages, int n_stages, int cam0_w, int cam0_h,
+                    int channels, int interp, int device, mcs_plan **out)
+{
+    mcs::clear_error();
+    if (!stages || !out) return mcs::fail(MCS_E_INVALID, "NULL stages/out");
+    *out = nullptr;
+    if (device < 0 || device >= kMaxDevices) return mcs::fail(MCS_E_INVALID, "device=%d", device);
+    mcs_plan *p = new (std::nothrow) mcs_plan();
+    if (!p) return mcs::fail(MCS_E_NOMEM, "plan allocation");
+    int rc = mcs::build_flat(stages, n_stages, cam0_w, cam0_h, channels, interp, &p->fd);
+    if (rc != MCS_OK) {
+        delete p;
+        return rc;
+    }
+    mcs::fill_kparams(p->fd, &p->kp);
+    p->device = device;
+    *out = p;
+    return MCS_OK;
+}
+
+int mcs_plan_destroy(mcs_plan *p)
+{
+    if (!p) return MCS_OK;
+    bool touched = p->stream || p->d_out;
+    for (int i = 0; i < MCS_MAX_CAMS; i++) touched = touched || p->d_cams[i];
+    if (touched) {
+        const Api *A = mcs::rt::api();
+        if (A) {
+            DeviceGuard g(A, p->device);
+            if (p->stream) (void)A->hipStreamSynchronize(p->stream);
+            for (int i = 0; i < MCS_MAX_CAMS; i++)
+                if (p->d_cams[i]) (void)A->hipFree(p->d_cams[i]);
+            if (p->d_out) (void)A->hipFree(p->d_out);
+            if (p->stream) (void)A->hipStreamDestroy(p->stream);
+        }
+    }
+    delete p;
+    return MCS_OK;
+}
+
+int mcs_plan_out_shape(const mcs_plan *p, int *w, int *h, int *channels)
+{
+    if (!p) return mcs::fail(MCS_E_INVALID, "NULL plan");
+    if (w) *w = p->fd.out_w;
+    if (h) *h = p->fd.out_h;
+    if (channels) *channels = p->fd.channels;
+    return MCS_OK;
+}
+
+int mcs_plan_describe(const mcs_plan *p, mcs_flat_desc *out)
+{
+    if (!p || !out) return mcs::fail(MCS_E_INVALID, "NULL plan/out");
+    *out = p->fd;
+    return MCS_OK;
+}
+
+int mcs_stitch_host(mcs_plan *p, const uint8_t *const *cams, uint8_t *out)
+{
+    mcs::clear_error();
+    if (!p || !cams || !out) return mcs::fail(MCS_E_INVALID, "NULL plan/cams/out");
+    const Api *A = mcs::rt::api();
+    if (!A) return MCS_E_HIP;
+    const int C = p->fd.channels;
+    DeviceGuard g(A, p->device);
+    if (g.err != hipSuccess)
+        return mcs::fail(MCS_E_HIP, "hipSetDevice(%d): %s", p->device, A->hipGetErrorString(g.err));
+    int rc = ensure_stream(A, p);
+    if (rc) return rc;
+    rc = ensure_host_buffers(A, p);
+    if (rc) return rc;
+    if (p->fd.out_w <= 0 || p->fd.out_h <= 0) return MCS_OK;
+    // only cameras that contribute are uploaded (a passthrough stage's A is never read)
+    bool need[MCS_MAX_CAMS];
+    need_mask(p->fd, need);
+    for (int i = 0; i < p->fd.n_cams; i++) {
+        if (!need[i]) continue;
+        if (!cams[i]) return mcs::fail(MCS_E_INVALID, "cams[%d] NULL", i);
+        const size_t bytes = (size_t)p->fd.cam_w[i] * p->fd.cam_h[i] * C;
+        HIP_TRY(A->hipMemcpyAsync(p->d_cams[i], cams[i], bytes, hipMemcpyHostToDevice, p->stream));
+    }
+    mcs::KParams kp = p->kp;
+    for (int i = 0; i < p->fd.n_cams; i++) {
+        kp.cams[i] = p->d_cams[i];
+        kp.cam_fstride[i] = 0;
+    }
+    kp.out = p->d_out;
+    kp.out_pitch = p->out_pitch;
+    kp.out_fstride = 0;
+    rc = launch_stitch(A, p, kp, 1, p->stream);
+    if (rc) return rc;
+    const size_t row = (size_t)p->fd.out_w * C;
+    HIP_TRY(A->hipMemcpy2DAsync(out, row, p->d_out, (size_t)p->out_pitch, row, p->fd.out_h,
+                                hipMemcpyDeviceToHost, p->stream));
+    HIP_TRY(A->hipStreamSynchronize(p->stream));
+    return MCS_OK;
+}
+
+int mcs_stitch_device(mcs_plan *p, const uint8_t *const *d_cams, const int64_t *cam_frame_stride,
+                      uint8_t *d_out, int64_t out_pitch, int64_t out_frame_stride, int n_frames,
+                      void *stream)
+{
+    if (!p || !d_cams || !d_out) return mcs::fail(MCS_E_INVALID, "NULL plan/d_cams/d_out");
+    if (n_frames < 0 || n_frames > 65535) return mcs::fail(MCS_E_INVALID, "n_frames=%d", n_frames);
+    const int C = p->fd.channels;
+    if (out_pitch < (int64_t)p->fd.out_w * C)
+        return mcs::fail(MCS_E_INVALID, "out_pitch %lld < row bytes %lld", (long long)out_pitch,
+                         (long long)p->fd.out_w * C);
+    const Api *A = mcs::rt::api();
+    if (!A) return MCS_E_HIP;
+    mcs::KParams kp = p->kp;
+    bool need[MCS_MAX_CAMS];
+    need_mask(p->fd, need);
+    for (int i = 0; i < p->fd.n_cams; i++) {
+        if (need[i] && !d_cams[i]) return mcs::fail(MCS_E_INVALID, "d_cams[%d] NULL", i);
+        kp.cams[i] = d_cams[i];
+        kp.cam_fstride[i] = cam_frame_stride ? cam_frame_stride[i]
+                                             : (int64_t)p->fd.cam_w[i] * p->fd.cam_h[i] * C;
+    }
+    kp.out = d_out;
+    kp.out_pitch = out_pitch;
+    kp.out_fstride = out_frame_stride ? out_frame_stride : out_pitch * p->fd.out_h;
+    DeviceGuard g(A, p->device);
+    if (g.err != hipSuccess)
+        return mcs::fail(MCS_E_HIP, "hipSetDevice(%d): %s", p->device, A->hipGetErrorString(g.err));
+    hipStream_t s = (hipStream_t)stream;
+    if (!s) {
+        int rc = ensure_stream(A, p);
+        if (rc) return rc;
+        s = p->stream;
+    }
+    return launch_stitch(A, p, kp, n_frames, s);
+}
+
+int mcs_plan_footprint(mcs_plan *p, int64_t *touched_px, int n_cams)
+{
+    if (!p || !touched_px) return mcs::fail(MCS_E_INVALID, "NULL plan/touched_px");
+    if (n_cams < p->fd.n_cams)
+        return mcs::fail(MCS_E_INVALID, "n_cams %d < %d", n_cams, p->fd.n_cams);
+    const Api *A = mcs::rt::api();
+    if (!A) return MCS_E_HIP;
+    DeviceGuard g(A, p->device);
+    if (g.err != hipSuccess)
+        return mcs::fail(MCS_E_HIP, "hipSetDevice(%d): %s", p->device, A->hipGetErrorString(g.err));
+    int rc = ensure_stream(A, p);
+    if (rc) return rc;
+    const Kernels *k = nullptr;
+    rc = kernels(A, p->device, &k);
+    if (rc) return rc;
+    const int n = p->fd.n_cams;
+    uint8_t *masks[MCS_MAX_CAMS] = {};
+    uint8_t **d_masks = nullptr;
+    unsigned long long *d_counts = nullptr;
+    unsigned long long counts[MCS_MAX_CAMS] = {};
+    hipError_t e = hipSuccess;
+    for (int i = 0; i < n && e == hipSuccess; i++) {
+        const size_t bytes = ((size_t)p->fd.cam_w[i] * p->fd.cam_h[i] + 3) / 4 * 4;
+        e = A->hipMalloc((void **)&masks[i], bytes > 0 ? bytes : 4);
+        if (e == hipSuccess) e = A->hipMemsetAsync(masks[i], 0, bytes > 0 ? bytes : 4, p->stream);
+    }
+    if (e == hipSuccess) e = A->hipMalloc((void **)&d_masks, sizeof(masks));
+    if (e == hipSuccess) e = A->hipMalloc((void **)&d_counts, sizeof(counts));
+    if (e == hipSuccess)
+        e = A->hipMemcpyAsync(d_masks, masks, sizeof(masks), hipMemcpyHostToDevice, p->stream);
+    if (e == hipSuccess) e = A->hipMemsetAsync(d_counts, 0, sizeof(counts), p->stream);
+    if (e == hipSuccess && p->fd.out_w > 0 && p->fd.out_h > 0) {
+        mcs::KFootprintArgs args;
+        args.P = p->kp;
+        args.masks = d_masks;
+        args.counts = d_counts;
+        size_t sz = sizeof(args);
+        void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, (void *)&args, HIP_LAUNCH_PARAM_BUFFER_SIZE,
+                       &sz, HIP_LAUNCH_PARAM_END};
+        e = A->hipModuleLaunchKernel(k->footprint[p->fd.interp], (p->fd.out_w + 255) / 256,
+                                     p->fd.out_h, 1, 256, 1, 1, 0, p->stream, nullptr, cfg);
+    }
+    if (e == hipSuccess)
+        e = A->hipMemcpyAsync(counts, d_counts, sizeof(counts), hipMemcpyDeviceToHost, p->stream);
+    if (e == hipSuccess) e = A->hipStreamSynchronize(p->stream);
+    for (int i = 0; i < n; i++)
+        if (masks[i]) (void)A->hipFree(masks[i]);
+    if (d_masks) (void)A->hipFree(d_masks);
+    if (d_counts) (void)A->hipFree(d_counts);
+    if (e != hipSuccess) return mcs::fail(MCS_E_HIP, "footprint: %s", A->hipGetErrorString(e));
+    for (int i = 0; i < n_cams; i++) touched_px[i] = i < n ? (int64_t)counts[i] : 0;
+    return MCS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,287 @@
+// mcs_kernels.hip -- gfx950 kernels of the stitch hot path.
+//
+// stitch_gather: renders the FINAL mosaic of the reference chain
+// (PostScripts/Stitcher/StitcherClass.py:114-136 -> :211-256) in one pass, one output pixel
+// once.  Per pixel: (1) ownership walk through the nested paste rectangles (integer compares
+// against wave-uniform kernargs), (2) OpenCV-exact projective map of its canvas coordinate
+// (FP64 in OpenCV's operation order, 64-column block start, round-half-even -- Appendix A of
+// SURVEY.md), (3) 4-tap 15-bit fixed-point bilinear (or nearest) gather from that camera, border
+// 0.  Layout: each lane owns 4 consecutive pixels of one row (12 B for BGR -> one dwordx3
+// store), a wave owns 256 contiguous pixels of a row, a 256-thread block 256 x 16 pixels of one
+// frame; grid.z walks the frames of a batch.
+//
+// Built device-only (hipcc --offload-device-only --no-gpu-bundle-output) into a gfx950 code
+// object embedded in libmcs.so; the host launches the extern "C" entry points at the bottom
+// through hipModuleLaunchKernel.  -ffp-contract=off: no FMA contraction, like OpenCV's
+// SSE2/SSE4.1 x86 code.
+#include <hip/hip_runtime.h>
+
+#include "mcs_kparams.h"
+
+namespace mcs {
+
+__device__ __forceinline__ int sat_i16(int v) { return min(max(v, -32768), 32767); }
+
+// std::max(INT_MIN, std::min(INT_MAX, v)) then cvRound (round half to even).
+__device__ __forceinline__ int cv_round_clamped(double v)
+{
+    const double a = 2147483647.0, b = -2147483648.0;
+    v = (v < a) ? v : a;
+    v = (b < v) ? v : b;
+    return (int)__builtin_rint(v);
+}
+
+// WarpPerspectiveInvoker arithmetic for canvas pixel (X, Y) of a stage.  Returns the
+// fixed-point source coordinate (1/32 px units for bilinear, whole px for nearest).
+template <int INTERP>
+__device__ __forceinline__ void map_exact(const KStage &S, int X, int Y, int &xo, int &yo)
+{
+    const int xb = S.bw_shift >= 0 ? ((X >> S.bw_shift) << S.bw_shift) : (X / S.bw0) * S.bw0;
+    const int x1 = X - xb;
+    const double dxb = (double)xb, dy = (double)Y, dx1 = (double)x1;
+    const double X0 = S.m[0] * dxb + S.m[1] * dy + S.m[2];
+    const double Y0 = S.m[3] * dxb + S.m[4] * dy + S.m[5];
+    const double W0 = S.m[6] * dxb + S.m[7] * dy + S.m[8];
+    double W = W0 + S.m[6] * dx1;
+    if (INTERP == MCS_INTER_LINEAR) W = (W != 0.0) ? 32.0 / W : 0.0;
+    else W = (W != 0.0) ? 1.0 / W : 0.0;
+    xo = cv_round_clamped((X0 + S.m[0] * dx1) * W);
+    yo = cv_round_clamped((Y0 + S.m[3] * dx1) * W);
+}
+
+// 8 bytes starting at byte offset o of a frame of `fbytes` bytes (only the first NB are used).
+// Unaligned dwordx2 in the common case; an in-bounds dword path at the very end of a frame.
+template <int NB>
+__device__ __forceinline__ uint2 load8(const uint8_t *fb, int64_t o, int64_t fbytes)
+{
+    uint2 r;
+    if (o + 8 <= fbytes) {
+        __builtin_memcpy(&r, fb + o, 8);
+    } else {
+        const uint32_t *p = reinterpret_cast<const uint32_t *>(fb + (o & ~int64_t(3)));
+        const uint32_t sh = (uint32_t)o & 3u;
+        const uint32_t last = (sh + NB - 1) >> 2;
+        const uint32_t w0 = p[0];
+        const uint32_t w1 = p[last < 1 ? last : 1];
+        const uint32_t w2 = p[last < 2 ? last : 2];
+        r.x = __builtin_amdgcn_alignbyte(w1, w0, sh);
+        r.y = __builtin_amdgcn_alignbyte(w2, w1, sh);
+    }
+    return r;
+}
+
+__device__ __forceinline__ uint32_t byte_of(uint2 v, int i)
+{
+    return ((i < 4 ? v.x : v.y) >> (8 * (i & 3))) & 0xffu;
+}
+
+// remapBilinear / remapNearest for one pixel, BORDER_CONSTANT 0, writing CN bytes to px[].
+template <int CN, int INTERP>
+__device__ __forceinline__ void sample(const uint8_t *fb, int sw, int sh, int64_t fbytes, int X,
+                                       int Y, uint32_t *px)
+{
+    const int64_t pitch = (int64_t)sw * CN;
+    if (INTERP == MCS_INTER_NEAREST) {
+        const int sx = sat_i16(X), sy = sat_i16(Y);
+        if ((unsigned)sx < (unsigned)sw && (unsigned)sy < (unsigned)sh) {
+            const uint2 v = load8<CN>(fb, sy * pitch + (int64_t)sx * CN, fbytes);
+#pragma unroll
+            for (int k = 0; k < CN; k++) px[k] = byte_of(v, k);
+        } else {
+#pragma unroll
+            for (int k = 0; k < CN; k++) px[k] = 0;
+        }
+        return;
+    }
+    const int sx = sat_i16(X >> 5), sy = sat_i16(Y >> 5);
+    const int fx = X & 31, fy = Y & 31;
+    // 15-bit weights of initInterTab2D: 32*(32-fx)*(32-fy) ... (sum 32768; the (0,0) entry's
+    // 32767/0/0/1 table quirk gives the same u8 result, see tests/test_oracle_known_answers.py)
+    const int w00 = (32 - fx) * (32 - fy) * 32, w01 = fx * (32 - fy) * 32;
+    const int w10 = (32 - fx) * fy * 32, w11 = fx * fy * 32;
+    if ((unsigned)sx < (unsigned)(sw - 1) && (unsigned)sy < (unsigned)(sh - 1)) {
+        const int64_t o = sy * pitch + (int64_t)sx * CN;
+        const uint2 r0 = load8<2 * CN>(fb, o, fbytes);
+        const uint2 r1 = load8<2 * CN>(fb, o + pitch, fbytes);
+#pragma unroll
+        for (int k = 0; k < CN; k++) {
+            const int s = (int)byte_of(r0, k) * w00 + (int)byte_of(r0, CN + k) * w01 +
+                          (int)byte_of(r1, k) * w10 + (int)byte_of(r1, CN + k) * w11;
+            px[k] = (uint32_t)((s + 16384) >> 15);
+        }
+    } else if (sx >= sw || sx + 1 < 0 || sy >= sh || sy + 1 < 0) {
+#pragma unroll
+        for (int k = 0; k < CN; k++) px[k] = 0;
+    } else {
+        // partial border: out-of-image taps read the border value 0
+        const bool x0ok = sx >= 0, x1ok = sx + 1 < sw, y0ok = sy >= 0, y1ok = sy + 1 < sh;
+        const uint8_t *r0 = fb + sy * pitch, *r1 = r0 + pitch;
+#pragma unroll
+        for (int k = 0; k < CN; k++) {
+            const int v0 = (x0ok && y0ok) ? r0[sx * CN + k] : 0;
+            const int v1 = (x1ok && y0ok) ? r0[(sx + 1) * CN + k] : 0;
+            const int v2 = (x0ok && y1ok) ? r1[sx * CN + k] : 0;
+            const int v3 = (x1ok && y1ok) ? r1[(sx + 1) * CN + k] : 0;
+            px[k] = (uint32_t)((v0 * w00 + v1 * w01 + v2 * w10 + v3 * w11 + 16384) >> 15);
+        }
+    }
+}
+
+// Stage that owns output pixel (x, y): the outermost stage whose paste rect does not contain
+// it (-1 = camera 0, reached through every rect).
+__device__ __forceinline__ int owner(const KParams &P, int x, int y)
+{
+    int sel = -1;
+    bool in = true;
+    for (int s = P.n_stages - 1; s >= 0; --s) {
+        const KStage &S = P.st[s];
+        const bool r = x >= S.rx0 && x < S.rx1 && y >= S.ry0 && y < S.ry1;
+        sel = (in && !r) ? s : sel;
+        in = in && r;
+    }
+    return sel;
+}
+
+template <int CN>
+__device__ __forceinline__ void put_px(uint32_t (&w)[CN], int p, const uint32_t *px)
+{
+#pragma unroll
+    for (int k = 0; k < CN; k++) {
+        const int b = p * CN + k;   // compile-time after unrolling
+        w[b >> 2] |= px[k] << (8 * (b & 3));
+    }
+}
+
+template <int CN, int INTERP>
+__device__ __forceinline__ void stitch_gather(const KParams &P)
+{
+    const int f = blockIdx.z;
+    const int xg = (blockIdx.x * kWave + threadIdx.x) * kPx;   // first pixel of this lane
+    if (xg >= P.out_w) return;
+    uint8_t *const out_f = P.out + (int64_t)f * P.out_fstride;
+    const uint8_t *cam0 = P.cams[0] + (int64_t)f * P.cam_fstride[0];
+    const int64_t cam0_bytes = (int64_t)P.cam0_w * P.cam0_h * CN;
+    const int npx = min(kPx, P.out_w - xg);
+
+    for (int r = threadIdx.y; r < kRows; r += kWavesPerBlock) {
+        const int y = blockIdx.y * kRows + r;
+        if (y >= P.out_h) break;
+        int sel[kPx];
+#pragma unroll
+        for (int p = 0; p < kPx; p++) sel[p] = owner(P, xg + p, y);
+
+        uint32_t w[CN];
+#pragma unroll
+        for (int i = 0; i < CN; i++) w[i] = 0;
+
+        // camera 0 (innermost B): pure integer translation
+#pragma unroll
+        for (int p = 0; p < kPx; p++) {
+            if (sel[p] == -1 && p < npx) {
+                const int X = xg + p + P.cam0_offx, Y = y + P.cam0_offy;
+                const uint2 v = load8<CN>(cam0, ((int64_t)Y * P.cam0_w + X) * CN, cam0_bytes);
+                uint32_t px[CN];
+#pragma unroll
+                for (int k = 0; k < CN; k++) px[k] = byte_of(v, k);
+                put_px<CN>(w, p, px);
+            }
+        }
+        // warped cameras: one exec-masked pass per stage present in the wave
+        for (int s = P.n_stages - 1; s >= 0; --s) {
+            const KStage &S = P.st[s];
+            const uint8_t *fb = P.cams[S.cam] + (int64_t)f * P.cam_fstride[S.cam];
+            const int64_t fbytes = (int64_t)S.src_w * S.src_h * CN;
+#pragma unroll
+            for (int p = 0; p < kPx; p++) {
+                if (sel[p] == s && p < npx) {
+                    int X, Y;
+                    map_exact<INTERP>(S, xg + p + S.offx, y + S.offy, X, Y);
+                    uint32_t px[CN];
+                    sample<CN, INTERP>(fb, S.src_w, S.src_h, fbytes, X, Y, px);
+                    put_px<CN>(w, p, px);
+                }
+            }
+        }
+        uint8_t *dst = out_f + (int64_t)y * P.out_pitch + (int64_t)xg * CN;
+        if (npx == kPx && (((uintptr_t)dst) & 3) == 0) {
+            uint32_t *d32 = reinterpret_cast<uint32_t *>(dst);
+#pragma unroll
+            for (int i = 0; i < CN; i++) d32[i] = w[i];
+        } else {
+            for (int b = 0; b < npx * CN; b++) dst[b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
+        }
+    }
+}
+
+// Footprint marking: sets mask[cam][pixel] = 1 for every source pixel the mosaic reads with a
+// non-zero weight; counts[cam] += number of newly marked pixels.
+template <int CN, int INTERP>
+__device__ __forceinline__ void footprint_mark(const KParams &P, uint8_t *const *masks,
+                                               unsigned long long *counts)
+{
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y;
+    if (x >= P.out_w || y >= P.out_h) return;
+    const int s = owner(P, x, y);
+    auto mark = [&](int cam, int sx, int sy, int w, int h) {
+        if ((unsigned)sx < (unsigned)w && (unsigned)sy < (unsigned)h) {
+            uint8_t *m = masks[cam] + (int64_t)sy * w + sx;
+            if (*m == 0) {
+                unsigned int *word = reinterpret_cast<unsigned int *>((uintptr_t)m & ~uintptr_t(3));
+                const unsigned int bit = 1u << (8 * ((uintptr_t)m & 3));
+                const unsigned int old = atomicOr(word, bit);
+                if (!(old & bit)) atomicAdd(&counts[cam], 1ull);
+            }
+        }
+    };
+    if (s < 0) {
+        mark(0, x + P.cam0_offx, y + P.cam0_offy, P.cam0_w, P.cam0_h);
+        return;
+    }
+    const KStage &S = P.st[s];
+    int X, Y;
+    map_exact<INTERP>(S, x + S.offx, y + S.offy, X, Y);
+    if (INTERP == MCS_INTER_NEAREST) {
+        mark(S.cam, sat_i16(X), sat_i16(Y), S.src_w, S.src_h);
+    } else {
+        const int sx = sat_i16(X >> 5), sy = sat_i16(Y >> 5), fx = X & 31, fy = Y & 31;
+        mark(S.cam, sx, sy, S.src_w, S.src_h);
+        if (fx) mark(S.cam, sx + 1, sy, S.src_w, S.src_h);
+        if (fy) mark(S.cam, sx, sy + 1, S.src_w, S.src_h);
+        if (fx && fy) mark(S.cam, sx + 1, sy + 1, S.src_w, S.src_h);
+    }
+}
+
+}  // namespace mcs
+
+// ---------------------------------------------------------------------------------------------
+// Entry points (names looked up by mcs_capi.cpp).  Block shapes: stitch (64, 4, 1) with grid
+// (ceil(out_w/256), ceil(out_h/16), frames); footprint (256, 1, 1) with grid (ceil(out_w/256), out_h).
+#define MCS_STITCH_ENTRY(CN, IN)                                                               \
+    extern "C" __global__ __launch_bounds__(256) void mcs_stitch_c##CN##_i##IN(                \
+        const mcs::KParams P)                                                                  \
+    {                                                                                          \
+        mcs::stitch_gather<CN, IN>(P);                                                         \
+    }
+MCS_STITCH_ENTRY(1, 0)
+MCS_STITCH_ENTRY(1, 1)
+MCS_STITCH_ENTRY(2, 0)
+MCS_STITCH_ENTRY(2, 1)
+MCS_STITCH_ENTRY(3, 0)
+MCS_STITCH_ENTRY(3, 1)
+MCS_STITCH_ENTRY(4, 0)
+MCS_STITCH_ENTRY(4, 1)
+
+extern "C" __global__ __launch_bounds__(256) void mcs_footprint_i0(const mcs::KParams P,
+                                                                   uint8_t *const *masks,
+                                                                   unsigned long long *counts)
+{
+    mcs::footprint_mark<1, 0>(P, masks, counts);
+}
+
+extern "C" __global__ __launch_bounds__(256) void mcs_footprint_i1(const mcs::KParams P,
+                                                                   uint8_t *const *masks,
+                                                                   unsigned long long *counts)
+{
+    mcs::footprint_mark<1, 1>(P, masks, counts);
+}

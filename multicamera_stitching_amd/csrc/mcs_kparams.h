@@ -1,0 +1,52 @@
+// mcs_kparams.h -- kernel parameter block shared by the host code (g++) and the gfx950 kernels
+// (hipcc, device-only).  Plain C++: no HIP headers.
+#pragma once
+
+#include <stdint.h>
+
+#include "mcs.h"
+
+namespace mcs {
+
+// One calibrated stage of the flattened chain (see mcs_plan.cpp).  Passed by value in the
+// kernarg segment, so every field is read with wave-uniform scalar loads.
+struct KStage {
+    double m[9];              // OpenCV-inverted stage matrix
+    int rx0, ry0, rx1, ry1;   // paste rect of B in output coords
+    int offx, offy;           // output -> canvas coords
+    int bw0;                  // OpenCV WarpPerspectiveInvoker block width
+    int bw_shift;             // log2(bw0) when bw0 is a power of two, else -1
+    int cam;                  // camera sampled by this stage
+    int src_w, src_h;         // its size
+    int pad_;
+};
+
+struct KParams {
+    int n_stages;
+    int out_w, out_h;
+    int cam0_offx, cam0_offy;
+    int cam0_w, cam0_h;
+    int pad_;
+    const uint8_t *cams[MCS_MAX_CAMS];
+    int64_t cam_fstride[MCS_MAX_CAMS];
+    uint8_t *out;
+    int64_t out_pitch;
+    int64_t out_fstride;
+    KStage st[MCS_MAX_STAGES];
+};
+
+// Kernarg block of the footprint kernel: (KParams, uint8_t* const* masks, u64* counts).
+struct KFootprintArgs {
+    KParams P;
+    uint8_t *const *masks;
+    unsigned long long *counts;
+};
+
+// Tiling of stitch_gather (must match the kernel).
+constexpr int kPx = 4;             // output pixels per lane
+constexpr int kWave = 64;
+constexpr int kWavesPerBlock = 4;
+constexpr int kRows = 16;          // rows per block
+constexpr int kTileW = kPx * kWave;
+
+}  // namespace mcs

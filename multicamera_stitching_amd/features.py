@@ -1,0 +1,67 @@
+"""Calibration-time feature matching behind StitcherBase.detectAndDescribe / matchKeypoints.
+
+Reference (StitcherClass.py:356-448): OpenCV SIFT keypoints + float descriptors, BruteForce L2
+kNN-2, Lowe ratio (strict <), more than 4 matches, findHomography(RANSAC, reprojThresh).  This
+runs once per calibration (a keypress, video_mapping_node.py:187-188), not per frame.
+
+Backends, in order: OpenCV contrib SIFT when cv2 is importable (the reference's own algorithm,
+CPU); otherwise none -- calibrate_stitcher then logs an error and returns, exactly like the
+reference without opencv-contrib (:87-93), unless the caller passes precomputed homographies.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from ._debugger import DEBUG_LEVEL_0
+
+
+def _cv2():
+    try:
+        import cv2
+        return cv2
+    except ImportError:
+        return None
+
+
+def available() -> bool:
+    cv2 = _cv2()
+    if cv2 is None:
+        return False
+    try:
+        if int(cv2.__version__.split(".")[0]) == 3:
+            cv2.xfeatures2d.SIFT_create()
+            return True
+        return hasattr(cv2, "SIFT_create") or hasattr(cv2, "FeatureDetector_create")
+    except Exception:
+        return False
+
+
+def detect_and_describe(owner, image):
+    cv2 = _cv2()
+    if cv2 is None or not available():
+        owner.debugger(DEBUG_LEVEL_0, "OpenCV is not a contrib version, check for the module "
+                       "xfeatures2d", log_type="err")
+        return None, None
+    major = int(cv2.__version__.split(".")[0])
+    if major == 3:
+        kps, features = cv2.xfeatures2d.SIFT_create().detectAndCompute(image, None)
+    elif hasattr(cv2, "SIFT_create"):
+        kps, features = cv2.SIFT_create().detectAndCompute(image, None)
+    else:
+        gray = cv2.cvtColor(image, cv2.COLOR_BGR2GRAY)
+        kps = cv2.FeatureDetector_create("SIFT").detect(gray)
+        kps, features = cv2.DescriptorExtractor_create("SIFT").compute(gray, kps)
+    return np.float32([kp.pt for kp in kps]), features
+
+
+def match_keypoints(owner, kpsA, kpsB, featuresA, featuresB, ratio=0.75, reprojThresh=4.0):
+    cv2 = _cv2()
+    raw = cv2.DescriptorMatcher_create("BruteForce").knnMatch(featuresA, featuresB, 2)
+    matches = [(m[0].trainIdx, m[0].queryIdx) for m in raw
+               if len(m) == 2 and m[0].distance < m[1].distance * ratio]
+    H = status = None
+    if len(matches) > 4:
+        ptsA = np.float32([kpsA[i] for (_, i) in matches])
+        ptsB = np.float32([kpsB[i] for (i, _) in matches])
+        H, status = cv2.findHomography(ptsA, ptsB, cv2.RANSAC, reprojThresh)
+    return H, matches, status

@@ -1,0 +1,119 @@
+"""Synthetic camera rigs for the bench and the tests.
+
+A rig is a row of cameras looking at a plane.  Camera k maps its pixels to the world plane with
+C_k = T(k*s, 0) . R(theta_k) . S(sigma_k) . P(p_k)  (s = (1 - overlap) * W), so the homography a
+perfect matcher would return for stage k of the reference chain (A = camera k+1, B = mosaic of
+cameras 0..k, StitcherClass.py:99-104) is
+    H_k = T(o_k) . C_0^-1 . C_{k+1},
+where o_k is where camera 0's origin sits in the stage-k mosaic: the sum over earlier stages of
+their paste offset Bpts[0] minus their super-mode crop origin.  No feature matching is involved
+(north-star config 2: "precomputed homographies").
+
+Frames are procedural u8 textures (sum of sinusoids + 64 px checker + noise, clipped to
+[1, 255] so that 0 always means "no camera here").
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def _T(tx, ty):
+    return np.array([[1.0, 0.0, tx], [0.0, 1.0, ty], [0.0, 0.0, 1.0]])
+
+
+def _R(theta):
+    c, s = np.cos(theta), np.sin(theta)
+    return np.array([[c, -s, 0.0], [s, c, 0.0], [0.0, 0.0, 1.0]])
+
+
+def _S(sigma):
+    return np.diag([sigma, sigma, 1.0])
+
+
+def _P(p1, p2):
+    return np.array([[1.0, 0.0, 0.0], [0.0, 1.0, 0.0], [p1, p2, 1.0]])
+
+
+def camera_models(n_cams, width, height, overlap=0.25, seed=0, rot_deg=0.5, scale_jitter=0.01,
+                  persp=2e-6, step=None):
+    """List of C_k (camera pixel -> world) for a left-to-right rig."""
+    s = (1.0 - overlap) * width if step is None else step
+    out = []
+    for k in range(n_cams):
+        rng = np.random.default_rng(1000 + seed * 97 + k)
+        th = np.deg2rad(rng.uniform(-rot_deg, rot_deg))
+        sg = 1.0 + rng.uniform(-scale_jitter, scale_jitter)
+        p1, p2 = rng.uniform(-persp, persp, size=2)
+        out.append(_T(k * s, 0.0) @ _R(th) @ _S(sg) @ _P(p1, p2))
+    return out
+
+
+def cam0_origin(prev_stages):
+    """Position of camera 0's origin in the mosaic produced by `prev_stages` (StitcherBase list)."""
+    ox, oy = 0, 0
+    for sb in prev_stages:
+        if sb.cachedAH is None:
+            continue
+        ox += int(sb.Bpts[0][0])
+        oy += int(sb.Bpts[0][1])
+        if sb.super_mode:
+            ox -= int(sb.x_limits[0])
+            oy -= int(sb.y_limits[0])
+    return ox, oy
+
+
+def stage_homography(C, k, prev_stages):
+    """A->B homography of stage k (camera k+1 onto the stage-k mosaic), H[2][2] = 1."""
+    ox, oy = cam0_origin(prev_stages)
+    H = _T(ox, oy) @ np.linalg.inv(C[0]) @ C[k + 1]
+    return H / H[2, 2]
+
+
+def homography_provider(C, chain_getter):
+    """Callable for Stitcher.calibrate_stitcher(homographies=...)."""
+    def provide(idx, stitcher_base, imageB, imageA):
+        chain = chain_getter()
+        return stage_homography(C, idx, chain[:idx])
+    return provide
+
+
+def texture(h, w, channels=3, seed=0):
+    """Procedural u8 image in [1, 255]."""
+    rng = np.random.default_rng(seed)
+    yy, xx = np.mgrid[0:h, 0:w].astype(np.float32)
+    base = np.zeros((h, w), np.float32)
+    for _ in range(8):
+        fx, fy = rng.uniform(0.002, 0.08, size=2)
+        ph = rng.uniform(0, 2 * np.pi)
+        base += np.sin(fx * xx + fy * yy + ph).astype(np.float32)
+    base = 128.0 + 12.0 * base
+    checker = (((xx // 64) + (yy // 64)) % 2).astype(np.float32) * 40.0 - 20.0
+    base += checker
+    chans = []
+    for c in range(channels):
+        noise = rng.uniform(-8, 8, size=(h, w)).astype(np.float32)
+        tint = rng.uniform(-30, 30)
+        chans.append(base + noise + tint)
+    img = np.clip(np.stack(chans, axis=-1), 1, 255).astype(np.uint8)
+    return img[..., 0] if channels == 1 else img
+
+
+def make_frames(n_cams, width, height, channels=3, seed=0):
+    return [texture(height, width, channels, seed=seed * 131 + k) for k in range(n_cams)]
+
+
+def labels(n_cams):
+    return ["CAM{}".format(i + 1) for i in range(n_cams)]
+
+
+def calibrated_stitcher(n_cams=4, width=1920, height=1080, channels=3, super_mode=False,
+                        seed=0, **cam_kw):
+    """(Stitcher, frames dict, C) for a synthetic rig, calibrated with exact homographies."""
+    from .StitcherClass import Stitcher
+    frames = make_frames(n_cams, width, height, channels, seed)
+    images = dict(zip(labels(n_cams), frames))
+    st = Stitcher(images, super_mode=super_mode)
+    C = camera_models(n_cams, width, height, seed=seed, **cam_kw)
+    st.calibrate_stitcher(images, save=False,
+                          homographies=homography_provider(C, lambda: st.stitchers))
+    return st, images, C

@@ -1,0 +1,178 @@
+"""TEST INFRASTRUCTURE ONLY -- ctypes wrapper around the CPU restatement in mcs_oracle.c.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module;
+the product path (multicamera_stitching_amd) never does.  See mcs_oracle.c for what each
+function restates (OpenCV 3.4 warpPerspective/remap/invert as called at
+PostScripts/Stitcher/StitcherClass.py:239, and the reference's cascade at :114-136/:211-256).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_SO = os.path.join(_HERE, "liboracle.so")
+_lib = None
+
+INTER_NEAREST = 0
+INTER_LINEAR = 1
+
+
+class OrcStage(ctypes.Structure):
+    _fields_ = [
+        ("H", ctypes.c_double * 9),
+        ("canvas_w", ctypes.c_int),
+        ("canvas_h", ctypes.c_int),
+        ("bx", ctypes.c_int),
+        ("by", ctypes.c_int),
+        ("super_mode", ctypes.c_int),
+        ("xl0", ctypes.c_int),
+        ("xl1", ctypes.c_int),
+        ("yl0", ctypes.c_int),
+        ("yl1", ctypes.c_int),
+    ]
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_SO):
+            build()
+        L = ctypes.CDLL(_SO)
+        P = ctypes.c_void_p
+        L.orc_invert3x3.argtypes = [P, P]
+        L.orc_invert3x3.restype = ctypes.c_int
+        L.orc_warp_perspective.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_long,
+                                           ctypes.c_int, P, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_long, P, ctypes.c_int, ctypes.c_int]
+        L.orc_cascade_out_size.argtypes = [P, ctypes.c_int, P, P]
+        L.orc_cascade_stitch.argtypes = [P, ctypes.c_int, P, P, P, ctypes.c_int, ctypes.c_int, P]
+        L.orc_flat_stitch.argtypes = [ctypes.c_int, P, P, P, P, P, P, P, P, ctypes.c_int,
+                                      ctypes.c_int, P, ctypes.c_int, ctypes.c_int]
+        L.orc_map_pixel.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                    P, P]
+        L.orc_bilinear_weights.argtypes = [ctypes.c_int, ctypes.c_int, P]
+        L.orc_num_threads.restype = ctypes.c_int
+        L.orc_set_num_threads.argtypes = [ctypes.c_int]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def set_threads(n: int):
+    lib().orc_set_num_threads(int(n))
+
+
+def num_threads() -> int:
+    return int(lib().orc_num_threads())
+
+
+def invert3x3(M) -> np.ndarray:
+    m = np.ascontiguousarray(np.asarray(M, dtype=np.float64).reshape(9))
+    out = np.zeros(9, np.float64)
+    lib().orc_invert3x3(_p(m), _p(out))
+    return out.reshape(3, 3)
+
+
+def bilinear_weights(fx: int, fy: int) -> np.ndarray:
+    w = np.zeros(4, np.int16)
+    lib().orc_bilinear_weights(int(fx), int(fy), _p(w))
+    return w
+
+
+def map_pixel(Minv, interp: int, xb: int, x1: int, y: int):
+    m = np.ascontiguousarray(np.asarray(Minv, dtype=np.float64).reshape(9))
+    X = ctypes.c_int()
+    Y = ctypes.c_int()
+    lib().orc_map_pixel(_p(m), interp, xb, x1, y, ctypes.byref(X), ctypes.byref(Y))
+    return X.value, Y.value
+
+
+def warp_perspective(src: np.ndarray, M, dsize, interp: int = INTER_LINEAR,
+                     inverse_map: bool = False) -> np.ndarray:
+    """cv2.warpPerspective(src, M, dsize=(W, H), flags=interp, BORDER_CONSTANT, 0)."""
+    src = np.ascontiguousarray(src, dtype=np.uint8)
+    cn = 1 if src.ndim == 2 else src.shape[2]
+    sh, sw = src.shape[:2]
+    W, H = int(dsize[0]), int(dsize[1])
+    dst = np.zeros((H, W, cn) if src.ndim == 3 else (H, W), np.uint8)
+    m = np.ascontiguousarray(np.asarray(M, dtype=np.float64).reshape(9))
+    lib().orc_warp_perspective(_p(src), sw, sh, sw * cn, cn, _p(dst), W, H, W * cn, _p(m),
+                               interp, 1 if inverse_map else 0)
+    return dst
+
+
+def _stage_array(stages):
+    arr = (OrcStage * len(stages))()
+    for i, s in enumerate(stages):
+        arr[i].H[:] = [float(v) for v in np.asarray(s["H"], np.float64).reshape(9)]
+        arr[i].canvas_w, arr[i].canvas_h = int(s["canvas_w"]), int(s["canvas_h"])
+        arr[i].bx, arr[i].by = int(s["bx"]), int(s["by"])
+        arr[i].super_mode = 1 if s.get("super_mode") else 0
+        xl = s.get("x_limits") or (0, 0)
+        yl = s.get("y_limits") or (0, 0)
+        arr[i].xl0, arr[i].xl1 = int(xl[0]), int(xl[1])
+        arr[i].yl0, arr[i].yl1 = int(yl[0]), int(yl[1])
+    return arr
+
+
+def cascade_stitch(stages, cams, interp: int = INTER_LINEAR) -> np.ndarray:
+    """Reference-structured cascade (per-stage full canvas warp + paste + crop).
+
+    stages: list of dicts {H, canvas_w, canvas_h, bx, by, super_mode, x_limits, y_limits}
+    cams: camera images in sorted-label order (len(stages)+1), all with the same channels.
+    """
+    n = len(stages)
+    arr = _stage_array(stages)
+    cams = [np.ascontiguousarray(c, dtype=np.uint8) for c in cams]
+    cn = 1 if cams[0].ndim == 2 else cams[0].shape[2]
+    ow = ctypes.c_int()
+    oh = ctypes.c_int()
+    L = lib()
+    if L.orc_cascade_out_size(ctypes.byref(arr), n, ctypes.byref(ow), ctypes.byref(oh)) != 0:
+        raise ValueError("no stages")
+    out = np.zeros((oh.value, ow.value, cn) if cams[0].ndim == 3 else (oh.value, ow.value),
+                   np.uint8)
+    ptrs = (ctypes.c_void_p * len(cams))(*[c.ctypes.data for c in cams])
+    cw = np.array([c.shape[1] for c in cams], np.int32)
+    ch = np.array([c.shape[0] for c in cams], np.int32)
+    rc = L.orc_cascade_stitch(ctypes.byref(arr), n, ptrs, _p(cw), _p(ch), cn, interp, _p(out))
+    if rc != 0:
+        raise ValueError("paste rectangle does not fit the canvas (numpy broadcast error)")
+    return out
+
+
+def flat_stitch(flat: dict, cams, interp: int = INTER_LINEAR) -> np.ndarray:
+    """CPU flattened gather through the nested rects (see mcs_oracle.c orc_flat_stitch).
+
+    flat: {n_stages, off_x[n+1], off_y[n+1], rect[n][4], minv[n][9], bw0[n], cam[n], out_w,
+    out_h} as returned by libmcs' mcs_plan_describe; cams: all cameras in sorted-label order.
+    """
+    n = int(flat["n_stages"])
+    offx = np.ascontiguousarray(flat["off_x"], np.int32)
+    offy = np.ascontiguousarray(flat["off_y"], np.int32)
+    rect = np.ascontiguousarray(flat["rect"], np.int32).reshape(-1)
+    minv = np.ascontiguousarray(flat["minv"], np.float64).reshape(-1)
+    bw0 = np.ascontiguousarray(flat["bw0"], np.int32)
+    cams = [np.ascontiguousarray(c, dtype=np.uint8) for c in cams]
+    # the C routine samples cams[s + 1] for stage s: reorder by the plan's camera map
+    cams = [cams[0]] + [cams[int(c)] for c in flat.get("cam", range(1, n + 1))]
+    cn = 1 if cams[0].ndim == 2 else cams[0].shape[2]
+    ow, oh = int(flat["out_w"]), int(flat["out_h"])
+    out = np.zeros((oh, ow, cn) if cams[0].ndim == 3 else (oh, ow), np.uint8)
+    ptrs = (ctypes.c_void_p * len(cams))(*[c.ctypes.data for c in cams])
+    cw = np.array([c.shape[1] for c in cams], np.int32)
+    ch = np.array([c.shape[0] for c in cams], np.int32)
+    lib().orc_flat_stitch(n, _p(offx), _p(offy), _p(rect), _p(minv), _p(bw0), ptrs, _p(cw),
+                          _p(ch), cn, interp, _p(out), ow, oh)
+    return out

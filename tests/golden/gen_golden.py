@@ -1,0 +1,224 @@
+"""Generate the golden fixtures by EXECUTING the reference's own StitcherClass.py.
+
+Container-only (needs /root/reference; the fixtures it writes are committed and travel, this
+script's inputs do not).  No reference source is copied into the repo: the file is read from
+/root/reference at generation time, compiled in memory and executed in a fresh module.
+
+What is real reference code here: Stitcher.__init__/calibrate_stitcher/stitch/save_stitcher,
+StitcherBase.calibrate/stitch/reset/params_to_*  (PostScripts/Stitcher/StitcherClass.py) and
+Utils.get_projection_point_dst (PostScripts/Calibration_Utils/Utils.py:23-37) -- i.e. the stage
+geometry (cachedAH patch, Apts/Bpts, ABSize, super-mode limits), the chain order, the paste and
+crop semantics, the passthrough branch and the pickle layout.
+
+What is substituted (the reference's third-party dependencies, absent from this image):
+  * cv2.warpPerspective -> the CPU restatement oracle/mcs_oracle.c (bilinear, BORDER_CONSTANT 0).
+    So the *pixel arithmetic* in these fixtures is our restatement of OpenCV 3.4, not OpenCV;
+    the fixtures pin the orchestration around it.
+  * SIFT / BF matcher / findHomography: detectAndDescribe and matchKeypoints are replaced so that
+    each stage receives a chosen homography (the inputs recorded in the fixture).
+  * extended_rospylogs.Debugger: a no-op logger.
+In-memory fix needed to parse under Python 3: StitcherClass.py:527 indents `def __str__` with a
+space followed by a tab (TabError); the space is dropped.  Python-2 `np.sort(dict.keys())` (:61)
+is served by a dict whose keys() returns a list.
+
+Usage:  python tests/golden/gen_golden.py   (writes tests/golden/*.npz, *.json, *.pkl)
+"""
+from __future__ import annotations
+
+import json
+import os
+import pickle
+import sys
+import types
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.path.insert(0, REPO)
+sys.dont_write_bytecode = True
+
+from oracle import oracle  # noqa: E402  (test infrastructure: the warp restatement)
+from multicamera_stitching_amd import rig  # noqa: E402  (inputs only: cameras + homographies)
+
+
+class Py2Dict(dict):
+    def keys(self):
+        return list(super().keys())
+
+
+def _install_stubs():
+    erl = types.ModuleType("extended_rospylogs")
+
+    class Debugger(object):
+        def debugger(self, level, msg, log_type="info"):
+            pass
+
+    erl.Debugger = Debugger
+    erl.update_debuggers = lambda *a, **k: None
+    erl.loginfo_cond = lambda *a, **k: None
+    erl.logerr_cond = lambda *a, **k: None
+    for i in range(5):
+        setattr(erl, "DEBUG_LEVEL_%d" % i, i)
+    sys.modules["extended_rospylogs"] = erl
+
+    cv2 = types.ModuleType("cv2")
+    cv2.__version__ = "3.4.0"
+    cv2.INTER_LINEAR = 1
+    cv2.INTER_NEAREST = 0
+    cv2.RANSAC = 8
+    cv2.COLOR_BGR2GRAY = 6
+    xf = types.SimpleNamespace(SIFT_create=lambda *a, **k: object())
+    cv2.xfeatures2d = xf
+
+    def warpPerspective(src, M, dsize, flags=1, borderMode=0, borderValue=0, dst=None):
+        return oracle.warp_perspective(src, np.asarray(M, np.float64), dsize,
+                                       interp=flags & 7 if flags is not None else 1)
+
+    def resize(*a, **k):
+        raise RuntimeError("cv2.resize reached: fixture inputs must have calibrated sizes")
+
+    cv2.warpPerspective = warpPerspective
+    cv2.resize = resize
+    sys.modules["cv2"] = cv2
+
+
+def load_reference():
+    _install_stubs()
+    sys.path.insert(0, os.path.join(REF, "PostScripts", "Calibration_Utils"))
+    import Utils  # noqa: F401  (the reference's own helper module, imported with the stub cv2)
+    path = os.path.join(REF, "PostScripts", "Stitcher", "StitcherClass.py")
+    src = open(path).read().replace(" \tdef __str__", "\tdef __str__")
+    mod = types.ModuleType("StitcherClass")
+    mod.__file__ = path
+    sys.modules["StitcherClass"] = mod
+    exec(compile(src, path, "exec"), mod.__dict__)
+    return mod
+
+
+def run_case(SC, name, frames, labels, super_mode, provider, pickle_out=None):
+    """provider(stage_index, stitcher) -> H (or None for a failed match)."""
+    images = Py2Dict(zip(labels, frames))
+    st = SC.Stitcher(images, super_mode=super_mode)
+    stage_of = {s.sid: i for i, s in enumerate(st.stitchers)}
+
+    def detectAndDescribe(self, image):
+        return np.zeros((1, 2), np.float32), np.zeros((1, 128), np.float32)
+
+    raw_H = {}
+
+    def matchKeypoints(self, kpsA, kpsB, featuresA, featuresB, ratio=0.75, reprojThresh=4.0):
+        i = stage_of[self.sid]
+        H = provider(i, st)
+        raw_H[i] = None if H is None else np.array(H, np.float64).tolist()
+        if H is None:
+            return None, [], None
+        return np.array(H, np.float64), [(0, 0)] * 8, np.ones((8, 1), np.uint8)
+
+    SC.StitcherBase.detectAndDescribe = detectAndDescribe
+    SC.StitcherBase.matchKeypoints = matchKeypoints
+    st.calibrate_stitcher(images, save=pickle_out is not None, save_path=pickle_out or "")
+    out = st.stitch(images)
+    stages = []
+    for i, s in enumerate(st.stitchers):
+        d = {"sid": s.sid, "H_in": raw_H.get(i)}
+        if s.cachedAH is None:
+            d["calibrated"] = False
+        else:
+            d.update({
+                "calibrated": True,
+                "cachedAH": np.asarray(s.cachedAH, np.float64).tolist(),
+                "cachedAINVH": np.asarray(s.cachedAINVH, np.float64).tolist(),
+                "cachedBH": np.asarray(s.cachedBH, np.float64).tolist(),
+                "ABSize": [int(v) for v in s.ABSize],
+                "Bpts": [[int(a), int(b)] for a, b in s.Bpts],
+                "Apts": [[int(a), int(b)] for a, b in s.Apts],
+                "x_limits": [int(v) for v in s.x_limits],
+                "y_limits": [int(v) for v in s.y_limits],
+                "AimgSize": list(s.AimgSize),
+                "BimgSize": list(s.BimgSize),
+            })
+        stages.append(d)
+    meta = {
+        "name": name,
+        "labels": list(labels),
+        "img_labels": [str(v) for v in st.img_labels],
+        "stitcher_labels": list(st.stitcher_labels),
+        "super_mode": bool(super_mode),
+        "stages": stages,
+        "out_shape": list(out.shape),
+        "str": [str(s) for s in st.stitchers],
+    }
+    arrays = {"cam%d" % i: f for i, f in enumerate(frames)}
+    arrays["out"] = np.ascontiguousarray(out)
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **arrays)
+    with open(os.path.join(HERE, name + ".json"), "w") as f:
+        json.dump(meta, f, indent=1)
+    print("%-28s out %s  stages %s" % (name, out.shape, [s.get("ABSize") for s in stages]))
+
+
+def rig_provider(C):
+    def provide(i, st):
+        return rig.stage_homography(C, i, st.stitchers[:i])
+    return provide
+
+
+def list_provider(Hs):
+    def provide(i, st):
+        return None if Hs[i] is None else np.array(Hs[i], np.float64)
+    return provide
+
+
+def main():
+    SC = load_reference()
+    # 1/2: mild 4-camera rig (rotation, scale, perspective) -- the C2 geometry at 96x64
+    C = rig.camera_models(4, 96, 64, seed=1, rot_deg=2.0, scale_jitter=0.03, persp=2e-4)
+    frames = rig.make_frames(4, 96, 64, 3, seed=1)
+    labs = rig.labels(4)
+    run_case(SC, "rig4_mild", frames, labs, False, rig_provider(C),
+             pickle_out=os.path.join(HERE, "rig4_mild_Stitcher_config.pkl"))
+    run_case(SC, "rig4_mild_super", frames, labs, True, rig_provider(C))
+    # 3/4: strong rotation + perspective, cameras stepping left/up (negative Ax_min)
+    C3 = rig.camera_models(3, 80, 60, seed=2, rot_deg=12.0, scale_jitter=0.1, persp=1.5e-3,
+                           step=-55.0)
+    f3 = rig.make_frames(3, 80, 60, 3, seed=2)
+    run_case(SC, "rig3_strong", f3, rig.labels(3), False, rig_provider(C3))
+    run_case(SC, "rig3_strong_super", f3, rig.labels(3), True, rig_provider(C3))
+    # 5: C1 geometry in small: integer translation (40 px)
+    f5 = rig.make_frames(2, 64, 48, 3, seed=5)
+    run_case(SC, "pair_translate", f5, ["CAM1", "CAM2"], False,
+             list_provider([[[1, 0, 40], [0, 1, 0], [0, 0, 1]]]))
+    # 6: single-channel frames (MediaPlayer passes H x W x 1 images, view.py:409)
+    C6 = rig.camera_models(3, 72, 40, seed=6, rot_deg=3.0, persp=3e-4)
+    f6 = rig.make_frames(3, 72, 40, 1, seed=6)
+    run_case(SC, "gray3", f6, rig.labels(3), False, rig_provider(C6))
+    # 7: lexicographic label order: CAM1 < CAM10 < CAM2
+    C7 = rig.camera_models(3, 48, 32, seed=7, rot_deg=1.0, persp=1e-4)
+    f7 = rig.make_frames(3, 48, 32, 3, seed=7)
+    run_case(SC, "labels_lex", f7, ["CAM2", "CAM10", "CAM1"], False, rig_provider(C7))
+    # 8: a failed match in the middle of the chain (stage 1 -> reset -> passthrough)
+    C8 = rig.camera_models(4, 64, 40, seed=8, rot_deg=1.0, persp=1e-4)
+    f8 = rig.make_frames(4, 64, 40, 3, seed=8)
+    base = rig_provider(C8)
+
+    def fail_mid(i, st):
+        if i == 1:
+            return None
+        # after the passthrough, camera 3 is matched against the (unchanged) stage-0 mosaic
+        idx = 2 if i == 2 else i
+        return rig.stage_homography(C8, idx, [s for s in st.stitchers[:i]])
+    run_case(SC, "fail_mid", f8, rig.labels(4), False, fail_mid)
+    # 9: shrinking / rotating pair with sub-pixel offsets and a large canvas
+    Hs = [[[0.93, 0.21, 37.25], [-0.18, 0.97, 12.5], [4e-4, -3e-4, 1.0]]]
+    f9 = rig.make_frames(2, 70, 50, 3, seed=9)
+    run_case(SC, "pair_affineish", f9, ["A", "B"], False, list_provider(Hs))
+    run_case(SC, "pair_affineish_super", f9, ["A", "B"], True, list_provider(Hs))
+    # 10: canvas narrower than one 64-column OpenCV block and shorter than 16 rows
+    Hs10 = [[[1.02, 0.01, 9.5], [0.0, 0.99, 1.25], [1e-3, 0.0, 1.0]]]
+    f10 = rig.make_frames(2, 20, 10, 3, seed=10)
+    run_case(SC, "tiny_blocks", f10, ["CAM1", "CAM2"], False, list_provider(Hs10))
+
+
+if __name__ == "__main__":
+    main()
