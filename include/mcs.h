@@ -105,7 +105,8 @@ int mcs_stitch_host(mcs_plan *plan, const uint8_t *const *cams, uint8_t *out);
 
 /* Device-resident batch: n_frames rigs.  d_cams[i] + f*cam_frame_stride[i] is frame f of camera
  * i (dense rows, pitch = w*C); d_out + f*out_frame_stride + y*out_pitch is output row y of frame
- * f.  Enqueued on `stream` (a hipStream_t; NULL = plan stream); does not synchronise. */
+ * f.  Enqueued on `stream` (a hipStream_t of the process's HIP runtime; NULL = the null
+ * stream); does not synchronise. */
 int mcs_stitch_device(mcs_plan *plan, const uint8_t *const *d_cams,
                       const int64_t *cam_frame_stride, uint8_t *d_out, int64_t out_pitch,
                       int64_t out_frame_stride, int n_frames, void *stream);

@@ -45,6 +45,8 @@ struct Kernels {
     hipModule_t mod = nullptr;
     hipFunction_t stitch[5][2] = {};   // [channels][interp]
     hipFunction_t footprint[2] = {};
+    hipFunction_t echo = nullptr;
+    hipFunction_t dbg = nullptr;
 };
 Kernels g_k[kMaxDevices];
 std::mutex g_k_mu;
@@ -66,6 +68,8 @@ int kernels(const Api *A, int device, const Kernels **out)
             }
         HIP_TRY(A->hipModuleGetFunction(&k.footprint[0], m, "mcs_footprint_i0"));
         HIP_TRY(A->hipModuleGetFunction(&k.footprint[1], m, "mcs_footprint_i1"));
+        HIP_TRY(A->hipModuleGetFunction(&k.echo, m, "mcs_echo_kparams"));
+        HIP_TRY(A->hipModuleGetFunction(&k.dbg, m, "mcs_debug_pixels_c3"));
         k.mod = m;
     }
     *out = &k;
@@ -288,13 +292,7 @@ int mcs_stitch_device(mcs_plan *p, const uint8_t *const *d_cams, const int64_t *
     DeviceGuard g(A, p->device);
     if (g.err != hipSuccess)
         return mcs::fail(MCS_E_HIP, "hipSetDevice(%d): %s", p->device, A->hipGetErrorString(g.err));
-    hipStream_t s = (hipStream_t)stream;
-    if (!s) {
-        int rc = ensure_stream(A, p);
-        if (rc) return rc;
-        s = p->stream;
-    }
-    return launch_stitch(A, p, kp, n_frames, s);
+    return launch_stitch(A, p, kp, n_frames, (hipStream_t)stream);
 }
 
 int mcs_plan_footprint(mcs_plan *p, int64_t *touched_px, int n_cams)
@@ -348,6 +346,79 @@ int mcs_plan_footprint(mcs_plan *p, int64_t *touched_px, int n_cams)
     if (d_counts) (void)A->hipFree(d_counts);
     if (e != hipSuccess) return mcs::fail(MCS_E_HIP, "footprint: %s", A->hipGetErrorString(e));
     for (int i = 0; i < n_cams; i++) touched_px[i] = i < n ? (int64_t)counts[i] : 0;
+    return MCS_OK;
+}
+
+// Diagnostic (not in mcs.h): the plan's KParams as the device receives them, and as the host
+// sent them, into two host buffers of mcs__kparams_size() bytes each.
+size_t mcs__kparams_size(void) { return sizeof(mcs::KParams); }
+
+int mcs__echo_kparams(mcs_plan *p, void *dev_view, void *host_view)
+{
+    const Api *A = mcs::rt::api();
+    if (!A) return MCS_E_HIP;
+    DeviceGuard g(A, p->device);
+    int rc = ensure_stream(A, p);
+    if (rc) return rc;
+    const Kernels *k = nullptr;
+    rc = kernels(A, p->device, &k);
+    if (rc) return rc;
+    struct {
+        mcs::KParams P;
+        uint8_t *out;
+    } args;
+    args.P = p->kp;
+    uint8_t *d = nullptr;
+    HIP_TRY(A->hipMalloc((void **)&d, sizeof(mcs::KParams)));
+    args.out = d;
+    size_t sz = sizeof(args);
+    void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, (void *)&args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz,
+                   HIP_LAUNCH_PARAM_END};
+    HIP_TRY(A->hipModuleLaunchKernel(k->echo, 1, 1, 1, 64, 1, 1, 0, p->stream, nullptr, cfg));
+    HIP_TRY(A->hipMemcpyAsync(dev_view, d, sizeof(mcs::KParams), hipMemcpyDeviceToHost, p->stream));
+    HIP_TRY(A->hipStreamSynchronize(p->stream));
+    (void)A->hipFree(d);
+    memcpy(host_view, &p->kp, sizeof(mcs::KParams));
+    return MCS_OK;
+}
+
+int mcs__debug_pixels(mcs_plan *p, const uint8_t *const *cams, int *host_out)
+{
+    const Api *A = mcs::rt::api();
+    if (!A) return MCS_E_HIP;
+    DeviceGuard g(A, p->device);
+    int rc = ensure_stream(A, p);
+    if (rc) return rc;
+    rc = ensure_host_buffers(A, p);
+    if (rc) return rc;
+    const Kernels *k = nullptr;
+    rc = kernels(A, p->device, &k);
+    if (rc) return rc;
+    bool need[MCS_MAX_CAMS];
+    need_mask(p->fd, need);
+    for (int i = 0; i < p->fd.n_cams; i++)
+        if (need[i])
+            HIP_TRY(A->hipMemcpyAsync(p->d_cams[i], cams[i],
+                                      (size_t)p->fd.cam_w[i] * p->fd.cam_h[i] * 3,
+                                      hipMemcpyHostToDevice, p->stream));
+    struct {
+        mcs::KParams P;
+        int *out;
+    } args;
+    args.P = p->kp;
+    for (int i = 0; i < p->fd.n_cams; i++) args.P.cams[i] = p->d_cams[i];
+    const size_t bytes = (size_t)p->fd.out_w * p->fd.out_h * 16;
+    int *d = nullptr;
+    HIP_TRY(A->hipMalloc((void **)&d, bytes));
+    args.out = d;
+    size_t sz = sizeof(args);
+    void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, (void *)&args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz,
+                   HIP_LAUNCH_PARAM_END};
+    HIP_TRY(A->hipModuleLaunchKernel(k->dbg, (p->fd.out_w + 255) / 256, p->fd.out_h, 1, 256, 1, 1,
+                                     0, p->stream, nullptr, cfg));
+    HIP_TRY(A->hipMemcpyAsync(host_out, d, bytes, hipMemcpyDeviceToHost, p->stream));
+    HIP_TRY(A->hipStreamSynchronize(p->stream));
+    (void)A->hipFree(d);
     return MCS_OK;
 }
 

@@ -75,23 +75,22 @@ __device__ __forceinline__ uint32_t byte_of(uint2 v, int i)
     return ((i < 4 ? v.x : v.y) >> (8 * (i & 3))) & 0xffu;
 }
 
-// remapBilinear / remapNearest for one pixel, BORDER_CONSTANT 0, writing CN bytes to px[].
+// remapBilinear / remapNearest for one pixel, BORDER_CONSTANT 0.  Returns the CN channel bytes
+// packed little-endian in one uint32 (byte k = channel k).  (A per-channel uint32 array here was
+// turned into <3 x i32> phis with poison lanes, which the ROCm 7.2 gfx950 backend miscompiled:
+// the fully-outside branch returned a stale register instead of 0.  One scalar avoids that.)
 template <int CN, int INTERP>
-__device__ __forceinline__ void sample(const uint8_t *fb, int sw, int sh, int64_t fbytes, int X,
-                                       int Y, uint32_t *px)
+__device__ __forceinline__ uint32_t sample(const uint8_t *fb, int sw, int sh, int64_t fbytes,
+                                           int X, int Y)
 {
     const int64_t pitch = (int64_t)sw * CN;
     if (INTERP == MCS_INTER_NEAREST) {
         const int sx = sat_i16(X), sy = sat_i16(Y);
         if ((unsigned)sx < (unsigned)sw && (unsigned)sy < (unsigned)sh) {
             const uint2 v = load8<CN>(fb, sy * pitch + (int64_t)sx * CN, fbytes);
-#pragma unroll
-            for (int k = 0; k < CN; k++) px[k] = byte_of(v, k);
-        } else {
-#pragma unroll
-            for (int k = 0; k < CN; k++) px[k] = 0;
+            return CN == 4 ? v.x : (v.x & ((1u << (8 * CN)) - 1u));
         }
-        return;
+        return 0u;
     }
     const int sx = sat_i16(X >> 5), sy = sat_i16(Y >> 5);
     const int fx = X & 31, fy = Y & 31;
@@ -99,6 +98,7 @@ __device__ __forceinline__ void sample(const uint8_t *fb, int sw, int sh, int64_
     // 32767/0/0/1 table quirk gives the same u8 result, see tests/test_oracle_known_answers.py)
     const int w00 = (32 - fx) * (32 - fy) * 32, w01 = fx * (32 - fy) * 32;
     const int w10 = (32 - fx) * fy * 32, w11 = fx * fy * 32;
+    uint32_t r = 0;
     if ((unsigned)sx < (unsigned)(sw - 1) && (unsigned)sy < (unsigned)(sh - 1)) {
         const int64_t o = sy * pitch + (int64_t)sx * CN;
         const uint2 r0 = load8<2 * CN>(fb, o, fbytes);
@@ -107,13 +107,10 @@ __device__ __forceinline__ void sample(const uint8_t *fb, int sw, int sh, int64_
         for (int k = 0; k < CN; k++) {
             const int s = (int)byte_of(r0, k) * w00 + (int)byte_of(r0, CN + k) * w01 +
                           (int)byte_of(r1, k) * w10 + (int)byte_of(r1, CN + k) * w11;
-            px[k] = (uint32_t)((s + 16384) >> 15);
+            r |= (uint32_t)((s + 16384) >> 15) << (8 * k);
         }
-    } else if (sx >= sw || sx + 1 < 0 || sy >= sh || sy + 1 < 0) {
-#pragma unroll
-        for (int k = 0; k < CN; k++) px[k] = 0;
-    } else {
-        // partial border: out-of-image taps read the border value 0
+    } else if (sx < sw && sx + 1 >= 0 && sy < sh && sy + 1 >= 0) {
+        // partial border: the taps outside the image read the border value 0
         const bool x0ok = sx >= 0, x1ok = sx + 1 < sw, y0ok = sy >= 0, y1ok = sy + 1 < sh;
         const uint8_t *r0 = fb + sy * pitch, *r1 = r0 + pitch;
 #pragma unroll
@@ -122,9 +119,10 @@ __device__ __forceinline__ void sample(const uint8_t *fb, int sw, int sh, int64_
             const int v1 = (x1ok && y0ok) ? r0[(sx + 1) * CN + k] : 0;
             const int v2 = (x0ok && y1ok) ? r1[sx * CN + k] : 0;
             const int v3 = (x1ok && y1ok) ? r1[(sx + 1) * CN + k] : 0;
-            px[k] = (uint32_t)((v0 * w00 + v1 * w01 + v2 * w10 + v3 * w11 + 16384) >> 15);
+            r |= (uint32_t)((v0 * w00 + v1 * w01 + v2 * w10 + v3 * w11 + 16384) >> 15) << (8 * k);
         }
     }
+    return r;   // all four taps outside: the border value 0
 }
 
 // Stage that owns output pixel (x, y): the outermost stage whose paste rect does not contain
@@ -142,13 +140,31 @@ __device__ __forceinline__ int owner(const KParams &P, int x, int y)
     return sel;
 }
 
+// The lane's 4*CN output bytes as four scalar words (scalars, not an array: small arrays become
+// <N x i32> vectors whose poison-lane phis the gfx950 backend has miscompiled, see sample()).
+struct OutWords {
+    uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+    __device__ __forceinline__ void or_at(int i, uint32_t v)
+    {
+        if (i == 0) w0 |= v;
+        else if (i == 1) w1 |= v;
+        else if (i == 2) w2 |= v;
+        else w3 |= v;
+    }
+    __device__ __forceinline__ uint32_t at(int i) const
+    {
+        return i == 0 ? w0 : (i == 1 ? w1 : (i == 2 ? w2 : w3));
+    }
+};
+
+// Inserts pixel p's packed bytes (channel k = byte k of v) into the lane's output words.
 template <int CN>
-__device__ __forceinline__ void put_px(uint32_t (&w)[CN], int p, const uint32_t *px)
+__device__ __forceinline__ void put_px(OutWords &w, int p, uint32_t v)
 {
 #pragma unroll
     for (int k = 0; k < CN; k++) {
         const int b = p * CN + k;   // compile-time after unrolling
-        w[b >> 2] |= px[k] << (8 * (b & 3));
+        w.or_at(b >> 2, ((v >> (8 * k)) & 0xffu) << (8 * (b & 3)));
     }
 }
 
@@ -170,9 +186,7 @@ __device__ __forceinline__ void stitch_gather(const KParams &P)
 #pragma unroll
         for (int p = 0; p < kPx; p++) sel[p] = owner(P, xg + p, y);
 
-        uint32_t w[CN];
-#pragma unroll
-        for (int i = 0; i < CN; i++) w[i] = 0;
+        OutWords w;
 
         // camera 0 (innermost B): pure integer translation
 #pragma unroll
@@ -180,10 +194,7 @@ __device__ __forceinline__ void stitch_gather(const KParams &P)
             if (sel[p] == -1 && p < npx) {
                 const int X = xg + p + P.cam0_offx, Y = y + P.cam0_offy;
                 const uint2 v = load8<CN>(cam0, ((int64_t)Y * P.cam0_w + X) * CN, cam0_bytes);
-                uint32_t px[CN];
-#pragma unroll
-                for (int k = 0; k < CN; k++) px[k] = byte_of(v, k);
-                put_px<CN>(w, p, px);
+                put_px<CN>(w, p, v.x);
             }
         }
         // warped cameras: one exec-masked pass per stage present in the wave
@@ -196,9 +207,7 @@ __device__ __forceinline__ void stitch_gather(const KParams &P)
                 if (sel[p] == s && p < npx) {
                     int X, Y;
                     map_exact<INTERP>(S, xg + p + S.offx, y + S.offy, X, Y);
-                    uint32_t px[CN];
-                    sample<CN, INTERP>(fb, S.src_w, S.src_h, fbytes, X, Y, px);
-                    put_px<CN>(w, p, px);
+                    put_px<CN>(w, p, sample<CN, INTERP>(fb, S.src_w, S.src_h, fbytes, X, Y));
                 }
             }
         }
@@ -206,9 +215,9 @@ __device__ __forceinline__ void stitch_gather(const KParams &P)
         if (npx == kPx && (((uintptr_t)dst) & 3) == 0) {
             uint32_t *d32 = reinterpret_cast<uint32_t *>(dst);
 #pragma unroll
-            for (int i = 0; i < CN; i++) d32[i] = w[i];
+            for (int i = 0; i < CN; i++) d32[i] = w.at(i);
         } else {
-            for (int b = 0; b < npx * CN; b++) dst[b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
+            for (int b = 0; b < npx * CN; b++) dst[b] = (uint8_t)(w.at(b >> 2) >> (8 * (b & 3)));
         }
     }
 }
@@ -284,4 +293,35 @@ extern "C" __global__ __launch_bounds__(256) void mcs_footprint_i1(const mcs::KP
                                                                    unsigned long long *counts)
 {
     mcs::footprint_mark<1, 1>(P, masks, counts);
+}
+
+// Diagnostic: per output pixel of frame 0, {owner stage, X, Y, packed sampled bytes}.
+extern "C" __global__ __launch_bounds__(256) void mcs_debug_pixels_c3(const mcs::KParams P,
+                                                                      int *dbg)
+{
+    using namespace mcs;
+    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
+    if (x >= P.out_w || y >= P.out_h) return;
+    const int s = owner(P, x, y);
+    int X = 0, Y = 0;
+    uint32_t v = 0;
+    if (s >= 0) {
+        const KStage &S = P.st[s];
+        map_exact<MCS_INTER_LINEAR>(S, x + S.offx, y + S.offy, X, Y);
+        v = sample<3, MCS_INTER_LINEAR>(P.cams[S.cam], S.src_w, S.src_h,
+                                        (int64_t)S.src_w * S.src_h * 3, X, Y);
+    }
+    int *d = dbg + 4 * ((int64_t)y * P.out_w + x);
+    d[0] = s;
+    d[1] = X;
+    d[2] = Y;
+    d[3] = (int)v;
+}
+
+// Diagnostic: copies the parameter block as the device sees it (kernarg transport check).
+extern "C" __global__ __launch_bounds__(64) void mcs_echo_kparams(const mcs::KParams P,
+                                                                  uint8_t *out)
+{
+    const uint8_t *src = reinterpret_cast<const uint8_t *>(&P);
+    for (int i = threadIdx.x; i < (int)sizeof(mcs::KParams); i += 64) out[i] = src[i];
 }
