@@ -120,14 +120,33 @@ int launch_stitch(const Api *A, const mcs_plan *p, const mcs::KParams &kp, int n
     const Kernels *k = nullptr;
     int rc = kernels(A, p->device, &k);
     if (rc) return rc;
-    size_t sz = sizeof(kp);
-    void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, (void *)&kp, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz,
-                   HIP_LAUNCH_PARAM_END};
+    hipFunction_t fn = k->stitch[p->fd.channels][p->fd.interp];
     const unsigned gx = (kp.out_w + mcs::kTileW - 1) / mcs::kTileW;
-    const unsigned gy = (kp.out_h + mcs::kRows - 1) / mcs::kRows;
-    HIP_TRY(A->hipModuleLaunchKernel(k->stitch[p->fd.channels][p->fd.interp], gx, gy,
-                                     (unsigned)n_frames, mcs::kWave, mcs::kWavesPerBlock, 1, 0, s,
-                                     nullptr, cfg));
+    const unsigned gy = (kp.out_h + mcs::kWavesPerBlock - 1) / mcs::kWavesPerBlock;
+    // the kernel walks the batch with one frame stride for every camera: split otherwise
+    bool uniform = true;
+    for (int j = 0; j < p->fd.n_stages; j++)
+        uniform = uniform && kp.cam_fstride[p->fd.st[j].cam] == kp.cam_fstride[0];
+    mcs::KStitchArgs args;
+    args.P = kp;
+    args.pad_ = 0;
+    size_t sz = sizeof(args);
+    void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, (void *)&args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz,
+                   HIP_LAUNCH_PARAM_END};
+    if (uniform) {
+        args.n_frames = n_frames;
+        HIP_TRY(A->hipModuleLaunchKernel(fn, gx, gy, 1, mcs::kWave, mcs::kWavesPerBlock, 1, 0, s,
+                                         nullptr, cfg));
+        return MCS_OK;
+    }
+    args.n_frames = 1;
+    for (int f = 0; f < n_frames; f++) {
+        for (int i = 0; i < p->fd.n_cams; i++)
+            args.P.cams[i] = kp.cams[i] ? kp.cams[i] + (int64_t)f * kp.cam_fstride[i] : nullptr;
+        args.P.out = kp.out + (int64_t)f * kp.out_fstride;
+        HIP_TRY(A->hipModuleLaunchKernel(fn, gx, gy, 1, mcs::kWave, mcs::kWavesPerBlock, 1, 0, s,
+                                         nullptr, cfg));
+    }
     return MCS_OK;
 }
 

@@ -168,56 +168,183 @@ __device__ __forceinline__ void put_px(OutWords &w, int p, uint32_t v)
     }
 }
 
-template <int CN, int INTERP>
-__device__ __forceinline__ void stitch_gather(const KParams &P)
+// ---------------------------------------------------------------------------------------------
+// Batched gather.  The geometry is frame-invariant (the reference re-warps every frame with the
+// same cachedAH), so each lane evaluates the exact OpenCV map of its 4 pixels ONCE per launch
+// into a compact descriptor -- a 64-bit pointer to the first tap in frame 0 plus one meta word --
+// and then streams every capture of the batch through it: per pixel and frame only two unaligned
+// 8-byte loads, the 15-bit blend and a share of one dwordx3 store remain.
+//
+// meta: bits 0-1 mode (0 border value, 1 copy CN bytes, 2 bilinear with all 4 taps inside,
+//       3 bilinear touching the border), 2-6 fx, 7-11 fy, 12-15 tap validity (mode 3:
+//       x0&y0, x1&y0, x0&y1, x1&y1), 16-17 "8-byte read of row 0 / row 1 stays inside the
+//       frame", 18-31 source width (pitch = width * CN).
+enum : uint32_t { kZero = 0, kCopy = 1, kInlier = 2, kPartial = 3 };
+
+struct PixDesc {
+    const uint8_t *ptr;
+    uint32_t meta;
+};
+
+template <int CN>
+__device__ __forceinline__ uint32_t load_px_bytes(const uint8_t *p, bool safe8)
 {
-    const int f = blockIdx.z;
-    const int xg = (blockIdx.x * kWave + threadIdx.x) * kPx;   // first pixel of this lane
-    if (xg >= P.out_w) return;
-    uint8_t *const out_f = P.out + (int64_t)f * P.out_fstride;
-    const uint8_t *cam0 = P.cams[0] + (int64_t)f * P.cam_fstride[0];
-    const int64_t cam0_bytes = (int64_t)P.cam0_w * P.cam0_h * CN;
-    const int npx = min(kPx, P.out_w - xg);
-
-    for (int r = threadIdx.y; r < kRows; r += kWavesPerBlock) {
-        const int y = blockIdx.y * kRows + r;
-        if (y >= P.out_h) break;
-        int sel[kPx];
+    // CN bytes at p (only the low CN bytes of the result are used)
+    if (safe8) {
+        uint32_t v;
+        __builtin_memcpy(&v, p, 4);
+        return v;
+    }
+    uint32_t v = 0;
 #pragma unroll
-        for (int p = 0; p < kPx; p++) sel[p] = owner(P, xg + p, y);
+    for (int k = 0; k < CN; k++) v |= (uint32_t)p[k] << (8 * k);
+    return v;
+}
 
-        OutWords w;
-
-        // camera 0 (innermost B): pure integer translation
+template <int CN>
+__device__ __forceinline__ uint2 load_pair_bytes(const uint8_t *p, bool safe8)
+{
+    // 2*CN bytes at p: one unaligned dwordx2, or byte loads at the very end of a frame
+    uint2 r;
+    if (safe8) {
+        __builtin_memcpy(&r, p, 8);
+    } else {
+        uint32_t lo = 0, hi = 0;
 #pragma unroll
-        for (int p = 0; p < kPx; p++) {
-            if (sel[p] == -1 && p < npx) {
-                const int X = xg + p + P.cam0_offx, Y = y + P.cam0_offy;
-                const uint2 v = load8<CN>(cam0, ((int64_t)Y * P.cam0_w + X) * CN, cam0_bytes);
-                put_px<CN>(w, p, v.x);
-            }
+        for (int b = 0; b < 2 * CN; b++) {
+            const uint32_t v = p[b];
+            if (b < 4) lo |= v << (8 * b);
+            else hi |= v << (8 * (b - 4));
         }
-        // warped cameras: one exec-masked pass per stage present in the wave
-        for (int s = P.n_stages - 1; s >= 0; --s) {
-            const KStage &S = P.st[s];
-            const uint8_t *fb = P.cams[S.cam] + (int64_t)f * P.cam_fstride[S.cam];
-            const int64_t fbytes = (int64_t)S.src_w * S.src_h * CN;
-#pragma unroll
-            for (int p = 0; p < kPx; p++) {
-                if (sel[p] == s && p < npx) {
-                    int X, Y;
-                    map_exact<INTERP>(S, xg + p + S.offx, y + S.offy, X, Y);
-                    put_px<CN>(w, p, sample<CN, INTERP>(fb, S.src_w, S.src_h, fbytes, X, Y));
-                }
-            }
-        }
-        uint8_t *dst = out_f + (int64_t)y * P.out_pitch + (int64_t)xg * CN;
-        if (npx == kPx && (((uintptr_t)dst) & 3) == 0) {
-            uint32_t *d32 = reinterpret_cast<uint32_t *>(dst);
-#pragma unroll
-            for (int i = 0; i < CN; i++) d32[i] = w.at(i);
+        r.x = lo;
+        r.y = hi;
+    }
+    return r;
+}
+
+// Exact OpenCV map of output pixel (x, y) -> descriptor (frame-0 pointers).
+template <int CN, int INTERP>
+__device__ __forceinline__ PixDesc describe(const KParams &P, int x, int y)
+{
+    PixDesc d;
+    const int s = owner(P, x, y);
+    if (s < 0) {
+        const int X = x + P.cam0_offx, Y = y + P.cam0_offy;
+        const int64_t o = ((int64_t)Y * P.cam0_w + X) * CN;
+        const int64_t fbytes = (int64_t)P.cam0_w * P.cam0_h * CN;
+        d.ptr = P.cams[0] + o;
+        d.meta = kCopy | ((o + 4 <= fbytes) ? (1u << 16) : 0u);
+        return d;
+    }
+    const KStage &S = P.st[s];
+    int X, Y;
+    map_exact<INTERP>(S, x + S.offx, y + S.offy, X, Y);
+    const int sw = S.src_w, sh = S.src_h;
+    const int64_t pitch = (int64_t)sw * CN, fbytes = pitch * sh;
+    const uint8_t *base = P.cams[S.cam];
+    const uint32_t wbits = (uint32_t)sw << 18;
+    if (INTERP == MCS_INTER_NEAREST) {
+        const int sx = sat_i16(X), sy = sat_i16(Y);
+        if ((unsigned)sx < (unsigned)sw && (unsigned)sy < (unsigned)sh) {
+            const int64_t o = sy * pitch + (int64_t)sx * CN;
+            d.ptr = base + o;
+            d.meta = kCopy | ((o + 4 <= fbytes) ? (1u << 16) : 0u) | wbits;
         } else {
-            for (int b = 0; b < npx * CN; b++) dst[b] = (uint8_t)(w.at(b >> 2) >> (8 * (b & 3)));
+            d.ptr = base;
+            d.meta = kZero;
+        }
+        return d;
+    }
+    const int sx = sat_i16(X >> 5), sy = sat_i16(Y >> 5);
+    const uint32_t fxy = ((uint32_t)(X & 31) << 2) | ((uint32_t)(Y & 31) << 7);
+    const int64_t o = sy * pitch + (int64_t)sx * CN;
+    d.ptr = base + o;   // may point outside the frame for mode 3; only valid taps are read
+    if ((unsigned)sx < (unsigned)(sw - 1) && (unsigned)sy < (unsigned)(sh - 1)) {
+        const uint32_t safe = ((o + 8 <= fbytes) ? (1u << 16) : 0u) |
+                              ((o + pitch + 8 <= fbytes) ? (1u << 17) : 0u);
+        d.meta = kInlier | fxy | safe | wbits;
+    } else if (sx < sw && sx + 1 >= 0 && sy < sh && sy + 1 >= 0) {
+        const bool x0 = sx >= 0, x1 = sx + 1 < sw, y0 = sy >= 0, y1 = sy + 1 < sh;
+        const uint32_t valid = ((x0 && y0) ? 1u : 0u) | ((x1 && y0) ? 2u : 0u) |
+                               ((x0 && y1) ? 4u : 0u) | ((x1 && y1) ? 8u : 0u);
+        d.meta = kPartial | fxy | (valid << 12) | wbits;
+    } else {
+        d.ptr = base;
+        d.meta = kZero;
+    }
+    return d;
+}
+
+// One pixel of one frame: CN channel bytes packed in a uint32.
+template <int CN>
+__device__ __forceinline__ uint32_t fetch(const uint8_t *p, uint32_t meta)
+{
+    const uint32_t mode = meta & 3u;
+    if (mode == kZero) return 0u;
+    if (mode == kCopy) {
+        const uint32_t v = load_px_bytes<CN>(p, (meta >> 16) & 1u);
+        return CN == 4 ? v : (v & ((1u << (8 * CN)) - 1u));
+    }
+    const int fx = (meta >> 2) & 31, fy = (meta >> 7) & 31;
+    const int w00 = (32 - fx) * (32 - fy) * 32, w01 = fx * (32 - fy) * 32;
+    const int w10 = (32 - fx) * fy * 32, w11 = fx * fy * 32;
+    const int64_t pitch = (int64_t)(meta >> 18) * CN;
+    uint32_t r = 0;
+    if (mode == kInlier) {
+        const uint2 r0 = load_pair_bytes<CN>(p, (meta >> 16) & 1u);
+        const uint2 r1 = load_pair_bytes<CN>(p + pitch, (meta >> 17) & 1u);
+#pragma unroll
+        for (int k = 0; k < CN; k++) {
+            const int s = (int)byte_of(r0, k) * w00 + (int)byte_of(r0, CN + k) * w01 +
+                          (int)byte_of(r1, k) * w10 + (int)byte_of(r1, CN + k) * w11;
+            r |= (uint32_t)((s + 16384) >> 15) << (8 * k);
+        }
+        return r;
+    }
+    // kPartial: taps outside the image read the border value 0
+    const uint32_t valid = (meta >> 12) & 15u;
+#pragma unroll
+    for (int k = 0; k < CN; k++) {
+        const int v0 = (valid & 1u) ? p[k] : 0;
+        const int v1 = (valid & 2u) ? p[CN + k] : 0;
+        const int v2 = (valid & 4u) ? p[pitch + k] : 0;
+        const int v3 = (valid & 8u) ? p[pitch + CN + k] : 0;
+        r |= (uint32_t)((v0 * w00 + v1 * w01 + v2 * w10 + v3 * w11 + 16384) >> 15) << (8 * k);
+    }
+    return r;
+}
+
+// grid (ceil(out_w / 256), ceil(out_h / 4)), block (64, 4): lane = 4 consecutive pixels of one
+// row; the whole batch of `n_frames` captures is walked inside the block.  All cameras share one
+// frame stride (P.cam_fstride[0]); the host splits batches that do not.
+template <int CN, int INTERP>
+__device__ __forceinline__ void stitch_batched(const KParams &P, int n_frames)
+{
+    const int xg = (blockIdx.x * kWave + threadIdx.x) * kPx;
+    const int y = blockIdx.y * kWavesPerBlock + threadIdx.y;
+    if (xg >= P.out_w || y >= P.out_h) return;
+    const int npx = min(kPx, P.out_w - xg);
+    PixDesc d[kPx];
+#pragma unroll
+    for (int p = 0; p < kPx; p++) {
+        d[p] = describe<CN, INTERP>(P, min(xg + p, P.out_w - 1), y);
+        if (p >= npx) d[p].meta = kZero;
+    }
+    const int64_t fstride = P.cam_fstride[0];
+    uint8_t *dst = P.out + (int64_t)y * P.out_pitch + (int64_t)xg * CN;
+    const bool wide = npx == kPx && (((uintptr_t)dst | (uintptr_t)P.out_fstride) & 3) == 0;
+    for (int f = 0; f < n_frames; f++) {
+        const int64_t so = (int64_t)f * fstride;
+        OutWords w;
+#pragma unroll
+        for (int p = 0; p < kPx; p++) put_px<CN>(w, p, fetch<CN>(d[p].ptr + so, d[p].meta));
+        uint8_t *o = dst + (int64_t)f * P.out_fstride;
+        if (wide) {
+            uint32_t *o32 = reinterpret_cast<uint32_t *>(o);
+#pragma unroll
+            for (int i = 0; i < CN; i++) o32[i] = w.at(i);
+        } else {
+            for (int b = 0; b < npx * CN; b++) o[b] = (uint8_t)(w.at(b >> 2) >> (8 * (b & 3)));
         }
     }
 }
@@ -265,12 +392,12 @@ __device__ __forceinline__ void footprint_mark(const KParams &P, uint8_t *const 
 
 // ---------------------------------------------------------------------------------------------
 // Entry points (names looked up by mcs_capi.cpp).  Block shapes: stitch (64, 4, 1) with grid
-// (ceil(out_w/256), ceil(out_h/16), frames); footprint (256, 1, 1) with grid (ceil(out_w/256), out_h).
+// (ceil(out_w/256), ceil(out_h/4)); footprint (256, 1, 1) with grid (ceil(out_w/256), out_h).
 #define MCS_STITCH_ENTRY(CN, IN)                                                               \
     extern "C" __global__ __launch_bounds__(256) void mcs_stitch_c##CN##_i##IN(                \
-        const mcs::KParams P)                                                                  \
+        const mcs::KParams P, int n_frames)                                                    \
     {                                                                                          \
-        mcs::stitch_gather<CN, IN>(P);                                                         \
+        mcs::stitch_batched<CN, IN>(P, n_frames);                                              \
     }
 MCS_STITCH_ENTRY(1, 0)
 MCS_STITCH_ENTRY(1, 1)

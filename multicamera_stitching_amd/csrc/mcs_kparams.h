@@ -42,11 +42,17 @@ struct KFootprintArgs {
     unsigned long long *counts;
 };
 
-// Tiling of stitch_gather (must match the kernel).
+// Kernarg block of the stitch kernels: (KParams, int n_frames).
+struct KStitchArgs {
+    KParams P;
+    int n_frames;
+    int pad_;
+};
+
+// Tiling of stitch_batched (must match the kernel): a block is 256 px x 4 rows.
 constexpr int kPx = 4;             // output pixels per lane
 constexpr int kWave = 64;
-constexpr int kWavesPerBlock = 4;
-constexpr int kRows = 16;          // rows per block
+constexpr int kWavesPerBlock = 4;  // one row per wave
 constexpr int kTileW = kPx * kWave;
 
 }  // namespace mcs
