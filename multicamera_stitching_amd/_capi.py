@@ -159,6 +159,8 @@ def load() -> ctypes.CDLL:
         L.mcs_stitch_device.restype = I
         L.mcs_plan_footprint.argtypes = [P, ctypes.POINTER(ctypes.c_int64), I]
         L.mcs_plan_footprint.restype = I
+        L.mcs__force_off64.argtypes = [I]   # test hook (not part of mcs.h)
+        L.mcs__force_off64.restype = None
         if L.mcs_abi_version() != ABI_VERSION:
             raise ImportError(f"libmcs ABI {L.mcs_abi_version()} != expected {ABI_VERSION}")
         _lib = L

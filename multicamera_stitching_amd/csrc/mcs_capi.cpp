@@ -43,7 +43,7 @@ constexpr int kMaxDevices = 64;
 
 struct Kernels {
     hipModule_t mod = nullptr;
-    hipFunction_t stitch[5][2] = {};   // [channels][interp]
+    hipFunction_t stitch[5][2][2] = {};   // [channels][interp][32-bit offsets]
     hipFunction_t footprint[2] = {};
     hipFunction_t echo = nullptr;
     hipFunction_t dbg = nullptr;
@@ -62,10 +62,11 @@ int kernels(const Api *A, int device, const Kernels **out)
         HIP_TRY(A->hipModuleLoadData(&m, mcs_hsaco_start));
         char name[64];
         for (int c = 1; c <= 4; c++)
-            for (int i = 0; i < 2; i++) {
-                snprintf(name, sizeof(name), "mcs_stitch_c%d_i%d", c, i);
-                HIP_TRY(A->hipModuleGetFunction(&k.stitch[c][i], m, name));
-            }
+            for (int i = 0; i < 2; i++)
+                for (int o = 0; o < 2; o++) {
+                    snprintf(name, sizeof(name), "mcs_stitch_c%d_i%d_o%d", c, i, o ? 32 : 64);
+                    HIP_TRY(A->hipModuleGetFunction(&k.stitch[c][i][o], m, name));
+                }
         HIP_TRY(A->hipModuleGetFunction(&k.footprint[0], m, "mcs_footprint_i0"));
         HIP_TRY(A->hipModuleGetFunction(&k.footprint[1], m, "mcs_footprint_i1"));
         HIP_TRY(A->hipModuleGetFunction(&k.echo, m, "mcs_echo_kparams"));
@@ -113,6 +114,34 @@ int ensure_host_buffers(const Api *A, mcs_plan *p)
     return MCS_OK;
 }
 
+void need_mask(const mcs_flat_desc &fd, bool *need)
+{
+    for (int i = 0; i < MCS_MAX_CAMS; i++) need[i] = false;
+    need[0] = true;
+    for (int j = 0; j < fd.n_stages; j++) need[fd.st[j].cam] = true;
+}
+
+// Lowest used camera address for frame 0 of `kp`, and whether every used byte of that frame lies
+// within 4 GiB above it (then the kernel addresses taps as SGPR base + 32-bit offsets).
+int g_force_off64 = 0;   // test hook: exercise the 64-bit-address kernels
+
+bool offset_base(const mcs_plan *p, const mcs::KParams &kp, const uint8_t **base)
+{
+    bool need[MCS_MAX_CAMS];
+    need_mask(p->fd, need);
+    uintptr_t lo = UINTPTR_MAX, hi = 0;
+    for (int i = 0; i < p->fd.n_cams; i++) {
+        if (!need[i]) continue;
+        const uintptr_t a = (uintptr_t)kp.cams[i];
+        const uintptr_t e = a + (uintptr_t)p->fd.cam_w[i] * p->fd.cam_h[i] * p->fd.channels;
+        lo = a < lo ? a : lo;
+        hi = e > hi ? e : hi;
+    }
+    const bool off32 = !g_force_off64 && hi - lo < (uintptr_t(1) << 32);
+    *base = off32 ? (const uint8_t *)lo : nullptr;
+    return off32;
+}
+
 int launch_stitch(const Api *A, const mcs_plan *p, const mcs::KParams &kp, int n_frames,
                   hipStream_t s)
 {
@@ -120,7 +149,6 @@ int launch_stitch(const Api *A, const mcs_plan *p, const mcs::KParams &kp, int n
     const Kernels *k = nullptr;
     int rc = kernels(A, p->device, &k);
     if (rc) return rc;
-    hipFunction_t fn = k->stitch[p->fd.channels][p->fd.interp];
     const unsigned gx = (kp.out_w + mcs::kTileW - 1) / mcs::kTileW;
     const unsigned gy = (kp.out_h + mcs::kWavesPerBlock - 1) / mcs::kWavesPerBlock;
     // the kernel walks the batch with one frame stride for every camera: split otherwise
@@ -133,8 +161,11 @@ int launch_stitch(const Api *A, const mcs_plan *p, const mcs::KParams &kp, int n
     size_t sz = sizeof(args);
     void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, (void *)&args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz,
                    HIP_LAUNCH_PARAM_END};
+    const int C = p->fd.channels, I = p->fd.interp;
     if (uniform) {
         args.n_frames = n_frames;
+        const bool off32 = offset_base(p, args.P, &args.P.base);
+        hipFunction_t fn = k->stitch[C][I][off32 ? 1 : 0];
         HIP_TRY(A->hipModuleLaunchKernel(fn, gx, gy, 1, mcs::kWave, mcs::kWavesPerBlock, 1, 0, s,
                                          nullptr, cfg));
         return MCS_OK;
@@ -144,17 +175,12 @@ int launch_stitch(const Api *A, const mcs_plan *p, const mcs::KParams &kp, int n
         for (int i = 0; i < p->fd.n_cams; i++)
             args.P.cams[i] = kp.cams[i] ? kp.cams[i] + (int64_t)f * kp.cam_fstride[i] : nullptr;
         args.P.out = kp.out + (int64_t)f * kp.out_fstride;
+        const bool off32 = offset_base(p, args.P, &args.P.base);
+        hipFunction_t fn = k->stitch[C][I][off32 ? 1 : 0];
         HIP_TRY(A->hipModuleLaunchKernel(fn, gx, gy, 1, mcs::kWave, mcs::kWavesPerBlock, 1, 0, s,
                                          nullptr, cfg));
     }
     return MCS_OK;
-}
-
-void need_mask(const mcs_flat_desc &fd, bool *need)
-{
-    for (int i = 0; i < MCS_MAX_CAMS; i++) need[i] = false;
-    need[0] = true;
-    for (int j = 0; j < fd.n_stages; j++) need[fd.st[j].cam] = true;
 }
 
 }  // namespace
@@ -367,6 +393,9 @@ int mcs_plan_footprint(mcs_plan *p, int64_t *touched_px, int n_cams)
     for (int i = 0; i < n_cams; i++) touched_px[i] = i < n ? (int64_t)counts[i] : 0;
     return MCS_OK;
 }
+
+// Test hook (not in mcs.h): force the 64-bit-address kernel variants.
+void mcs__force_off64(int on) { g_force_off64 = on; }
 
 // Diagnostic (not in mcs.h): the plan's KParams as the device receives them, and as the host
 // sent them, into two host buffers of mcs__kparams_size() bytes each.

@@ -16,6 +16,8 @@
 // SSE2/SSE4.1 x86 code.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "mcs_kparams.h"
 
 namespace mcs {
@@ -171,173 +173,170 @@ __device__ __forceinline__ void put_px(OutWords &w, int p, uint32_t v)
 // ---------------------------------------------------------------------------------------------
 // Batched gather.  The geometry is frame-invariant (the reference re-warps every frame with the
 // same cachedAH), so each lane evaluates the exact OpenCV map of its 4 pixels ONCE per launch
-// into a compact descriptor -- a 64-bit pointer to the first tap in frame 0 plus one meta word --
-// and then streams every capture of the batch through it: per pixel and frame only two unaligned
-// 8-byte loads, the 15-bit blend and a share of one dwordx3 store remain.
+// into a compact descriptor and then streams every capture of the batch through it.
 //
-// meta: bits 0-1 mode (0 border value, 1 copy CN bytes, 2 bilinear with all 4 taps inside,
-//       3 bilinear touching the border), 2-6 fx, 7-11 fy, 12-15 tap validity (mode 3:
-//       x0&y0, x1&y0, x0&y1, x1&y1), 16-17 "8-byte read of row 0 / row 1 stays inside the
-//       frame", 18-31 source width (pitch = width * CN).
-enum : uint32_t { kZero = 0, kCopy = 1, kInlier = 2, kPartial = 3 };
-
-struct PixDesc {
-    const uint8_t *ptr;
-    uint32_t meta;
+// Every pixel -- bilinear inside the image, bilinear on its border, a paste copy, a nearest
+// sample, or outside everything -- is expressed in ONE form: two row windows of 2*CN bytes
+// (row 0 at off0, row 1 at off1) and 15-bit weights packed as u16 pairs W0 = (w00, w01),
+// W1 = (w10, w11), so that per channel k
+//     out_k = dot2(row1_k, W1, dot2(row0_k, W0, 16384)) >> 15            (v_dot2_u32_u16)
+// which is remapBilinear's sum(p * w) + 2^14 >> 15 exactly.  A copy is W0 = (32768, 0),
+// W1 = 0; a pixel outside every camera has W0 = W1 = 0; taps outside the image get weight 0
+// and their window is moved onto valid bytes (so nothing outside a frame is ever read, see
+// place_window()).  No per-pixel branching remains in the frame loop except the rare
+// "window would end past the frame" case (last pixels of a frame), flagged in `slow`.
+template <bool OFF32>
+struct Desc {
+    typedef typename std::conditional<OFF32, uint32_t, uint64_t>::type off_t;
+    off_t off0, off1;      // window byte offsets from the launch base (or absolute addresses)
+    uint32_t w0, w1;       // packed u16 weight pairs (w00, w01), (w10, w11)
+    uint32_t shift;        // bits 0-3 / 4-7: bytes row 0 / row 1 were moved left to end in-frame
 };
 
-template <int CN>
-__device__ __forceinline__ uint32_t load_px_bytes(const uint8_t *p, bool safe8)
+// Column placement of one row's tap pair (sx, sx+1) with weights (wl, wr): returns the window's
+// first column cx (the window covers cx, cx+1) and the weights as seen from the window.
+__device__ __forceinline__ int place_cols(int sx, int sw, uint32_t wl, uint32_t wr, uint32_t &wa,
+                                          uint32_t &wb)
 {
-    // CN bytes at p (only the low CN bytes of the result are used)
-    if (safe8) {
-        uint32_t v;
-        __builtin_memcpy(&v, p, 4);
-        return v;
+    const bool l_in = sx >= 0 && sx < sw, r_in = sx + 1 >= 0 && sx + 1 < sw;
+    if (l_in && r_in) {
+        wa = wl;
+        wb = wr;
+        return sx;
     }
-    uint32_t v = 0;
-#pragma unroll
-    for (int k = 0; k < CN; k++) v |= (uint32_t)p[k] << (8 * k);
-    return v;
-}
-
-template <int CN>
-__device__ __forceinline__ uint2 load_pair_bytes(const uint8_t *p, bool safe8)
-{
-    // 2*CN bytes at p: one unaligned dwordx2, or byte loads at the very end of a frame
-    uint2 r;
-    if (safe8) {
-        __builtin_memcpy(&r, p, 8);
-    } else {
-        uint32_t lo = 0, hi = 0;
-#pragma unroll
-        for (int b = 0; b < 2 * CN; b++) {
-            const uint32_t v = p[b];
-            if (b < 4) lo |= v << (8 * b);
-            else hi |= v << (8 * (b - 4));
+    if (l_in) {                  // sx = sw - 1: its right neighbour is outside the image
+        if (sw >= 2) {
+            wa = 0u;
+            wb = wl;
+            return sx - 1;
         }
-        r.x = lo;
-        r.y = hi;
+        wa = wl;
+        wb = 0u;
+        return sx;
     }
-    return r;
+    if (r_in) {                  // sx = -1: only column 0 contributes
+        wa = wr;
+        wb = 0u;
+        return 0;
+    }
+    wa = wb = 0u;                // both taps outside: weight 0, any in-image window
+    return 0;
 }
 
-// Exact OpenCV map of output pixel (x, y) -> descriptor (frame-0 pointers).
-template <int CN, int INTERP>
-__device__ __forceinline__ PixDesc describe(const KParams &P, int x, int y)
+template <int CN, int INTERP, bool OFF32>
+__device__ __forceinline__ Desc<OFF32> describe(const KParams &P, int x, int y)
 {
-    PixDesc d;
+    Desc<OFF32> d;
     const int s = owner(P, x, y);
-    if (s < 0) {
-        const int X = x + P.cam0_offx, Y = y + P.cam0_offy;
-        const int64_t o = ((int64_t)Y * P.cam0_w + X) * CN;
-        const int64_t fbytes = (int64_t)P.cam0_w * P.cam0_h * CN;
-        d.ptr = P.cams[0] + o;
-        d.meta = kCopy | ((o + 4 <= fbytes) ? (1u << 16) : 0u);
-        return d;
-    }
-    const KStage &S = P.st[s];
-    int X, Y;
-    map_exact<INTERP>(S, x + S.offx, y + S.offy, X, Y);
-    const int sw = S.src_w, sh = S.src_h;
-    const int64_t pitch = (int64_t)sw * CN, fbytes = pitch * sh;
-    const uint8_t *base = P.cams[S.cam];
-    const uint32_t wbits = (uint32_t)sw << 18;
-    if (INTERP == MCS_INTER_NEAREST) {
-        const int sx = sat_i16(X), sy = sat_i16(Y);
-        if ((unsigned)sx < (unsigned)sw && (unsigned)sy < (unsigned)sh) {
-            const int64_t o = sy * pitch + (int64_t)sx * CN;
-            d.ptr = base + o;
-            d.meta = kCopy | ((o + 4 <= fbytes) ? (1u << 16) : 0u) | wbits;
-        } else {
-            d.ptr = base;
-            d.meta = kZero;
-        }
-        return d;
-    }
-    const int sx = sat_i16(X >> 5), sy = sat_i16(Y >> 5);
-    const uint32_t fxy = ((uint32_t)(X & 31) << 2) | ((uint32_t)(Y & 31) << 7);
-    const int64_t o = sy * pitch + (int64_t)sx * CN;
-    d.ptr = base + o;   // may point outside the frame for mode 3; only valid taps are read
-    if ((unsigned)sx < (unsigned)(sw - 1) && (unsigned)sy < (unsigned)(sh - 1)) {
-        const uint32_t safe = ((o + 8 <= fbytes) ? (1u << 16) : 0u) |
-                              ((o + pitch + 8 <= fbytes) ? (1u << 17) : 0u);
-        d.meta = kInlier | fxy | safe | wbits;
-    } else if (sx < sw && sx + 1 >= 0 && sy < sh && sy + 1 >= 0) {
-        const bool x0 = sx >= 0, x1 = sx + 1 < sw, y0 = sy >= 0, y1 = sy + 1 < sh;
-        const uint32_t valid = ((x0 && y0) ? 1u : 0u) | ((x1 && y0) ? 2u : 0u) |
-                               ((x0 && y1) ? 4u : 0u) | ((x1 && y1) ? 8u : 0u);
-        d.meta = kPartial | fxy | (valid << 12) | wbits;
+    int cam, sw, sh, X, Y;
+    if (s < 0) {                 // camera 0 pasted whole: a copy (weights 32768, 0, 0, 0)
+        cam = 0;
+        sw = P.cam0_w;
+        sh = P.cam0_h;
+        X = (x + P.cam0_offx) << 5;
+        Y = (y + P.cam0_offy) << 5;
     } else {
-        d.ptr = base;
-        d.meta = kZero;
+        const KStage &S = P.st[s];
+        cam = S.cam;
+        sw = S.src_w;
+        sh = S.src_h;
+        map_exact<INTERP>(S, x + S.offx, y + S.offy, X, Y);
+        if (INTERP == MCS_INTER_NEAREST) {   // remapNearest: a copy of (X, Y) or the border value
+            X = sat_i16(X);
+            Y = sat_i16(Y);
+            const bool in = (unsigned)X < (unsigned)sw && (unsigned)Y < (unsigned)sh;
+            X = in ? X * 32 : -(1 << 20);
+            Y = in ? Y * 32 : -(1 << 20);
+        }
     }
+    const int64_t pitch = (int64_t)sw * CN, fbytes = pitch * sh;
+    const int sx = sat_i16(X >> 5), sy = sat_i16(Y >> 5), fx = X & 31, fy = Y & 31;
+    const uint32_t w00 = (32 - fx) * (32 - fy) * 32, w01 = fx * (32 - fy) * 32;
+    const uint32_t w10 = (32 - fx) * fy * 32, w11 = fx * fy * 32;
+    const bool y0_in = sy >= 0 && sy < sh, y1_in = sy + 1 >= 0 && sy + 1 < sh;
+    uint32_t a0, b0, a1, b1;
+    const int c0 = place_cols(sx, sw, y0_in ? w00 : 0u, y0_in ? w01 : 0u, a0, b0);
+    const int c1 = place_cols(sx, sw, y1_in ? w10 : 0u, y1_in ? w11 : 0u, a1, b1);
+    int64_t o0 = (int64_t)(y0_in ? sy : 0) * pitch + (int64_t)c0 * CN;
+    int64_t o1 = (int64_t)(y1_in ? sy + 1 : 0) * pitch + (int64_t)c1 * CN;
+    // an 8-byte window must end inside the frame: move it left, remember by how much
+    const int64_t sh0 = o0 + 8 > fbytes ? o0 + 8 - fbytes : 0;
+    const int64_t sh1 = o1 + 8 > fbytes ? o1 + 8 - fbytes : 0;
+    const uint64_t cam_off = (uint64_t)(uintptr_t)P.cams[cam] - (uint64_t)(uintptr_t)P.base;
+    d.off0 = (typename Desc<OFF32>::off_t)(cam_off + (uint64_t)(o0 - sh0));
+    d.off1 = (typename Desc<OFF32>::off_t)(cam_off + (uint64_t)(o1 - sh1));
+    d.w0 = a0 | (b0 << 16);
+    d.w1 = a1 | (b1 << 16);
+    d.shift = (uint32_t)sh0 | ((uint32_t)sh1 << 4);
     return d;
 }
 
-// One pixel of one frame: CN channel bytes packed in a uint32.
+// Channel k of a pixel from its two row windows: v_perm_b32 + 2 x v_dot2_u32_u16.
 template <int CN>
-__device__ __forceinline__ uint32_t fetch(const uint8_t *p, uint32_t meta)
+__device__ __forceinline__ uint32_t blend(uint2 r0, uint2 r1, uint32_t w0, uint32_t w1, int k)
 {
-    const uint32_t mode = meta & 3u;
-    if (mode == kZero) return 0u;
-    if (mode == kCopy) {
-        const uint32_t v = load_px_bytes<CN>(p, (meta >> 16) & 1u);
-        return CN == 4 ? v : (v & ((1u << (8 * CN)) - 1u));
-    }
-    const int fx = (meta >> 2) & 31, fy = (meta >> 7) & 31;
-    const int w00 = (32 - fx) * (32 - fy) * 32, w01 = fx * (32 - fy) * 32;
-    const int w10 = (32 - fx) * fy * 32, w11 = fx * fy * 32;
-    const int64_t pitch = (int64_t)(meta >> 18) * CN;
-    uint32_t r = 0;
-    if (mode == kInlier) {
-        const uint2 r0 = load_pair_bytes<CN>(p, (meta >> 16) & 1u);
-        const uint2 r1 = load_pair_bytes<CN>(p + pitch, (meta >> 17) & 1u);
-#pragma unroll
-        for (int k = 0; k < CN; k++) {
-            const int s = (int)byte_of(r0, k) * w00 + (int)byte_of(r0, CN + k) * w01 +
-                          (int)byte_of(r1, k) * w10 + (int)byte_of(r1, CN + k) * w11;
-            r |= (uint32_t)((s + 16384) >> 15) << (8 * k);
-        }
-        return r;
-    }
-    // kPartial: taps outside the image read the border value 0
-    const uint32_t valid = (meta >> 12) & 15u;
-#pragma unroll
-    for (int k = 0; k < CN; k++) {
-        const int v0 = (valid & 1u) ? p[k] : 0;
-        const int v1 = (valid & 2u) ? p[CN + k] : 0;
-        const int v2 = (valid & 4u) ? p[pitch + k] : 0;
-        const int v3 = (valid & 8u) ? p[pitch + CN + k] : 0;
-        r |= (uint32_t)((v0 * w00 + v1 * w01 + v2 * w10 + v3 * w11 + 16384) >> 15) << (8 * k);
-    }
-    return r;
+    typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+    const uint32_t sel = (uint32_t)k | (0x0cu << 8) | ((uint32_t)(CN + k) << 16) | (0x0cu << 24);
+    const uint32_t a0 = __builtin_amdgcn_perm(r0.y, r0.x, sel);
+    const uint32_t a1 = __builtin_amdgcn_perm(r1.y, r1.x, sel);
+    uint32_t s = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, a0), __builtin_bit_cast(us2, w0),
+                                        16384u, false);
+    s = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, a1), __builtin_bit_cast(us2, w1), s, false);
+    return s >> 15;
+}
+
+__device__ __forceinline__ uint2 shr_bytes(uint2 v, uint32_t n)
+{
+    uint64_t t;
+    __builtin_memcpy(&t, &v, 8);
+    t >>= 8 * n;
+    __builtin_memcpy(&v, &t, 8);
+    return v;
 }
 
 // grid (ceil(out_w / 256), ceil(out_h / 4)), block (64, 4): lane = 4 consecutive pixels of one
-// row; the whole batch of `n_frames` captures is walked inside the block.  All cameras share one
-// frame stride (P.cam_fstride[0]); the host splits batches that do not.
-template <int CN, int INTERP>
+// row; the block walks all `n_frames` captures.  All cameras share one frame stride
+// (P.cam_fstride[0]); the host splits batches that do not.
+template <int CN, int INTERP, bool OFF32>
 __device__ __forceinline__ void stitch_batched(const KParams &P, int n_frames)
 {
     const int xg = (blockIdx.x * kWave + threadIdx.x) * kPx;
     const int y = blockIdx.y * kWavesPerBlock + threadIdx.y;
     if (xg >= P.out_w || y >= P.out_h) return;
     const int npx = min(kPx, P.out_w - xg);
-    PixDesc d[kPx];
+    Desc<OFF32> d[kPx];
+    uint32_t any_shift = 0;
 #pragma unroll
     for (int p = 0; p < kPx; p++) {
-        d[p] = describe<CN, INTERP>(P, min(xg + p, P.out_w - 1), y);
-        if (p >= npx) d[p].meta = kZero;
+        d[p] = describe<CN, INTERP, OFF32>(P, min(xg + p, P.out_w - 1), y);
+        any_shift |= d[p].shift;
     }
     const int64_t fstride = P.cam_fstride[0];
     uint8_t *dst = P.out + (int64_t)y * P.out_pitch + (int64_t)xg * CN;
     const bool wide = npx == kPx && (((uintptr_t)dst | (uintptr_t)P.out_fstride) & 3) == 0;
     for (int f = 0; f < n_frames; f++) {
-        const int64_t so = (int64_t)f * fstride;
+        const uint8_t *bf = P.base + (int64_t)f * fstride;
+        uint2 r0[kPx], r1[kPx];
+#pragma unroll
+        for (int p = 0; p < kPx; p++) {
+            __builtin_memcpy(&r0[p], bf + d[p].off0, 8);
+            __builtin_memcpy(&r1[p], bf + d[p].off1, 8);
+        }
+        if (any_shift) {         // windows moved left at a frame's end (last pixels only)
+#pragma unroll
+            for (int p = 0; p < kPx; p++) {
+                r0[p] = shr_bytes(r0[p], d[p].shift & 15u);
+                r1[p] = shr_bytes(r1[p], d[p].shift >> 4);
+            }
+        }
         OutWords w;
 #pragma unroll
-        for (int p = 0; p < kPx; p++) put_px<CN>(w, p, fetch<CN>(d[p].ptr + so, d[p].meta));
+        for (int p = 0; p < kPx; p++)
+#pragma unroll
+            for (int k = 0; k < CN; k++) {
+                const int b = p * CN + k;
+                w.or_at(b >> 2, blend<CN>(r0[p], r1[p], d[p].w0, d[p].w1, k) << (8 * (b & 3)));
+            }
         uint8_t *o = dst + (int64_t)f * P.out_fstride;
         if (wide) {
             uint32_t *o32 = reinterpret_cast<uint32_t *>(o);
@@ -393,20 +392,21 @@ __device__ __forceinline__ void footprint_mark(const KParams &P, uint8_t *const 
 // ---------------------------------------------------------------------------------------------
 // Entry points (names looked up by mcs_capi.cpp).  Block shapes: stitch (64, 4, 1) with grid
 // (ceil(out_w/256), ceil(out_h/4)); footprint (256, 1, 1) with grid (ceil(out_w/256), out_h).
-#define MCS_STITCH_ENTRY(CN, IN)                                                               \
-    extern "C" __global__ __launch_bounds__(256) void mcs_stitch_c##CN##_i##IN(                \
+#define MCS_STITCH_ENTRY(CN, IN, O32)                                                          \
+    extern "C" __global__ __launch_bounds__(256) void mcs_stitch_c##CN##_i##IN##_o##O32(       \
         const mcs::KParams P, int n_frames)                                                    \
     {                                                                                          \
-        mcs::stitch_batched<CN, IN>(P, n_frames);                                              \
+        mcs::stitch_batched<CN, IN, O32 == 32>(P, n_frames);                                   \
     }
-MCS_STITCH_ENTRY(1, 0)
-MCS_STITCH_ENTRY(1, 1)
-MCS_STITCH_ENTRY(2, 0)
-MCS_STITCH_ENTRY(2, 1)
-MCS_STITCH_ENTRY(3, 0)
-MCS_STITCH_ENTRY(3, 1)
-MCS_STITCH_ENTRY(4, 0)
-MCS_STITCH_ENTRY(4, 1)
+#define MCS_STITCH_ENTRIES(CN)                                                                 \
+    MCS_STITCH_ENTRY(CN, 0, 32)                                                                \
+    MCS_STITCH_ENTRY(CN, 1, 32)                                                                \
+    MCS_STITCH_ENTRY(CN, 0, 64)                                                                \
+    MCS_STITCH_ENTRY(CN, 1, 64)
+MCS_STITCH_ENTRIES(1)
+MCS_STITCH_ENTRIES(2)
+MCS_STITCH_ENTRIES(3)
+MCS_STITCH_ENTRIES(4)
 
 extern "C" __global__ __launch_bounds__(256) void mcs_footprint_i0(const mcs::KParams P,
                                                                    uint8_t *const *masks,

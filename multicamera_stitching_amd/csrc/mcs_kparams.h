@@ -32,6 +32,10 @@ struct KParams {
     uint8_t *out;
     int64_t out_pitch;
     int64_t out_fstride;
+    // Common base of the used camera buffers: when every byte of frame 0 of every used camera
+    // lies in [base, base + 4 GiB), pixels address their taps as base + f*fstride + u32 offset
+    // (SGPR base, VGPR offset); otherwise base is NULL and offsets are full 64-bit addresses.
+    const uint8_t *base;
     KStage st[MCS_MAX_STAGES];
 };
 

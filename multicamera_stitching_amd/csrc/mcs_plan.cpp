@@ -92,6 +92,9 @@ int build_flat(const mcs_stage_desc *stages, int n_stages, int cam0_w, int cam0_
     if (interp != MCS_INTER_LINEAR && interp != MCS_INTER_NEAREST)
         return fail(MCS_E_INVALID, "interp=%d", interp);
     if (cam0_w < 1 || cam0_h < 1) return fail(MCS_E_SHAPE, "camera 0 size %dx%d", cam0_w, cam0_h);
+    if ((long)cam0_w * cam0_h * channels < 8)
+        return fail(MCS_E_UNSUPPORTED, "camera 0 frame of %ld bytes (< 8)",
+                    (long)cam0_w * cam0_h * channels);
 
     memset(fd, 0, sizeof(*fd));
     fd->channels = channels;
@@ -112,6 +115,9 @@ int build_flat(const mcs_stage_desc *stages, int n_stages, int cam0_w, int cam0_
         if (!s.calibrated) continue;   // StitcherClass.py:255-256: returns B unchanged
         if (s.a_w < 1 || s.a_h < 1)
             return fail(MCS_E_SHAPE, "stage %d: A size %dx%d", k, s.a_w, s.a_h);
+        if ((long)s.a_w * s.a_h * channels < 8)
+            return fail(MCS_E_UNSUPPORTED, "stage %d: camera frame of %ld bytes (< 8)", k,
+                        (long)s.a_w * s.a_h * channels);
         if (s.b_w != bw || s.b_h != bh)
             return fail(MCS_E_SHAPE,
                         "stage %d: calibrated B size %dx%d != chain size %ldx%ld (the reference "

@@ -140,3 +140,58 @@ def test_footprint_counts():
     assert fp[0] == 320 * 180          # camera 0 is pasted whole (no super crop)
     for i in range(1, 4):
         assert 0 < fp[i] <= 320 * 180
+
+
+def _batch(plan, cams, F, seed, pad=None):
+    """Device batch of F captures per camera; pad[i] extra bytes between frames of camera i."""
+    import torch
+    from multicamera_stitching_amd import rig
+    frames = [[rig.texture(c.shape[0], c.shape[1], c.shape[2] if c.ndim == 3 else 1,
+                           seed=seed + 100 * f + i) for i, c in enumerate(cams)]
+              for f in range(F)]
+    dev, strides = [], []
+    for i, c in enumerate(cams):
+        n = c.size + (pad[i] if pad else 0)
+        buf = torch.zeros((F, n), dtype=torch.uint8)
+        for f in range(F):
+            buf[f, :c.size] = torch.from_numpy(np.ascontiguousarray(frames[f][i]).reshape(-1))
+        dev.append(buf.cuda())
+        strides.append(n)
+    return frames, dev, strides
+
+
+@pytest.mark.parametrize("force64", [False, True])
+@pytest.mark.parametrize("pad", [None, [0, 64, 0, 4096]])
+def test_batch_address_modes_and_mixed_strides(force64, pad):
+    """32-bit-offset and 64-bit-address kernels; uniform and per-camera frame strides (the
+    latter is split into per-frame launches) -- all equal to the per-frame host path."""
+    import ctypes
+    import torch
+    from multicamera_stitching_amd import _capi
+    L = _capi.load()
+    plan, cams, _ = _rig_plan(4, 200, 120, 3, False, seed=7, interp=1, rot_deg=4.0, persp=1e-4)
+    F = 3
+    frames, dev, strides = _batch(plan, cams, F, seed=11, pad=pad)
+    pitch = plan.out_w * 3 + 4
+    out = torch.full((F, plan.out_h, pitch), 9, dtype=torch.uint8, device="cuda")
+    L.mcs__force_off64(ctypes.c_int(1 if force64 else 0))
+    try:
+        plan.stitch_device([d.data_ptr() for d in dev], strides, out.data_ptr(), pitch,
+                           out[0].numel(), F, 0)
+        torch.cuda.synchronize()
+    finally:
+        L.mcs__force_off64(ctypes.c_int(0))
+    got = out.cpu().numpy()
+    for f in range(F):
+        want = plan.stitch_host(frames[f])
+        assert _diff(got[f, :, :plan.out_w * 3].reshape(plan.out_h, plan.out_w, 3), want) == 0
+        assert (got[f, :, plan.out_w * 3:] == 9).all()
+
+
+@pytest.mark.parametrize("ch", [1, 2, 4])
+def test_channel_counts_vs_oracle(ch):
+    plan, cams, stages = _rig_plan(3, 150, 90, ch, False, seed=9, interp=1, rot_deg=5.0,
+                                   persp=2e-4)
+    want = oracle.cascade_stitch(stages, cams, oracle.INTER_LINEAR)
+    got = plan.stitch_host(cams)
+    assert _diff(got.reshape(want.shape), want) == 0
