@@ -150,7 +150,7 @@ int launch_stitch(const Api *A, const mcs_plan *p, const mcs::KParams &kp, int n
     int rc = kernels(A, p->device, &k);
     if (rc) return rc;
     const unsigned gx = (kp.out_w + mcs::kTileW - 1) / mcs::kTileW;
-    const unsigned gy = (kp.out_h + mcs::kWavesPerBlock - 1) / mcs::kWavesPerBlock;
+    const unsigned gy = (kp.out_h + mcs::kTileH - 1) / mcs::kTileH;
     // the kernel walks the batch with one frame stride for every camera: split otherwise
     bool uniform = true;
     for (int j = 0; j < p->fd.n_stages; j++)
@@ -166,8 +166,8 @@ int launch_stitch(const Api *A, const mcs_plan *p, const mcs::KParams &kp, int n
         args.n_frames = n_frames;
         const bool off32 = offset_base(p, args.P, &args.P.base);
         hipFunction_t fn = k->stitch[C][I][off32 ? 1 : 0];
-        HIP_TRY(A->hipModuleLaunchKernel(fn, gx, gy, 1, mcs::kWave, mcs::kWavesPerBlock, 1, 0, s,
-                                         nullptr, cfg));
+        HIP_TRY(A->hipModuleLaunchKernel(fn, gx, gy, 1, mcs::kWave, mcs::kWavesPerBlock, 1,
+                                         mcs::kLdsBytes, s, nullptr, cfg));
         return MCS_OK;
     }
     args.n_frames = 1;
@@ -177,8 +177,8 @@ int launch_stitch(const Api *A, const mcs_plan *p, const mcs::KParams &kp, int n
         args.P.out = kp.out + (int64_t)f * kp.out_fstride;
         const bool off32 = offset_base(p, args.P, &args.P.base);
         hipFunction_t fn = k->stitch[C][I][off32 ? 1 : 0];
-        HIP_TRY(A->hipModuleLaunchKernel(fn, gx, gy, 1, mcs::kWave, mcs::kWavesPerBlock, 1, 0, s,
-                                         nullptr, cfg));
+        HIP_TRY(A->hipModuleLaunchKernel(fn, gx, gy, 1, mcs::kWave, mcs::kWavesPerBlock, 1,
+                                         mcs::kLdsBytes, s, nullptr, cfg));
     }
     return MCS_OK;
 }

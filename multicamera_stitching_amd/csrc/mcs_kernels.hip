@@ -223,21 +223,28 @@ __device__ __forceinline__ int place_cols(int sx, int sw, uint32_t wl, uint32_t 
     return 0;
 }
 
-template <int CN, int INTERP, bool OFF32>
-__device__ __forceinline__ Desc<OFF32> describe(const KParams &P, int x, int y)
+// Geometry of one output pixel: the camera it samples, its two row windows (in-image row and
+// byte column of each window's first tap) and the packed u16 weight pairs seen from them.
+struct Geo {
+    int cam, r0, c0, r1, c1;
+    uint32_t w0, w1;
+};
+
+template <int CN, int INTERP>
+__device__ __forceinline__ Geo describe_geo(const KParams &P, int x, int y)
 {
-    Desc<OFF32> d;
+    Geo g;
     const int s = owner(P, x, y);
-    int cam, sw, sh, X, Y;
+    int sw, sh, X, Y;
     if (s < 0) {                 // camera 0 pasted whole: a copy (weights 32768, 0, 0, 0)
-        cam = 0;
+        g.cam = 0;
         sw = P.cam0_w;
         sh = P.cam0_h;
         X = (x + P.cam0_offx) << 5;
         Y = (y + P.cam0_offy) << 5;
     } else {
         const KStage &S = P.st[s];
-        cam = S.cam;
+        g.cam = S.cam;
         sw = S.src_w;
         sh = S.src_h;
         map_exact<INTERP>(S, x + S.offx, y + S.offy, X, Y);
@@ -249,24 +256,44 @@ __device__ __forceinline__ Desc<OFF32> describe(const KParams &P, int x, int y)
             Y = in ? Y * 32 : -(1 << 20);
         }
     }
-    const int64_t pitch = (int64_t)sw * CN, fbytes = pitch * sh;
     const int sx = sat_i16(X >> 5), sy = sat_i16(Y >> 5), fx = X & 31, fy = Y & 31;
     const uint32_t w00 = (32 - fx) * (32 - fy) * 32, w01 = fx * (32 - fy) * 32;
     const uint32_t w10 = (32 - fx) * fy * 32, w11 = fx * fy * 32;
     const bool y0_in = sy >= 0 && sy < sh, y1_in = sy + 1 >= 0 && sy + 1 < sh;
     uint32_t a0, b0, a1, b1;
-    const int c0 = place_cols(sx, sw, y0_in ? w00 : 0u, y0_in ? w01 : 0u, a0, b0);
-    const int c1 = place_cols(sx, sw, y1_in ? w10 : 0u, y1_in ? w11 : 0u, a1, b1);
-    int64_t o0 = (int64_t)(y0_in ? sy : 0) * pitch + (int64_t)c0 * CN;
-    int64_t o1 = (int64_t)(y1_in ? sy + 1 : 0) * pitch + (int64_t)c1 * CN;
+    g.c0 = place_cols(sx, sw, y0_in ? w00 : 0u, y0_in ? w01 : 0u, a0, b0) * CN;
+    g.c1 = place_cols(sx, sw, y1_in ? w10 : 0u, y1_in ? w11 : 0u, a1, b1) * CN;
+    g.r0 = y0_in ? sy : 0;
+    g.r1 = y1_in ? sy + 1 : 0;
+    g.w0 = a0 | (b0 << 16);
+    g.w1 = a1 | (b1 << 16);
+    if (g.w0 == 0u) {            // no live tap in row 0: reuse row 1's window
+        g.r0 = g.r1;
+        g.c0 = g.c1;
+    }
+    if (g.w1 == 0u) {
+        g.r1 = g.r0;
+        g.c1 = g.c0;
+    }
+    return g;
+}
+
+// Global-gather form of a pixel (tiles whose footprint does not fit the LDS budget).
+template <int CN, int INTERP, bool OFF32>
+__device__ __forceinline__ Desc<OFF32> describe(const KParams &P, int x, int y)
+{
+    const Geo g = describe_geo<CN, INTERP>(P, x, y);
+    Desc<OFF32> d;
+    const int64_t pitch = (int64_t)P.cam_w[g.cam] * CN, fbytes = pitch * P.cam_h[g.cam];
+    const int64_t o0 = (int64_t)g.r0 * pitch + g.c0, o1 = (int64_t)g.r1 * pitch + g.c1;
     // an 8-byte window must end inside the frame: move it left, remember by how much
     const int64_t sh0 = o0 + 8 > fbytes ? o0 + 8 - fbytes : 0;
     const int64_t sh1 = o1 + 8 > fbytes ? o1 + 8 - fbytes : 0;
-    const uint64_t cam_off = (uint64_t)(uintptr_t)P.cams[cam] - (uint64_t)(uintptr_t)P.base;
+    const uint64_t cam_off = (uint64_t)(uintptr_t)P.cams[g.cam] - (uint64_t)(uintptr_t)P.base;
     d.off0 = (typename Desc<OFF32>::off_t)(cam_off + (uint64_t)(o0 - sh0));
     d.off1 = (typename Desc<OFF32>::off_t)(cam_off + (uint64_t)(o1 - sh1));
-    d.w0 = a0 | (b0 << 16);
-    d.w1 = a1 | (b1 << 16);
+    d.w0 = g.w0;
+    d.w1 = g.w1;
     d.shift = (uint32_t)sh0 | ((uint32_t)sh1 << 4);
     return d;
 }
@@ -294,15 +321,11 @@ __device__ __forceinline__ uint2 shr_bytes(uint2 v, uint32_t n)
     return v;
 }
 
-// grid (ceil(out_w / 256), ceil(out_h / 4)), block (64, 4): lane = 4 consecutive pixels of one
-// row; the block walks all `n_frames` captures.  All cameras share one frame stride
-// (P.cam_fstride[0]); the host splits batches that do not.
+// Direct global-gather path for the 4 pixels at (xg, y): descriptors once, then every capture
+// (frame stride P.cam_fstride[0] for all cameras; the host splits batches that differ).
 template <int CN, int INTERP, bool OFF32>
-__device__ __forceinline__ void stitch_batched(const KParams &P, int n_frames)
+__device__ __forceinline__ void stitch_direct(const KParams &P, int n_frames, int xg, int y)
 {
-    const int xg = (blockIdx.x * kWave + threadIdx.x) * kPx;
-    const int y = blockIdx.y * kWavesPerBlock + threadIdx.y;
-    if (xg >= P.out_w || y >= P.out_h) return;
     const int npx = min(kPx, P.out_w - xg);
     Desc<OFF32> d[kPx];
     uint32_t any_shift = 0;
@@ -348,6 +371,197 @@ __device__ __forceinline__ void stitch_batched(const KParams &P, int n_frames)
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// LDS-staged gather (the main path).  Per launch, every block (256 x 8 output pixels, 8 waves)
+// evaluates its pixels' exact maps, reduces them to one source footprint per camera (rows x
+// 16-byte chunks, the union of all its row windows) and lays the footprints out in LDS.  Per
+// capture, each footprint row is ONE global_load_lds_dwordx4 wave instruction (LDS-DMA: wide,
+// contiguous, no registers), double-buffered across captures; pixels then read their 8-byte
+// windows from LDS with aligned ds_read2_b32 + ds_read_b32 and v_alignbyte.  Blocks whose
+// footprint exceeds kLdsBuf (steep perspective, 3+ cameras in one tile) take the direct path.
+struct LdsHeader {
+    int rmin[MCS_MAX_CAMS], rmax[MCS_MAX_CAMS], cmin[MCS_MAX_CAMS], cmax[MCS_MAX_CAMS];
+    int base[MCS_MAX_CAMS], stride[MCS_MAX_CAMS], cal[MCS_MAX_CAMS];
+    int jobstart[MCS_MAX_CAMS + 1];
+    int fits, njobs;
+};
+static_assert(sizeof(LdsHeader) <= kLdsHeader, "LDS header");
+
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+__device__ __forceinline__ uint2 lds_window(const uint8_t *smem, uint32_t a)
+{
+    const lds_u32 *d = (const lds_u32 *)(((const lds_u8 *)smem) + (a & ~3u));
+    const uint32_t sh = a & 3u;
+    const uint32_t x0 = d[0], x1 = d[1], x2 = d[2];
+    uint2 r;
+    r.x = __builtin_amdgcn_alignbyte(x1, x0, sh);
+    r.y = __builtin_amdgcn_alignbyte(x2, x1, sh);
+    return r;
+}
+
+// Issues the LDS-DMA loads of capture f's footprint rows into buffer `buf` (rows split over the
+// block's waves; lanes = 16-byte chunks of a row).  Chunks that would cross the end of a camera
+// frame are copied byte by byte instead (only the bytes inside the frame).
+template <int CN>
+__device__ __forceinline__ void stage_capture(const KParams &P, const LdsHeader *h, uint8_t *buf,
+                                              int f, int lane, int wave)
+{
+    const int njobs = h->njobs;
+    for (int j = wave; j < njobs; j += kWavesPerBlock) {
+        int c = 0;
+        while (j >= h->jobstart[c + 1]) c++;
+        c = __builtin_amdgcn_readfirstlane(c);
+        const int row = j - h->jobstart[c];
+        const int stride = __builtin_amdgcn_readfirstlane(h->stride[c]);
+        const int64_t pitch = (int64_t)P.cam_w[c] * CN;
+        const int64_t fbytes = pitch * P.cam_h[c];
+        const int64_t goff = (int64_t)(h->rmin[c] + row) * pitch + h->cal[c] + 16 * lane;
+        const uint8_t *src = P.cams[c] + (int64_t)f * P.cam_fstride[0];
+        const uint32_t lds_row = (uint32_t)(h->base[c] + row * stride);
+        lds_u8 *dst = ((lds_u8 *)buf) + __builtin_amdgcn_readfirstlane(lds_row);
+        if (16 * lane < stride) {
+            if (goff + 16 <= fbytes) {
+                __builtin_amdgcn_global_load_lds(src + goff, dst, 16, 0, 0);
+            } else {
+                for (int b = 0; b < 16; b++)
+                    if (goff + b < fbytes) dst[16 * lane + b] = src[goff + b];
+            }
+        }
+    }
+}
+
+template <int CN, int INTERP, bool OFF32>
+__device__ __forceinline__ void stitch_lds(const KParams &P, int n_frames, uint8_t *smem)
+{
+    const int lane = threadIdx.x, wave = threadIdx.y;
+    const int tid = wave * kWave + lane;
+    const int xg = (blockIdx.x * kWave + lane) * kPx;
+    const int y = blockIdx.y * kTileH + wave;
+    const bool live = xg < P.out_w && y < P.out_h;
+    const int npx = live ? min(kPx, P.out_w - xg) : 0;
+    LdsHeader *h = reinterpret_cast<LdsHeader *>(smem);
+    if (tid < MCS_MAX_CAMS) {
+        h->rmin[tid] = 0x7fffffff;
+        h->rmax[tid] = -0x7fffffff;
+        h->cmin[tid] = 0x7fffffff;
+        h->cmax[tid] = -0x7fffffff;
+    }
+    __syncthreads();
+
+    // 1. exact map of this lane's pixels, then the per-camera footprint of the block
+    Geo g[kPx];
+#pragma unroll
+    for (int p = 0; p < kPx; p++) {
+        g[p] = describe_geo<CN, INTERP>(P, min(xg + p, P.out_w - 1), min(y, P.out_h - 1));
+        if (p >= npx) g[p].w0 = g[p].w1 = 0u;
+    }
+    {
+        int cam = -1, rmin = 0x7fffffff, rmax = -0x7fffffff, cmin = 0x7fffffff, cmax = -0x7fffffff;
+#pragma unroll
+        for (int p = 0; p < kPx; p++) {
+            if ((g[p].w0 | g[p].w1) == 0u) continue;
+            if (cam < 0) cam = g[p].cam;
+            const int r_lo = min(g[p].r0, g[p].r1), r_hi = max(g[p].r0, g[p].r1);
+            const int c_lo = min(g[p].c0, g[p].c1), c_hi = max(g[p].c0, g[p].c1);
+            if (g[p].cam == cam) {
+                rmin = min(rmin, r_lo);
+                rmax = max(rmax, r_hi);
+                cmin = min(cmin, c_lo);
+                cmax = max(cmax, c_hi);
+            } else {
+                atomicMin(&h->rmin[g[p].cam], r_lo);
+                atomicMax(&h->rmax[g[p].cam], r_hi);
+                atomicMin(&h->cmin[g[p].cam], c_lo);
+                atomicMax(&h->cmax[g[p].cam], c_hi);
+            }
+        }
+        if (cam >= 0) {
+            atomicMin(&h->rmin[cam], rmin);
+            atomicMax(&h->rmax[cam], rmax);
+            atomicMin(&h->cmin[cam], cmin);
+            atomicMax(&h->cmax[cam], cmax);
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int total = 0, jobs = 0, fits = 1;
+        for (int c = 0; c < MCS_MAX_CAMS; c++) {
+            h->jobstart[c] = jobs;
+            if (h->rmin[c] > h->rmax[c]) continue;
+            const int cal = h->cmin[c] & ~15;
+            const int stride = (h->cmax[c] + 8 - cal + 15) & ~15;
+            const int rows = h->rmax[c] - h->rmin[c] + 1;
+            h->cal[c] = cal;
+            h->stride[c] = stride;
+            h->base[c] = total;
+            total += rows * stride;
+            jobs += rows;
+            if (stride > 16 * kWave) fits = 0;
+        }
+        h->jobstart[MCS_MAX_CAMS] = jobs;
+        h->njobs = jobs;
+        h->fits = fits && total <= kLdsBuf;
+    }
+    __syncthreads();
+    if (!h->fits) {              // block-uniform: footprint too large for the LDS budget
+        if (live) stitch_direct<CN, INTERP, OFF32>(P, n_frames, xg, y);
+        return;
+    }
+
+    // 2. LDS window addresses of every pixel (buffer-relative)
+    uint32_t win[kPx], w0[kPx], w1[kPx];
+#pragma unroll
+    for (int p = 0; p < kPx; p++) {
+        const int c = g[p].cam;
+        const int st = h->stride[c], rm = h->rmin[c], ca = h->cal[c], bs = h->base[c];
+        uint32_t a0 = (uint32_t)(bs + (g[p].r0 - rm) * st + (g[p].c0 - ca));
+        uint32_t a1 = (uint32_t)(bs + (g[p].r1 - rm) * st + (g[p].c1 - ca));
+        if ((g[p].w0 | g[p].w1) == 0u) a0 = a1 = 0u;
+        win[p] = a0 | (a1 << 16);
+        w0[p] = g[p].w0;
+        w1[p] = g[p].w1;
+    }
+
+    uint8_t *bufs[2] = {smem + kLdsHeader, smem + kLdsHeader + kLdsBuf + kLdsSlack};
+    uint8_t *dst = P.out + (int64_t)min(y, P.out_h - 1) * P.out_pitch + (int64_t)xg * CN;
+    const bool wide = npx == kPx && (((uintptr_t)dst | (uintptr_t)P.out_fstride) & 3) == 0;
+
+    // 3. stream the captures: DMA(f+1) || gather(f), one barrier per capture
+    stage_capture<CN>(P, h, bufs[0], 0, lane, wave);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int f = 0; f < n_frames; f++) {
+        if (f + 1 < n_frames) stage_capture<CN>(P, h, bufs[(f + 1) & 1], f + 1, lane, wave);
+        const uint8_t *b = bufs[f & 1];
+        if (live) {
+            OutWords w;
+#pragma unroll
+            for (int p = 0; p < kPx; p++) {
+                const uint2 r0 = lds_window(b, win[p] & 0xffffu);
+                const uint2 r1 = lds_window(b, win[p] >> 16);
+#pragma unroll
+                for (int k = 0; k < CN; k++) {
+                    const int bb = p * CN + k;
+                    w.or_at(bb >> 2, blend<CN>(r0, r1, w0[p], w1[p], k) << (8 * (bb & 3)));
+                }
+            }
+            uint8_t *o = dst + (int64_t)f * P.out_fstride;
+            if (wide) {
+                uint32_t *o32 = reinterpret_cast<uint32_t *>(o);
+#pragma unroll
+                for (int i = 0; i < CN; i++) o32[i] = w.at(i);
+            } else {
+                for (int bb = 0; bb < npx * CN; bb++)
+                    o[bb] = (uint8_t)(w.at(bb >> 2) >> (8 * (bb & 3)));
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+}
+
 // Footprint marking: sets mask[cam][pixel] = 1 for every source pixel the mosaic reads with a
 // non-zero weight; counts[cam] += number of newly marked pixels.
 template <int CN, int INTERP>
@@ -390,13 +604,15 @@ __device__ __forceinline__ void footprint_mark(const KParams &P, uint8_t *const 
 }  // namespace mcs
 
 // ---------------------------------------------------------------------------------------------
-// Entry points (names looked up by mcs_capi.cpp).  Block shapes: stitch (64, 4, 1) with grid
-// (ceil(out_w/256), ceil(out_h/4)); footprint (256, 1, 1) with grid (ceil(out_w/256), out_h).
+// Entry points (names looked up by mcs_capi.cpp).  Block shapes: stitch (64, 8, 1) with grid
+// (ceil(out_w/256), ceil(out_h/8)) and kLdsBytes of dynamic LDS; footprint (256, 1, 1) with grid
+// (ceil(out_w/256), out_h).
 #define MCS_STITCH_ENTRY(CN, IN, O32)                                                          \
-    extern "C" __global__ __launch_bounds__(256) void mcs_stitch_c##CN##_i##IN##_o##O32(       \
+    extern "C" __global__ __launch_bounds__(512) void mcs_stitch_c##CN##_i##IN##_o##O32(       \
         const mcs::KParams P, int n_frames)                                                    \
     {                                                                                          \
-        mcs::stitch_batched<CN, IN, O32 == 32>(P, n_frames);                                   \
+        extern __shared__ __attribute__((aligned(16))) uint8_t smem[];                         \
+        mcs::stitch_lds<CN, IN, O32 == 32>(P, n_frames, smem);                                 \
     }
 #define MCS_STITCH_ENTRIES(CN)                                                                 \
     MCS_STITCH_ENTRY(CN, 0, 32)                                                                \

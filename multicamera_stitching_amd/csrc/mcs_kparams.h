@@ -36,6 +36,7 @@ struct KParams {
     // lies in [base, base + 4 GiB), pixels address their taps as base + f*fstride + u32 offset
     // (SGPR base, VGPR offset); otherwise base is NULL and offsets are full 64-bit addresses.
     const uint8_t *base;
+    int cam_w[MCS_MAX_CAMS], cam_h[MCS_MAX_CAMS];   // sizes of every camera (sorted-label order)
     KStage st[MCS_MAX_STAGES];
 };
 
@@ -53,10 +54,18 @@ struct KStitchArgs {
     int pad_;
 };
 
-// Tiling of stitch_batched (must match the kernel): a block is 256 px x 4 rows.
+// Tiling of the stitch kernel (must match the kernel): a block is 256 px x 8 rows, one row per
+// wave, 4 consecutive pixels per lane.
 constexpr int kPx = 4;             // output pixels per lane
 constexpr int kWave = 64;
-constexpr int kWavesPerBlock = 4;  // one row per wave
+constexpr int kWavesPerBlock = 8;  // one row per wave
 constexpr int kTileW = kPx * kWave;
+constexpr int kTileH = kWavesPerBlock;
+
+// LDS of one block: a header (per-camera footprint and layout) and two staging buffers.
+constexpr int kLdsHeader = 1024;
+constexpr int kLdsBuf = 19456;     // bytes of source footprint one capture may occupy
+constexpr int kLdsSlack = 16;      // window reads run up to 8 bytes past a row's last byte
+constexpr int kLdsBytes = kLdsHeader + 2 * (kLdsBuf + kLdsSlack);
 
 }  // namespace mcs

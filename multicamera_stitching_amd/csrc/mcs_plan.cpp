@@ -189,6 +189,10 @@ void fill_kparams(const mcs_flat_desc &fd, KParams *kp)
     kp->cam0_offy = fd.cam0_off_y;
     kp->cam0_w = fd.cam_w[0];
     kp->cam0_h = fd.cam_h[0];
+    for (int i = 0; i < fd.n_cams; i++) {
+        kp->cam_w[i] = fd.cam_w[i];
+        kp->cam_h[i] = fd.cam_h[i];
+    }
     for (int j = 0; j < fd.n_stages; j++) {
         const mcs_flat_stage &s = fd.st[j];
         KStage &k = kp->st[j];
