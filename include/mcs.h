@@ -98,6 +98,16 @@ int mcs_plan_destroy(mcs_plan *plan);
 int mcs_plan_out_shape(const mcs_plan *plan, int *w, int *h, int *channels);
 int mcs_plan_describe(const mcs_plan *plan, mcs_flat_desc *out);
 
+/* Evaluates the plan's exact OpenCV coordinate map once on its device and stores it as per-tile
+ * LDS layouts + per-pixel window descriptors (the fixed-point remap tables of this plan; OpenCV's
+ * own remap path uses the same idea, cv::convertMaps).  Allocates device memory and
+ * synchronises: call it before capturing stitch calls into a HIP graph.  The stitch entry points
+ * call it on first use.  stream: hipStream_t or NULL for the plan's own stream. */
+int mcs_plan_prepare(mcs_plan *plan, void *stream);
+
+/* stats[0..4] = prepared, tiles, tiles on the LDS path, tiles on the direct path, table bytes. */
+int mcs_plan_stats(const mcs_plan *plan, int64_t *stats, int n);
+
 /* Stitcher.stitch on host arrays (drop-in path, :114-136): cams[i] is the i-th camera in
  * sorted-label order, dense HxWxC u8 of the calibrated size; out is a dense out_h x out_w x C
  * buffer.  Synchronous: H2D -> kernel -> D2H on the plan's stream. */

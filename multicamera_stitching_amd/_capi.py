@@ -30,7 +30,8 @@ ABI_VERSION = 1
 EXPORTS = (
     "mcs_version", "mcs_abi_version", "mcs_last_error", "mcs_device_count", "mcs_hip_runtime",
     "mcs_plan_create", "mcs_plan_destroy", "mcs_plan_out_shape", "mcs_plan_describe",
-    "mcs_stitch_host", "mcs_stitch_device", "mcs_plan_footprint",
+    "mcs_stitch_host", "mcs_stitch_device", "mcs_plan_footprint", "mcs_plan_prepare",
+    "mcs_plan_stats",
 )
 
 
@@ -157,6 +158,10 @@ def load() -> ctypes.CDLL:
         L.mcs_stitch_device.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_int64), P,
                                         ctypes.c_int64, ctypes.c_int64, I, P]
         L.mcs_stitch_device.restype = I
+        L.mcs_plan_prepare.argtypes = [P, P]
+        L.mcs_plan_prepare.restype = I
+        L.mcs_plan_stats.argtypes = [P, ctypes.POINTER(ctypes.c_int64), I]
+        L.mcs_plan_stats.restype = I
         L.mcs_plan_footprint.argtypes = [P, ctypes.POINTER(ctypes.c_int64), I]
         L.mcs_plan_footprint.restype = I
         L.mcs__force_off64.argtypes = [I]   # test hook (not part of mcs.h)
@@ -261,6 +266,16 @@ class Plan:
         check(self._lib.mcs_stitch_device(self._h, ptrs, strides, ctypes.c_void_p(int(out_ptr)),
                                           int(out_pitch), int(out_frame_stride), int(n_frames),
                                           ctypes.c_void_p(int(stream))))
+
+    def prepare(self, stream: int = 0):
+        """Evaluate and store the plan's map tables on its device (once)."""
+        check(self._lib.mcs_plan_prepare(self._h, ctypes.c_void_p(int(stream))))
+
+    def stats(self) -> dict:
+        arr = (ctypes.c_int64 * 5)()
+        check(self._lib.mcs_plan_stats(self._h, arr, 5))
+        return {"prepared": bool(arr[0]), "tiles": arr[1], "lds_tiles": arr[2],
+                "direct_tiles": arr[3], "table_bytes": arr[4]}
 
     def footprint(self):
         arr = (ctypes.c_int64 * MCS_MAX_CAMS)()

@@ -24,6 +24,12 @@ struct mcs_plan {
     uint8_t *d_cams[MCS_MAX_CAMS] = {};
     uint8_t *d_out = nullptr;
     int64_t out_pitch = 0;
+    // prepared tables (mcs_plan_prepare): tile headers, per-pixel LDS descriptors, fallback list
+    bool prepared = false;
+    int gx = 0, gy = 0, n_fallback = 0;
+    mcs::TileHdr *d_tiles = nullptr;
+    uint32_t *d_desc = nullptr;
+    int *d_fallback = nullptr;
 };
 
 #define MCS_VERSION_STRING "mcs 0.1.0 (gfx950 code object, HIP module launch)"
@@ -43,10 +49,10 @@ constexpr int kMaxDevices = 64;
 
 struct Kernels {
     hipModule_t mod = nullptr;
-    hipFunction_t stitch[5][2][2] = {};   // [channels][interp][32-bit offsets]
+    hipFunction_t prepare[5][2] = {};     // [channels][interp]
+    hipFunction_t stream[5] = {};         // [channels]
+    hipFunction_t direct[5][2][2] = {};   // [channels][interp][32-bit offsets]
     hipFunction_t footprint[2] = {};
-    hipFunction_t echo = nullptr;
-    hipFunction_t dbg = nullptr;
 };
 Kernels g_k[kMaxDevices];
 std::mutex g_k_mu;
@@ -61,16 +67,20 @@ int kernels(const Api *A, int device, const Kernels **out)
         hipModule_t m = nullptr;
         HIP_TRY(A->hipModuleLoadData(&m, mcs_hsaco_start));
         char name[64];
-        for (int c = 1; c <= 4; c++)
-            for (int i = 0; i < 2; i++)
+        for (int c = 1; c <= 4; c++) {
+            snprintf(name, sizeof(name), "mcs_stream_c%d", c);
+            HIP_TRY(A->hipModuleGetFunction(&k.stream[c], m, name));
+            for (int i = 0; i < 2; i++) {
+                snprintf(name, sizeof(name), "mcs_prepare_c%d_i%d", c, i);
+                HIP_TRY(A->hipModuleGetFunction(&k.prepare[c][i], m, name));
                 for (int o = 0; o < 2; o++) {
-                    snprintf(name, sizeof(name), "mcs_stitch_c%d_i%d_o%d", c, i, o ? 32 : 64);
-                    HIP_TRY(A->hipModuleGetFunction(&k.stitch[c][i][o], m, name));
+                    snprintf(name, sizeof(name), "mcs_direct_c%d_i%d_o%d", c, i, o ? 32 : 64);
+                    HIP_TRY(A->hipModuleGetFunction(&k.direct[c][i][o], m, name));
                 }
+            }
+        }
         HIP_TRY(A->hipModuleGetFunction(&k.footprint[0], m, "mcs_footprint_i0"));
         HIP_TRY(A->hipModuleGetFunction(&k.footprint[1], m, "mcs_footprint_i1"));
-        HIP_TRY(A->hipModuleGetFunction(&k.echo, m, "mcs_echo_kparams"));
-        HIP_TRY(A->hipModuleGetFunction(&k.dbg, m, "mcs_debug_pixels_c3"));
         k.mod = m;
     }
     *out = &k;
@@ -142,43 +152,98 @@ bool offset_base(const mcs_plan *p, const mcs::KParams &kp, const uint8_t **base
     return off32;
 }
 
-int launch_stitch(const Api *A, const mcs_plan *p, const mcs::KParams &kp, int n_frames,
-                  hipStream_t s)
+// Prepared tables of a plan: one prepare launch, then the fallback-tile count is read back.
+// Allocates and synchronises: call before graph capture (the stitch entry points call it lazily).
+int prepare(const Api *A, mcs_plan *p, hipStream_t s)
+{
+    if (p->prepared) return MCS_OK;
+    const Kernels *k = nullptr;
+    int rc = kernels(A, p->device, &k);
+    if (rc) return rc;
+    p->gx = (p->fd.out_w + mcs::kTileW - 1) / mcs::kTileW;
+    p->gy = (p->fd.out_h + mcs::kTileH - 1) / mcs::kTileH;
+    const size_t tiles = (size_t)p->gx * p->gy;
+    if (tiles == 0) {
+        p->prepared = true;
+        return MCS_OK;
+    }
+    HIP_TRY(A->hipMalloc((void **)&p->d_tiles, tiles * sizeof(mcs::TileHdr)));
+    HIP_TRY(A->hipMalloc((void **)&p->d_desc, tiles * mcs::kTilePx * mcs::kDescWords * 4));
+    HIP_TRY(A->hipMalloc((void **)&p->d_fallback, (tiles + 1) * sizeof(int)));
+    HIP_TRY(A->hipMemsetAsync(p->d_fallback, 0, sizeof(int), s));
+    mcs::KPrepareArgs args;
+    args.P = p->kp;
+    args.tiles = p->d_tiles;
+    args.desc = p->d_desc;
+    args.fallback = p->d_fallback;
+    size_t sz = sizeof(args);
+    void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, (void *)&args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz,
+                   HIP_LAUNCH_PARAM_END};
+    HIP_TRY(A->hipModuleLaunchKernel(k->prepare[p->fd.channels][p->fd.interp], p->gx, p->gy, 1,
+                                     mcs::kWave, mcs::kWavesPerBlock, 1, 0, s, nullptr, cfg));
+    int nf = 0;
+    HIP_TRY(A->hipMemcpyAsync(&nf, p->d_fallback, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(A->hipStreamSynchronize(s));
+    p->n_fallback = nf;
+    p->prepared = true;
+    return MCS_OK;
+}
+
+// One launch pair (stream over all tiles + direct over the fallback tiles) for n_frames captures
+// that share one frame stride.
+int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams &P, int n_frames,
+                hipStream_t s)
+{
+    {
+        mcs::KStreamArgs args;
+        args.P = P;
+        args.tiles = p->d_tiles;
+        args.desc = p->d_desc;
+        args.n_frames = n_frames;
+        args.pad_ = 0;
+        size_t sz = sizeof(args);
+        void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, (void *)&args, HIP_LAUNCH_PARAM_BUFFER_SIZE,
+                       &sz, HIP_LAUNCH_PARAM_END};
+        HIP_TRY(A->hipModuleLaunchKernel(k->stream[p->fd.channels], p->gx, p->gy, 1, mcs::kWave,
+                                         mcs::kWavesPerBlock, 1, mcs::kLdsStream, s, nullptr, cfg));
+    }
+    if (p->n_fallback > 0) {
+        mcs::KDirectArgs args;
+        args.P = P;
+        const bool off32 = offset_base(p, args.P, &args.P.base);
+        args.fallback = p->d_fallback;
+        args.n_frames = n_frames;
+        args.pad_ = 0;
+        size_t sz = sizeof(args);
+        void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, (void *)&args, HIP_LAUNCH_PARAM_BUFFER_SIZE,
+                       &sz, HIP_LAUNCH_PARAM_END};
+        HIP_TRY(A->hipModuleLaunchKernel(k->direct[p->fd.channels][p->fd.interp][off32 ? 1 : 0],
+                                         p->n_fallback, 1, 1, mcs::kWave, mcs::kWavesPerBlock, 1,
+                                         0, s, nullptr, cfg));
+    }
+    return MCS_OK;
+}
+
+int launch_stitch(const Api *A, mcs_plan *p, const mcs::KParams &kp, int n_frames, hipStream_t s)
 {
     if (kp.out_w <= 0 || kp.out_h <= 0 || n_frames <= 0) return MCS_OK;
     const Kernels *k = nullptr;
     int rc = kernels(A, p->device, &k);
     if (rc) return rc;
-    const unsigned gx = (kp.out_w + mcs::kTileW - 1) / mcs::kTileW;
-    const unsigned gy = (kp.out_h + mcs::kTileH - 1) / mcs::kTileH;
-    // the kernel walks the batch with one frame stride for every camera: split otherwise
+    rc = prepare(A, p, s);
+    if (rc) return rc;
+    // the kernels walk the batch with one frame stride for every camera: split otherwise
     bool uniform = true;
     for (int j = 0; j < p->fd.n_stages; j++)
         uniform = uniform && kp.cam_fstride[p->fd.st[j].cam] == kp.cam_fstride[0];
-    mcs::KStitchArgs args;
-    args.P = kp;
-    args.pad_ = 0;
-    size_t sz = sizeof(args);
-    void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, (void *)&args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz,
-                   HIP_LAUNCH_PARAM_END};
-    const int C = p->fd.channels, I = p->fd.interp;
-    if (uniform) {
-        args.n_frames = n_frames;
-        const bool off32 = offset_base(p, args.P, &args.P.base);
-        hipFunction_t fn = k->stitch[C][I][off32 ? 1 : 0];
-        HIP_TRY(A->hipModuleLaunchKernel(fn, gx, gy, 1, mcs::kWave, mcs::kWavesPerBlock, 1,
-                                         mcs::kLdsBytes, s, nullptr, cfg));
-        return MCS_OK;
-    }
-    args.n_frames = 1;
+    mcs::KParams P = kp;
+    if (uniform) return launch_pair(A, p, k, P, n_frames, s);
     for (int f = 0; f < n_frames; f++) {
         for (int i = 0; i < p->fd.n_cams; i++)
-            args.P.cams[i] = kp.cams[i] ? kp.cams[i] + (int64_t)f * kp.cam_fstride[i] : nullptr;
-        args.P.out = kp.out + (int64_t)f * kp.out_fstride;
-        const bool off32 = offset_base(p, args.P, &args.P.base);
-        hipFunction_t fn = k->stitch[C][I][off32 ? 1 : 0];
-        HIP_TRY(A->hipModuleLaunchKernel(fn, gx, gy, 1, mcs::kWave, mcs::kWavesPerBlock, 1,
-                                         mcs::kLdsBytes, s, nullptr, cfg));
+            P.cams[i] = kp.cams[i] ? kp.cams[i] + (int64_t)f * kp.cam_fstride[i] : nullptr;
+        P.out = kp.out + (int64_t)f * kp.out_fstride;
+        rc = launch_pair(A, p, k, P, 1, s);
+        if (rc) return rc;
     }
     return MCS_OK;
 }
@@ -236,7 +301,7 @@ int mcs_plan_create(const mcs_stage_desc *stages, int n_stages, int cam0_w, int 
 int mcs_plan_destroy(mcs_plan *p)
 {
     if (!p) return MCS_OK;
-    bool touched = p->stream || p->d_out;
+    bool touched = p->stream || p->d_out || p->d_tiles;
     for (int i = 0; i < MCS_MAX_CAMS; i++) touched = touched || p->d_cams[i];
     if (touched) {
         const Api *A = mcs::rt::api();
@@ -246,6 +311,9 @@ int mcs_plan_destroy(mcs_plan *p)
             for (int i = 0; i < MCS_MAX_CAMS; i++)
                 if (p->d_cams[i]) (void)A->hipFree(p->d_cams[i]);
             if (p->d_out) (void)A->hipFree(p->d_out);
+            if (p->d_tiles) (void)A->hipFree(p->d_tiles);
+            if (p->d_desc) (void)A->hipFree(p->d_desc);
+            if (p->d_fallback) (void)A->hipFree(p->d_fallback);
             if (p->stream) (void)A->hipStreamDestroy(p->stream);
         }
     }
@@ -340,6 +408,35 @@ int mcs_stitch_device(mcs_plan *p, const uint8_t *const *d_cams, const int64_t *
     return launch_stitch(A, p, kp, n_frames, (hipStream_t)stream);
 }
 
+int mcs_plan_prepare(mcs_plan *p, void *stream)
+{
+    if (!p) return mcs::fail(MCS_E_INVALID, "NULL plan");
+    const Api *A = mcs::rt::api();
+    if (!A) return MCS_E_HIP;
+    if (p->fd.out_w <= 0 || p->fd.out_h <= 0) return MCS_OK;
+    DeviceGuard g(A, p->device);
+    if (g.err != hipSuccess)
+        return mcs::fail(MCS_E_HIP, "hipSetDevice(%d): %s", p->device, A->hipGetErrorString(g.err));
+    hipStream_t s = (hipStream_t)stream;
+    if (!s) {
+        int rc = ensure_stream(A, p);
+        if (rc) return rc;
+        s = p->stream;
+    }
+    return prepare(A, p, s);
+}
+
+int mcs_plan_stats(const mcs_plan *p, int64_t *stats, int n)
+{
+    if (!p || !stats) return mcs::fail(MCS_E_INVALID, "NULL plan/stats");
+    const int64_t tiles = (int64_t)p->gx * p->gy;
+    const int64_t v[5] = {p->prepared ? 1 : 0, tiles, tiles - p->n_fallback, p->n_fallback,
+                          tiles * (int64_t)(sizeof(mcs::TileHdr) +
+                                            mcs::kTilePx * mcs::kDescWords * 4)};
+    for (int i = 0; i < n; i++) stats[i] = i < 5 ? v[i] : 0;
+    return MCS_OK;
+}
+
 int mcs_plan_footprint(mcs_plan *p, int64_t *touched_px, int n_cams)
 {
     if (!p || !touched_px) return mcs::fail(MCS_E_INVALID, "NULL plan/touched_px");
@@ -396,78 +493,5 @@ int mcs_plan_footprint(mcs_plan *p, int64_t *touched_px, int n_cams)
 
 // Test hook (not in mcs.h): force the 64-bit-address kernel variants.
 void mcs__force_off64(int on) { g_force_off64 = on; }
-
-// Diagnostic (not in mcs.h): the plan's KParams as the device receives them, and as the host
-// sent them, into two host buffers of mcs__kparams_size() bytes each.
-size_t mcs__kparams_size(void) { return sizeof(mcs::KParams); }
-
-int mcs__echo_kparams(mcs_plan *p, void *dev_view, void *host_view)
-{
-    const Api *A = mcs::rt::api();
-    if (!A) return MCS_E_HIP;
-    DeviceGuard g(A, p->device);
-    int rc = ensure_stream(A, p);
-    if (rc) return rc;
-    const Kernels *k = nullptr;
-    rc = kernels(A, p->device, &k);
-    if (rc) return rc;
-    struct {
-        mcs::KParams P;
-        uint8_t *out;
-    } args;
-    args.P = p->kp;
-    uint8_t *d = nullptr;
-    HIP_TRY(A->hipMalloc((void **)&d, sizeof(mcs::KParams)));
-    args.out = d;
-    size_t sz = sizeof(args);
-    void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, (void *)&args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz,
-                   HIP_LAUNCH_PARAM_END};
-    HIP_TRY(A->hipModuleLaunchKernel(k->echo, 1, 1, 1, 64, 1, 1, 0, p->stream, nullptr, cfg));
-    HIP_TRY(A->hipMemcpyAsync(dev_view, d, sizeof(mcs::KParams), hipMemcpyDeviceToHost, p->stream));
-    HIP_TRY(A->hipStreamSynchronize(p->stream));
-    (void)A->hipFree(d);
-    memcpy(host_view, &p->kp, sizeof(mcs::KParams));
-    return MCS_OK;
-}
-
-int mcs__debug_pixels(mcs_plan *p, const uint8_t *const *cams, int *host_out)
-{
-    const Api *A = mcs::rt::api();
-    if (!A) return MCS_E_HIP;
-    DeviceGuard g(A, p->device);
-    int rc = ensure_stream(A, p);
-    if (rc) return rc;
-    rc = ensure_host_buffers(A, p);
-    if (rc) return rc;
-    const Kernels *k = nullptr;
-    rc = kernels(A, p->device, &k);
-    if (rc) return rc;
-    bool need[MCS_MAX_CAMS];
-    need_mask(p->fd, need);
-    for (int i = 0; i < p->fd.n_cams; i++)
-        if (need[i])
-            HIP_TRY(A->hipMemcpyAsync(p->d_cams[i], cams[i],
-                                      (size_t)p->fd.cam_w[i] * p->fd.cam_h[i] * 3,
-                                      hipMemcpyHostToDevice, p->stream));
-    struct {
-        mcs::KParams P;
-        int *out;
-    } args;
-    args.P = p->kp;
-    for (int i = 0; i < p->fd.n_cams; i++) args.P.cams[i] = p->d_cams[i];
-    const size_t bytes = (size_t)p->fd.out_w * p->fd.out_h * 16;
-    int *d = nullptr;
-    HIP_TRY(A->hipMalloc((void **)&d, bytes));
-    args.out = d;
-    size_t sz = sizeof(args);
-    void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, (void *)&args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz,
-                   HIP_LAUNCH_PARAM_END};
-    HIP_TRY(A->hipModuleLaunchKernel(k->dbg, (p->fd.out_w + 255) / 256, p->fd.out_h, 1, 256, 1, 1,
-                                     0, p->stream, nullptr, cfg));
-    HIP_TRY(A->hipMemcpyAsync(host_out, d, bytes, hipMemcpyDeviceToHost, p->stream));
-    HIP_TRY(A->hipStreamSynchronize(p->stream));
-    (void)A->hipFree(d);
-    return MCS_OK;
-}
 
 }  // extern "C"

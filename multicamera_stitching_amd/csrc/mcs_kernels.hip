@@ -372,23 +372,119 @@ __device__ __forceinline__ void stitch_direct(const KParams &P, int n_frames, in
 }
 
 // ---------------------------------------------------------------------------------------------
-// LDS-staged gather (the main path).  Per launch, every block (256 x 8 output pixels, 8 waves)
-// evaluates its pixels' exact maps, reduces them to one source footprint per camera (rows x
-// 16-byte chunks, the union of all its row windows) and lays the footprints out in LDS.  Per
-// capture, each footprint row is ONE global_load_lds_dwordx4 wave instruction (LDS-DMA: wide,
-// contiguous, no registers), double-buffered across captures; pixels then read their 8-byte
-// windows from LDS with aligned ds_read2_b32 + ds_read_b32 and v_alignbyte.  Blocks whose
-// footprint exceeds kLdsBuf (steep perspective, 3+ cameras in one tile) take the direct path.
-struct LdsHeader {
-    int rmin[MCS_MAX_CAMS], rmax[MCS_MAX_CAMS], cmin[MCS_MAX_CAMS], cmax[MCS_MAX_CAMS];
-    int base[MCS_MAX_CAMS], stride[MCS_MAX_CAMS], cal[MCS_MAX_CAMS];
-    int jobstart[MCS_MAX_CAMS + 1];
-    int fits, njobs;
-};
-static_assert(sizeof(LdsHeader) <= kLdsHeader, "LDS header");
+// LDS-staged gather (the main path), in two kernels.
+//
+// prepare (once per plan): every 256 x 8 tile evaluates its pixels' exact maps, reduces them to
+// one source footprint per camera (rows x 16-byte chunks: the union of all its row windows),
+// lays the footprints out as one LDS slot, and stores a TileHdr plus each pixel's LDS window
+// addresses and weights.  Tiles that do not fit (more than kTileCams cameras, a slot larger than
+// kLdsRing / 2, rows wider than 1 KiB) are listed for the direct-gather kernel instead.
+//
+// stream (every launch): per capture, each footprint row is ONE global_load_lds_dwordx4 wave
+// instruction (LDS-DMA: wide, contiguous, no registers) into a ring of slots, several captures in
+// flight; pixels read their 8-byte windows from LDS with aligned ds_read2_b32 + ds_read_b32 and
+// v_alignbyte, blend with v_dot2_u32_u16, and store 12 contiguous bytes per lane.
 
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+struct FootprintLds {
+    int rmin[MCS_MAX_CAMS], rmax[MCS_MAX_CAMS], cmin[MCS_MAX_CAMS], cmax[MCS_MAX_CAMS];
+};
+
+template <int CN, int INTERP>
+__device__ __forceinline__ void prepare_tile(const KParams &P, TileHdr *tiles, uint32_t *desc,
+                                             int *fallback)
+{
+    __shared__ FootprintLds fl;
+    __shared__ TileHdr th;
+    const int lane = threadIdx.x, wave = threadIdx.y;
+    const int tid = wave * kWave + lane;
+    const int tile = blockIdx.y * gridDim.x + blockIdx.x;
+    const int xg = (blockIdx.x * kWave + lane) * kPx;
+    const int y = blockIdx.y * kTileH + wave;
+    const bool live = xg < P.out_w && y < P.out_h;
+    const int npx = live ? min(kPx, P.out_w - xg) : 0;
+    if (tid < MCS_MAX_CAMS) {
+        fl.rmin[tid] = 0x7fffffff;
+        fl.rmax[tid] = -0x7fffffff;
+        fl.cmin[tid] = 0x7fffffff;
+        fl.cmax[tid] = -0x7fffffff;
+    }
+    __syncthreads();
+    Geo g[kPx];
+#pragma unroll
+    for (int p = 0; p < kPx; p++) {
+        g[p] = describe_geo<CN, INTERP>(P, min(xg + p, P.out_w - 1), min(y, P.out_h - 1));
+        if (p >= npx) g[p].w0 = g[p].w1 = 0u;
+    }
+#pragma unroll
+    for (int p = 0; p < kPx; p++) {
+        if ((g[p].w0 | g[p].w1) == 0u) continue;
+        const int c = g[p].cam;
+        atomicMin(&fl.rmin[c], min(g[p].r0, g[p].r1));
+        atomicMax(&fl.rmax[c], max(g[p].r0, g[p].r1));
+        atomicMin(&fl.cmin[c], min(g[p].c0, g[p].c1));
+        atomicMax(&fl.cmax[c], max(g[p].c0, g[p].c1));
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int total = 0, jobs = 0, n = 0, fits = 1;
+        for (int c = 0; c < MCS_MAX_CAMS; c++) {
+            if (fl.rmin[c] > fl.rmax[c]) continue;
+            if (n == kTileCams) {
+                fits = 0;
+                break;
+            }
+            const int cal = fl.cmin[c] & ~15;
+            const int stride = (fl.cmax[c] + 8 - cal + 15) & ~15;
+            const int rows = fl.rmax[c] - fl.rmin[c] + 1;
+            th.cam[n] = c;
+            th.rmin[n] = fl.rmin[c];
+            th.cal[n] = cal;
+            th.stride[n] = stride;
+            th.base[n] = total;
+            th.jobstart[n] = jobs;
+            total += rows * stride;
+            jobs += rows;
+            if (stride > 16 * kWave) fits = 0;
+            n++;
+        }
+        for (int k = n; k < kTileCams; k++) {
+            th.cam[k] = th.rmin[k] = th.cal[k] = th.stride[k] = th.base[k] = 0;
+            th.jobstart[k] = jobs;
+        }
+        th.jobstart[kTileCams] = jobs;
+        th.ncam = n;
+        th.njobs = jobs;
+        const int buf = (total + kLdsSlack + 15) & ~15;
+        th.buf_bytes = buf;
+        th.ring = min(kMaxRing, kLdsRing / buf);
+        th.fits = fits && th.ring >= 2 && total < 65536 - kLdsSlack;
+        th.pad_[0] = th.pad_[1] = 0;
+        tiles[tile] = th;
+        if (!th.fits) fallback[1 + atomicAdd(&fallback[0], 1)] = tile;
+    }
+    __syncthreads();
+    uint32_t d[kPx * kDescWords];
+#pragma unroll
+    for (int p = 0; p < kPx; p++) {
+        int k = 0;
+        while (k < th.ncam - 1 && th.cam[k] != g[p].cam) k++;
+        const int st = th.stride[k], rm = th.rmin[k], ca = th.cal[k], bs = th.base[k];
+        uint32_t a0 = (uint32_t)(bs + (g[p].r0 - rm) * st + (g[p].c0 - ca));
+        uint32_t a1 = (uint32_t)(bs + (g[p].r1 - rm) * st + (g[p].c1 - ca));
+        if ((g[p].w0 | g[p].w1) == 0u || !th.fits) a0 = a1 = 0u;
+        d[p * kDescWords + 0] = (a0 & 0xffffu) | (a1 << 16);
+        d[p * kDescWords + 1] = g[p].w0;
+        d[p * kDescWords + 2] = g[p].w1;
+    }
+    uint4 *o = reinterpret_cast<uint4 *>(desc + ((int64_t)tile * kTilePx + (int64_t)tid * kPx) *
+                                                    kDescWords);
+#pragma unroll
+    for (int i = 0; i < kPx * kDescWords / 4; i++)
+        o[i] = make_uint4(d[4 * i], d[4 * i + 1], d[4 * i + 2], d[4 * i + 3]);
+}
 
 __device__ __forceinline__ uint2 lds_window(const uint8_t *smem, uint32_t a)
 {
@@ -401,26 +497,54 @@ __device__ __forceinline__ uint2 lds_window(const uint8_t *smem, uint32_t a)
     return r;
 }
 
-// Issues the LDS-DMA loads of capture f's footprint rows into buffer `buf` (rows split over the
-// block's waves; lanes = 16-byte chunks of a row).  Chunks that would cross the end of a camera
-// frame are copied byte by byte instead (only the bytes inside the frame).
-template <int CN>
-__device__ __forceinline__ void stage_capture(const KParams &P, const LdsHeader *h, uint8_t *buf,
-                                              int f, int lane, int wave)
+// s_waitcnt vmcnt(n) for a run-time n (clamped to 15: waiting for fewer outstanding is stricter).
+__device__ __forceinline__ void wait_vmcnt_le(int n)
 {
-    const int njobs = h->njobs;
+    switch (n < 0 ? 0 : (n > 15 ? 15 : n)) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
+    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+// Issues the LDS-DMA loads of capture f's footprint rows into `slot` (rows split over the block's
+// waves; lanes = 16-byte chunks of a row).  Chunks that would cross the end of a camera frame are
+// copied byte by byte instead (only the bytes inside the frame).
+// Block-uniform value read from LDS (broadcast read + readfirstlane -> SGPR).
+__device__ __forceinline__ int uni(const int &v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// Issues the LDS-DMA loads of capture f's footprint rows into `slot` (rows split over the block's
+// waves; lanes = 16-byte chunks of a row).  Chunks that would cross the end of a camera frame are
+// copied byte by byte instead (only the bytes inside the frame).  h lives in LDS.
+template <int CN>
+__device__ __forceinline__ void stage_capture(const KParams &P, const TileHdr &h, uint8_t *slot,
+                                              int f, int lane, int wave, int njobs)
+{
     for (int j = wave; j < njobs; j += kWavesPerBlock) {
-        int c = 0;
-        while (j >= h->jobstart[c + 1]) c++;
-        c = __builtin_amdgcn_readfirstlane(c);
-        const int row = j - h->jobstart[c];
-        const int stride = __builtin_amdgcn_readfirstlane(h->stride[c]);
+        int k = 0;
+        while (k < kTileCams - 1 && j >= uni(h.jobstart[k + 1])) k++;
+        const int c = uni(h.cam[k]);
+        const int row = j - uni(h.jobstart[k]);
+        const int stride = uni(h.stride[k]);
         const int64_t pitch = (int64_t)P.cam_w[c] * CN;
         const int64_t fbytes = pitch * P.cam_h[c];
-        const int64_t goff = (int64_t)(h->rmin[c] + row) * pitch + h->cal[c] + 16 * lane;
+        const int64_t goff = (int64_t)(uni(h.rmin[k]) + row) * pitch + uni(h.cal[k]) + 16 * lane;
         const uint8_t *src = P.cams[c] + (int64_t)f * P.cam_fstride[0];
-        const uint32_t lds_row = (uint32_t)(h->base[c] + row * stride);
-        lds_u8 *dst = ((lds_u8 *)buf) + __builtin_amdgcn_readfirstlane(lds_row);
+        lds_u8 *dst = ((lds_u8 *)slot) + uni(h.base[k]) + row * stride;
         if (16 * lane < stride) {
             if (goff + 16 <= fbytes) {
                 __builtin_amdgcn_global_load_lds(src + goff, dst, 16, 0, 0);
@@ -432,119 +556,71 @@ __device__ __forceinline__ void stage_capture(const KParams &P, const LdsHeader 
     }
 }
 
-template <int CN, int INTERP, bool OFF32>
-__device__ __forceinline__ void stitch_lds(const KParams &P, int n_frames, uint8_t *smem)
+template <int CN>
+__device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *tiles,
+                                            const uint32_t *desc, int n_frames, uint8_t *smem)
 {
-    const int lane = threadIdx.x, wave = threadIdx.y;
+    // threadIdx.y is the wave index (blockDim.x == 64): make that provable to the compiler so
+    // job/camera lookups stay scalar and the LDS-DMA base (M0) needs no waterfall
+    const int lane = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(threadIdx.y);
     const int tid = wave * kWave + lane;
+    const int tile = blockIdx.y * gridDim.x + blockIdx.x;
+    // the tile header, copied once into LDS (the kernel also stores to global memory, so the
+    // compiler cannot serve `tiles` from the scalar cache)
+    TileHdr &h = *reinterpret_cast<TileHdr *>(smem);
+    uint8_t *const ring0 = smem + sizeof(TileHdr);
+    if (tid < (int)(sizeof(TileHdr) / 4))
+        reinterpret_cast<int *>(&h)[tid] = reinterpret_cast<const int *>(&tiles[tile])[tid];
+    __syncthreads();
+    if (!uni(h.fits)) return;                  // handled by the direct-gather launch
     const int xg = (blockIdx.x * kWave + lane) * kPx;
     const int y = blockIdx.y * kTileH + wave;
     const bool live = xg < P.out_w && y < P.out_h;
     const int npx = live ? min(kPx, P.out_w - xg) : 0;
-    LdsHeader *h = reinterpret_cast<LdsHeader *>(smem);
-    if (tid < MCS_MAX_CAMS) {
-        h->rmin[tid] = 0x7fffffff;
-        h->rmax[tid] = -0x7fffffff;
-        h->cmin[tid] = 0x7fffffff;
-        h->cmax[tid] = -0x7fffffff;
-    }
-    __syncthreads();
-
-    // 1. exact map of this lane's pixels, then the per-camera footprint of the block
-    Geo g[kPx];
-#pragma unroll
-    for (int p = 0; p < kPx; p++) {
-        g[p] = describe_geo<CN, INTERP>(P, min(xg + p, P.out_w - 1), min(y, P.out_h - 1));
-        if (p >= npx) g[p].w0 = g[p].w1 = 0u;
-    }
+    uint32_t d[kPx * kDescWords];
     {
-        int cam = -1, rmin = 0x7fffffff, rmax = -0x7fffffff, cmin = 0x7fffffff, cmax = -0x7fffffff;
+        const uint4 *s4 = reinterpret_cast<const uint4 *>(
+            desc + ((int64_t)tile * kTilePx + (int64_t)tid * kPx) * kDescWords);
 #pragma unroll
-        for (int p = 0; p < kPx; p++) {
-            if ((g[p].w0 | g[p].w1) == 0u) continue;
-            if (cam < 0) cam = g[p].cam;
-            const int r_lo = min(g[p].r0, g[p].r1), r_hi = max(g[p].r0, g[p].r1);
-            const int c_lo = min(g[p].c0, g[p].c1), c_hi = max(g[p].c0, g[p].c1);
-            if (g[p].cam == cam) {
-                rmin = min(rmin, r_lo);
-                rmax = max(rmax, r_hi);
-                cmin = min(cmin, c_lo);
-                cmax = max(cmax, c_hi);
-            } else {
-                atomicMin(&h->rmin[g[p].cam], r_lo);
-                atomicMax(&h->rmax[g[p].cam], r_hi);
-                atomicMin(&h->cmin[g[p].cam], c_lo);
-                atomicMax(&h->cmax[g[p].cam], c_hi);
-            }
-        }
-        if (cam >= 0) {
-            atomicMin(&h->rmin[cam], rmin);
-            atomicMax(&h->rmax[cam], rmax);
-            atomicMin(&h->cmin[cam], cmin);
-            atomicMax(&h->cmax[cam], cmax);
+        for (int i = 0; i < kPx * kDescWords / 4; i++) {
+            const uint4 v = s4[i];
+            d[4 * i] = v.x;
+            d[4 * i + 1] = v.y;
+            d[4 * i + 2] = v.z;
+            d[4 * i + 3] = v.w;
         }
     }
-    __syncthreads();
-    if (tid == 0) {
-        int total = 0, jobs = 0, fits = 1;
-        for (int c = 0; c < MCS_MAX_CAMS; c++) {
-            h->jobstart[c] = jobs;
-            if (h->rmin[c] > h->rmax[c]) continue;
-            const int cal = h->cmin[c] & ~15;
-            const int stride = (h->cmax[c] + 8 - cal + 15) & ~15;
-            const int rows = h->rmax[c] - h->rmin[c] + 1;
-            h->cal[c] = cal;
-            h->stride[c] = stride;
-            h->base[c] = total;
-            total += rows * stride;
-            jobs += rows;
-            if (stride > 16 * kWave) fits = 0;
-        }
-        h->jobstart[MCS_MAX_CAMS] = jobs;
-        h->njobs = jobs;
-        h->fits = fits && total <= kLdsBuf;
-    }
-    __syncthreads();
-    if (!h->fits) {              // block-uniform: footprint too large for the LDS budget
-        if (live) stitch_direct<CN, INTERP, OFF32>(P, n_frames, xg, y);
-        return;
-    }
-
-    // 2. LDS window addresses of every pixel (buffer-relative)
-    uint32_t win[kPx], w0[kPx], w1[kPx];
-#pragma unroll
-    for (int p = 0; p < kPx; p++) {
-        const int c = g[p].cam;
-        const int st = h->stride[c], rm = h->rmin[c], ca = h->cal[c], bs = h->base[c];
-        uint32_t a0 = (uint32_t)(bs + (g[p].r0 - rm) * st + (g[p].c0 - ca));
-        uint32_t a1 = (uint32_t)(bs + (g[p].r1 - rm) * st + (g[p].c1 - ca));
-        if ((g[p].w0 | g[p].w1) == 0u) a0 = a1 = 0u;
-        win[p] = a0 | (a1 << 16);
-        w0[p] = g[p].w0;
-        w1[p] = g[p].w1;
-    }
-
-    uint8_t *bufs[2] = {smem + kLdsHeader, smem + kLdsHeader + kLdsBuf + kLdsSlack};
+    const int ring = uni(h.ring), buf_bytes = uni(h.buf_bytes), njobs = uni(h.njobs);
+    // VMEM instructions this wave issues per capture: D footprint rows (LDS-DMA), S >= 1 store
+    const int D = wave < njobs ? (njobs - 1 - wave) / kWavesPerBlock + 1 : 0;
+    const int S = y < P.out_h ? 1 : 0;
     uint8_t *dst = P.out + (int64_t)min(y, P.out_h - 1) * P.out_pitch + (int64_t)xg * CN;
     const bool wide = npx == kPx && (((uintptr_t)dst | (uintptr_t)P.out_fstride) & 3) == 0;
 
-    // 3. stream the captures: DMA(f+1) || gather(f), one barrier per capture
-    stage_capture<CN>(P, h, bufs[0], 0, lane, wave);
+    // Stream the captures through the ring: while capture f is gathered from slot f % ring,
+    // captures f+1 .. f+ring-1 are in flight.  One barrier per capture.
+    for (int q = 0; q < ring - 1 && q < n_frames; q++)
+        stage_capture<CN>(P, h, ring0 + q * buf_bytes, q, lane, wave, njobs);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    __builtin_amdgcn_s_barrier();
     for (int f = 0; f < n_frames; f++) {
-        if (f + 1 < n_frames) stage_capture<CN>(P, h, bufs[(f + 1) & 1], f + 1, lane, wave);
-        const uint8_t *b = bufs[f & 1];
+        const int ahead = f + ring - 1;
+        if (ahead < n_frames)
+            stage_capture<CN>(P, h, ring0 + (ahead % ring) * buf_bytes, ahead, lane, wave, njobs);
+        const uint8_t *b = ring0 + (f % ring) * buf_bytes;
         if (live) {
             OutWords w;
 #pragma unroll
             for (int p = 0; p < kPx; p++) {
-                const uint2 r0 = lds_window(b, win[p] & 0xffffu);
-                const uint2 r1 = lds_window(b, win[p] >> 16);
+                const uint32_t win = d[p * kDescWords];
+                const uint2 r0 = lds_window(b, win & 0xffffu);
+                const uint2 r1 = lds_window(b, win >> 16);
 #pragma unroll
                 for (int k = 0; k < CN; k++) {
                     const int bb = p * CN + k;
-                    w.or_at(bb >> 2, blend<CN>(r0, r1, w0[p], w1[p], k) << (8 * (bb & 3)));
+                    w.or_at(bb >> 2, blend<CN>(r0, r1, d[p * kDescWords + 1],
+                                               d[p * kDescWords + 2], k)
+                                         << (8 * (bb & 3)));
                 }
             }
             uint8_t *o = dst + (int64_t)f * P.out_fstride;
@@ -557,13 +633,30 @@ __device__ __forceinline__ void stitch_lds(const KParams &P, int n_frames, uint8
                     o[bb] = (uint8_t)(w.at(bb >> 2) >> (8 * (bb & 3)));
             }
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
+        // Capture f+1 must have landed before the barrier; later captures' DMA may stay in
+        // flight.  vmcnt counts this wave's VMEM instructions in issue order: younger than
+        // DMA(f+1) are at least, per later iteration, its D DMA + S store instructions, and this
+        // iteration's S stores -> waiting for "<= younger" outstanding is exact or stricter.
+        const int younger = min(n_frames - 1 - f, ring - 2) * (D + S) + S;
+        wait_vmcnt_le(f + 1 < n_frames ? younger : 0);
+        __builtin_amdgcn_s_barrier();
     }
 }
 
-// Footprint marking: sets mask[cam][pixel] = 1 for every source pixel the mosaic reads with a
-// non-zero weight; counts[cam] += number of newly marked pixels.
+// Direct global gather for the tiles prepare could not fit in LDS (list in fallback[1..]).
+template <int CN, int INTERP, bool OFF32>
+__device__ __forceinline__ void direct_tile(const KParams &P, const int *fallback, int n_frames)
+{
+    const int tile = fallback[1 + blockIdx.x];
+    const int gx = (P.out_w + kTileW - 1) / kTileW;
+    const int tx = tile % gx, ty = tile / gx;
+    const int xg = (tx * kWave + threadIdx.x) * kPx;
+    const int y = ty * kTileH + threadIdx.y;
+    if (xg < P.out_w && y < P.out_h) stitch_direct<CN, INTERP, OFF32>(P, n_frames, xg, y);
+}
+
+// Footprint marking: mask[cam][pixel] = 1 for every source pixel the mosaic reads with a
+// non-zero weight; counts[cam] += newly marked pixels (algorithmic bytes of the roofline).
 template <int CN, int INTERP>
 __device__ __forceinline__ void footprint_mark(const KParams &P, uint8_t *const *masks,
                                                unsigned long long *counts)
@@ -604,25 +697,41 @@ __device__ __forceinline__ void footprint_mark(const KParams &P, uint8_t *const 
 }  // namespace mcs
 
 // ---------------------------------------------------------------------------------------------
-// Entry points (names looked up by mcs_capi.cpp).  Block shapes: stitch (64, 8, 1) with grid
-// (ceil(out_w/256), ceil(out_h/8)) and kLdsBytes of dynamic LDS; footprint (256, 1, 1) with grid
+// Entry points (names looked up by mcs_capi.cpp).  Block shapes: prepare and stream (64, 8, 1)
+// over the tile grid (ceil(out_w/256), ceil(out_h/8)), stream with kLdsRing bytes of dynamic
+// LDS; direct (64, 8, 1) over the fallback tile list; footprint (256, 1, 1) with grid
 // (ceil(out_w/256), out_h).
-#define MCS_STITCH_ENTRY(CN, IN, O32)                                                          \
-    extern "C" __global__ __launch_bounds__(512) void mcs_stitch_c##CN##_i##IN##_o##O32(       \
-        const mcs::KParams P, int n_frames)                                                    \
+#define MCS_PREPARE_ENTRY(CN, IN)                                                              \
+    extern "C" __global__ __launch_bounds__(512) void mcs_prepare_c##CN##_i##IN(               \
+        const mcs::KParams P, mcs::TileHdr *tiles, uint32_t *desc, int *fallback)              \
+    {                                                                                          \
+        mcs::prepare_tile<CN, IN>(P, tiles, desc, fallback);                                   \
+    }
+#define MCS_STREAM_ENTRY(CN)                                                                   \
+    extern "C" __global__ __launch_bounds__(512) void mcs_stream_c##CN(                        \
+        const mcs::KParams P, const mcs::TileHdr *tiles, const uint32_t *desc, int n_frames)  \
     {                                                                                          \
         extern __shared__ __attribute__((aligned(16))) uint8_t smem[];                         \
-        mcs::stitch_lds<CN, IN, O32 == 32>(P, n_frames, smem);                                 \
+        mcs::stream_tile<CN>(P, tiles, desc, n_frames, smem);                                  \
     }
-#define MCS_STITCH_ENTRIES(CN)                                                                 \
-    MCS_STITCH_ENTRY(CN, 0, 32)                                                                \
-    MCS_STITCH_ENTRY(CN, 1, 32)                                                                \
-    MCS_STITCH_ENTRY(CN, 0, 64)                                                                \
-    MCS_STITCH_ENTRY(CN, 1, 64)
-MCS_STITCH_ENTRIES(1)
-MCS_STITCH_ENTRIES(2)
-MCS_STITCH_ENTRIES(3)
-MCS_STITCH_ENTRIES(4)
+#define MCS_DIRECT_ENTRY(CN, IN, O32)                                                          \
+    extern "C" __global__ __launch_bounds__(512) void mcs_direct_c##CN##_i##IN##_o##O32(       \
+        const mcs::KParams P, const int *fallback, int n_frames)                              \
+    {                                                                                          \
+        mcs::direct_tile<CN, IN, O32 == 32>(P, fallback, n_frames);                            \
+    }
+#define MCS_ENTRIES(CN)                                                                        \
+    MCS_PREPARE_ENTRY(CN, 0)                                                                   \
+    MCS_PREPARE_ENTRY(CN, 1)                                                                   \
+    MCS_STREAM_ENTRY(CN)                                                                       \
+    MCS_DIRECT_ENTRY(CN, 0, 32)                                                                \
+    MCS_DIRECT_ENTRY(CN, 1, 32)                                                                \
+    MCS_DIRECT_ENTRY(CN, 0, 64)                                                                \
+    MCS_DIRECT_ENTRY(CN, 1, 64)
+MCS_ENTRIES(1)
+MCS_ENTRIES(2)
+MCS_ENTRIES(3)
+MCS_ENTRIES(4)
 
 extern "C" __global__ __launch_bounds__(256) void mcs_footprint_i0(const mcs::KParams P,
                                                                    uint8_t *const *masks,
@@ -636,35 +745,4 @@ extern "C" __global__ __launch_bounds__(256) void mcs_footprint_i1(const mcs::KP
                                                                    unsigned long long *counts)
 {
     mcs::footprint_mark<1, 1>(P, masks, counts);
-}
-
-// Diagnostic: per output pixel of frame 0, {owner stage, X, Y, packed sampled bytes}.
-extern "C" __global__ __launch_bounds__(256) void mcs_debug_pixels_c3(const mcs::KParams P,
-                                                                      int *dbg)
-{
-    using namespace mcs;
-    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
-    if (x >= P.out_w || y >= P.out_h) return;
-    const int s = owner(P, x, y);
-    int X = 0, Y = 0;
-    uint32_t v = 0;
-    if (s >= 0) {
-        const KStage &S = P.st[s];
-        map_exact<MCS_INTER_LINEAR>(S, x + S.offx, y + S.offy, X, Y);
-        v = sample<3, MCS_INTER_LINEAR>(P.cams[S.cam], S.src_w, S.src_h,
-                                        (int64_t)S.src_w * S.src_h * 3, X, Y);
-    }
-    int *d = dbg + 4 * ((int64_t)y * P.out_w + x);
-    d[0] = s;
-    d[1] = X;
-    d[2] = Y;
-    d[3] = (int)v;
-}
-
-// Diagnostic: copies the parameter block as the device sees it (kernarg transport check).
-extern "C" __global__ __launch_bounds__(64) void mcs_echo_kparams(const mcs::KParams P,
-                                                                  uint8_t *out)
-{
-    const uint8_t *src = reinterpret_cast<const uint8_t *>(&P);
-    for (int i = threadIdx.x; i < (int)sizeof(mcs::KParams); i += 64) out[i] = src[i];
 }

@@ -47,13 +47,6 @@ struct KFootprintArgs {
     unsigned long long *counts;
 };
 
-// Kernarg block of the stitch kernels: (KParams, int n_frames).
-struct KStitchArgs {
-    KParams P;
-    int n_frames;
-    int pad_;
-};
-
 // Tiling of the stitch kernel (must match the kernel): a block is 256 px x 8 rows, one row per
 // wave, 4 consecutive pixels per lane.
 constexpr int kPx = 4;             // output pixels per lane
@@ -62,10 +55,48 @@ constexpr int kWavesPerBlock = 8;  // one row per wave
 constexpr int kTileW = kPx * kWave;
 constexpr int kTileH = kWavesPerBlock;
 
-// LDS of one block: a header (per-camera footprint and layout) and two staging buffers.
-constexpr int kLdsHeader = 1024;
-constexpr int kLdsBuf = 19456;     // bytes of source footprint one capture may occupy
+// Prepared per-plan tables (mcs_plan_prepare): one TileHdr per 256 x 8 tile, and per pixel of the
+// tile three u32 -- the LDS byte addresses of its two row windows (16 bits each) and the packed
+// u16 weight pairs (w00, w01), (w10, w11) -- stored thread-major so each lane loads its 4 pixels
+// as 48 contiguous bytes.
+constexpr int kTileCams = 4;       // cameras one LDS tile may draw from
+constexpr int kTilePx = kTileW * kTileH;
+constexpr int kDescWords = 3;
+struct TileHdr {
+    int fits;                      // 1: LDS path, 0: listed for the direct-gather launch
+    int ncam, njobs, ring, buf_bytes;
+    int cam[kTileCams], rmin[kTileCams], cal[kTileCams], stride[kTileCams], base[kTileCams];
+    int jobstart[kTileCams + 1];
+    int pad_[2];
+};
+static_assert(sizeof(TileHdr) == 128, "TileHdr layout");
+
+// Kernarg blocks.
+struct KPrepareArgs {
+    KParams P;
+    TileHdr *tiles;
+    uint32_t *desc;
+    int *fallback;                 // [0] = count, then tile indices
+};
+struct KStreamArgs {
+    KParams P;
+    const TileHdr *tiles;
+    const uint32_t *desc;
+    int n_frames;
+    int pad_;
+};
+struct KDirectArgs {
+    KParams P;
+    const int *fallback;
+    int n_frames;
+    int pad_;
+};
+
+// LDS of a streaming block: the tile header, then a ring of capture footprints, as many slots (up
+// to kMaxRing, at least 2) as fit in kLdsRing bytes.
+constexpr int kLdsRing = 40832;
 constexpr int kLdsSlack = 16;      // window reads run up to 8 bytes past a row's last byte
-constexpr int kLdsBytes = kLdsHeader + 2 * (kLdsBuf + kLdsSlack);
+constexpr int kMaxRing = 4;
+constexpr int kLdsStream = (int)sizeof(TileHdr) + kLdsRing;   // 40960 bytes: 4 blocks per CU
 
 }  // namespace mcs
