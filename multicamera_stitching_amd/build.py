@@ -59,13 +59,20 @@ def _run(cmd, verbose):
     subprocess.check_call(cmd)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
+def build(force: bool = False, verbose: bool = False, lib: str = None, defines=()) -> str:
+    """Builds libmcs.so (or, for kernel experiments, a variant at `lib` with extra -D defines)."""
+    if lib is not None:
+        return _build_to(lib, HSACO + "." + os.path.basename(lib), list(defines), verbose)
     if not force and not _stale():
         return LIB
-    _run([HIPCC, *DEVICE_FLAGS, *INC, "-o", HSACO + ".tmp", os.path.join(CSRC, DEVICE_SRC)],
-         verbose)
+    return _build_to(LIB, HSACO, [], verbose)
+
+
+def _build_to(LIB: str, HSACO: str, defines, verbose: bool) -> str:
+    _run([HIPCC, *DEVICE_FLAGS, *["-D" + d for d in defines], *INC, "-o", HSACO + ".tmp",
+          os.path.join(CSRC, DEVICE_SRC)], verbose)
     os.replace(HSACO + ".tmp", HSACO)
-    blob = os.path.join(HERE, "mcs_blob.S")
+    blob = LIB + ".blob.S"
     with open(blob, "w") as f:
         f.write('    .section .rodata\n    .balign 4096\n    .globl mcs_hsaco_start\n'
                 'mcs_hsaco_start:\n    .incbin "%s"\n    .globl mcs_hsaco_end\n'

@@ -30,6 +30,8 @@ namespace rt {
     X(hipStreamDestroy, hipError_t, (hipStream_t))                                             \
     X(hipStreamSynchronize, hipError_t, (hipStream_t))                                         \
     X(hipEventCreate, hipError_t, (hipEvent_t *))                                              \
+    X(hipEventCreateWithFlags, hipError_t, (hipEvent_t *, unsigned int))                       \
+    X(hipStreamWaitEvent, hipError_t, (hipStream_t, hipEvent_t, unsigned int))                 \
     X(hipEventDestroy, hipError_t, (hipEvent_t))                                               \
     X(hipEventRecord, hipError_t, (hipEvent_t, hipStream_t))                                   \
     X(hipEventSynchronize, hipError_t, (hipEvent_t))                                           \

@@ -30,6 +30,9 @@ struct mcs_plan {
     mcs::TileHdr *d_tiles = nullptr;
     uint32_t *d_desc = nullptr;
     int *d_fallback = nullptr;
+    // side stream for the direct-gather tiles, forked from / joined to the caller's stream
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 };
 
 #define MCS_VERSION_STRING "mcs 0.1.0 (gfx950 code object, HIP module launch)"
@@ -194,6 +197,25 @@ int prepare(const Api *A, mcs_plan *p, hipStream_t s)
 int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams &P, int n_frames,
                 hipStream_t s)
 {
+    // the few direct-gather tiles run on the side stream, concurrently with the streaming kernel
+    if (p->n_fallback > 0) {
+        HIP_TRY(A->hipEventRecord(p->ev_fork, s));
+        HIP_TRY(A->hipStreamWaitEvent(p->side, p->ev_fork, 0));
+        mcs::KDirectArgs args;
+        args.P = P;
+        const bool off32 = offset_base(p, args.P, &args.P.base);
+        args.fallback = p->d_fallback;
+        args.n_frames = n_frames;
+        args.pad_ = 0;
+        size_t sz = sizeof(args);
+        void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, (void *)&args, HIP_LAUNCH_PARAM_BUFFER_SIZE,
+                       &sz, HIP_LAUNCH_PARAM_END};
+        const unsigned gy = (unsigned)((n_frames + mcs::kDirectFrames - 1) / mcs::kDirectFrames);
+        HIP_TRY(A->hipModuleLaunchKernel(k->direct[p->fd.channels][p->fd.interp][off32 ? 1 : 0],
+                                         p->n_fallback, gy, 1, mcs::kWave, mcs::kWavesPerBlock, 1,
+                                         0, p->side, nullptr, cfg));
+        HIP_TRY(A->hipEventRecord(p->ev_join, p->side));
+    }
     {
         mcs::KStreamArgs args;
         args.P = P;
@@ -204,23 +226,23 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
         size_t sz = sizeof(args);
         void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, (void *)&args, HIP_LAUNCH_PARAM_BUFFER_SIZE,
                        &sz, HIP_LAUNCH_PARAM_END};
-        HIP_TRY(A->hipModuleLaunchKernel(k->stream[p->fd.channels], p->gx, p->gy, 1, mcs::kWave,
+        // 1-D grid dealt over the 8 XCDs; the kernel maps block -> tile (XCD-contiguous bands)
+        const unsigned n_tiles = (unsigned)(p->gx * p->gy);
+        const unsigned grid = 8u * ((n_tiles + 7u) / 8u);
+        HIP_TRY(A->hipModuleLaunchKernel(k->stream[p->fd.channels], grid, 1, 1, mcs::kWave,
                                          mcs::kWavesPerBlock, 1, mcs::kLdsStream, s, nullptr, cfg));
     }
-    if (p->n_fallback > 0) {
-        mcs::KDirectArgs args;
-        args.P = P;
-        const bool off32 = offset_base(p, args.P, &args.P.base);
-        args.fallback = p->d_fallback;
-        args.n_frames = n_frames;
-        args.pad_ = 0;
-        size_t sz = sizeof(args);
-        void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, (void *)&args, HIP_LAUNCH_PARAM_BUFFER_SIZE,
-                       &sz, HIP_LAUNCH_PARAM_END};
-        HIP_TRY(A->hipModuleLaunchKernel(k->direct[p->fd.channels][p->fd.interp][off32 ? 1 : 0],
-                                         p->n_fallback, 1, 1, mcs::kWave, mcs::kWavesPerBlock, 1,
-                                         0, s, nullptr, cfg));
-    }
+    if (p->n_fallback > 0) HIP_TRY(A->hipStreamWaitEvent(s, p->ev_join, 0));
+    return MCS_OK;
+}
+
+// Side stream + fork/join events for the direct-gather tiles (created once per plan).
+int ensure_side(const Api *A, mcs_plan *p)
+{
+    if (p->n_fallback == 0 || p->side) return MCS_OK;
+    HIP_TRY(A->hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming));
+    HIP_TRY(A->hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming));
+    HIP_TRY(A->hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking));
     return MCS_OK;
 }
 
@@ -231,6 +253,8 @@ int launch_stitch(const Api *A, mcs_plan *p, const mcs::KParams &kp, int n_frame
     int rc = kernels(A, p->device, &k);
     if (rc) return rc;
     rc = prepare(A, p, s);
+    if (rc) return rc;
+    rc = ensure_side(A, p);
     if (rc) return rc;
     // the kernels walk the batch with one frame stride for every camera: split otherwise
     bool uniform = true;
@@ -301,7 +325,7 @@ int mcs_plan_create(const mcs_stage_desc *stages, int n_stages, int cam0_w, int 
 int mcs_plan_destroy(mcs_plan *p)
 {
     if (!p) return MCS_OK;
-    bool touched = p->stream || p->d_out || p->d_tiles;
+    bool touched = p->stream || p->d_out || p->d_tiles || p->side;
     for (int i = 0; i < MCS_MAX_CAMS; i++) touched = touched || p->d_cams[i];
     if (touched) {
         const Api *A = mcs::rt::api();
@@ -314,7 +338,11 @@ int mcs_plan_destroy(mcs_plan *p)
             if (p->d_tiles) (void)A->hipFree(p->d_tiles);
             if (p->d_desc) (void)A->hipFree(p->d_desc);
             if (p->d_fallback) (void)A->hipFree(p->d_fallback);
+            if (p->side) (void)A->hipStreamSynchronize(p->side);
             if (p->stream) (void)A->hipStreamDestroy(p->stream);
+            if (p->side) (void)A->hipStreamDestroy(p->side);
+            if (p->ev_fork) (void)A->hipEventDestroy(p->ev_fork);
+            if (p->ev_join) (void)A->hipEventDestroy(p->ev_join);
         }
     }
     delete p;

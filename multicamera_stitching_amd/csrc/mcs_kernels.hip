@@ -324,7 +324,8 @@ __device__ __forceinline__ uint2 shr_bytes(uint2 v, uint32_t n)
 // Direct global-gather path for the 4 pixels at (xg, y): descriptors once, then every capture
 // (frame stride P.cam_fstride[0] for all cameras; the host splits batches that differ).
 template <int CN, int INTERP, bool OFF32>
-__device__ __forceinline__ void stitch_direct(const KParams &P, int n_frames, int xg, int y)
+__device__ __forceinline__ void stitch_direct(const KParams &P, int f0, int n_frames, int xg,
+                                              int y)
 {
     const int npx = min(kPx, P.out_w - xg);
     Desc<OFF32> d[kPx];
@@ -337,7 +338,7 @@ __device__ __forceinline__ void stitch_direct(const KParams &P, int n_frames, in
     const int64_t fstride = P.cam_fstride[0];
     uint8_t *dst = P.out + (int64_t)y * P.out_pitch + (int64_t)xg * CN;
     const bool wide = npx == kPx && (((uintptr_t)dst | (uintptr_t)P.out_fstride) & 3) == 0;
-    for (int f = 0; f < n_frames; f++) {
+    for (int f = f0; f < n_frames; f++) {
         const uint8_t *bf = P.base + (int64_t)f * fstride;
         uint2 r0[kPx], r1[kPx];
 #pragma unroll
@@ -429,7 +430,7 @@ __device__ __forceinline__ void prepare_tile(const KParams &P, TileHdr *tiles, u
     }
     __syncthreads();
     if (tid == 0) {
-        int total = 0, jobs = 0, n = 0, fits = 1;
+        int total = 0, jobs = 0, n = 0, fits = 1, shifts = 0;
         for (int c = 0; c < MCS_MAX_CAMS; c++) {
             if (fl.rmin[c] > fl.rmax[c]) continue;
             if (n == kTileCams) {
@@ -448,6 +449,15 @@ __device__ __forceinline__ void prepare_tile(const KParams &P, TileHdr *tiles, u
             total += rows * stride;
             jobs += rows;
             if (stride > 16 * kWave) fits = 0;
+            // DMA chunks must end inside the camera frame: the frame's last row is fetched from
+            // `e` bytes earlier (the bytes it needs end before the frame end, so they are all
+            // still covered); the preceding bytes must exist
+            const int pitch = P.cam_w[c] * CN;
+            if (fl.rmax[c] == P.cam_h[c] - 1 && cal + stride > pitch) {
+                const int e = cal + stride - pitch;
+                if (e > 255 || (int64_t)fl.rmax[c] * pitch + cal - e < 0) fits = 0;
+                else shifts |= e << (8 * n);
+            }
             n++;
         }
         for (int k = n; k < kTileCams; k++) {
@@ -460,8 +470,10 @@ __device__ __forceinline__ void prepare_tile(const KParams &P, TileHdr *tiles, u
         const int buf = (total + kLdsSlack + 15) & ~15;
         th.buf_bytes = buf;
         th.ring = min(kMaxRing, kLdsRing / buf);
-        th.fits = fits && th.ring >= 2 && total < 65536 - kLdsSlack;
-        th.pad_[0] = th.pad_[1] = 0;
+        th.fits = fits && th.ring >= 2 && total < 65536 - kLdsSlack &&
+                  jobs <= kJobsPerWave * kWavesPerBlock;
+        th.last_shift = shifts;
+        th.pad_ = 0;
         tiles[tile] = th;
         if (!th.fits) fallback[1 + atomicAdd(&fallback[0], 1)] = tile;
     }
@@ -472,8 +484,11 @@ __device__ __forceinline__ void prepare_tile(const KParams &P, TileHdr *tiles, u
         int k = 0;
         while (k < th.ncam - 1 && th.cam[k] != g[p].cam) k++;
         const int st = th.stride[k], rm = th.rmin[k], ca = th.cal[k], bs = th.base[k];
-        uint32_t a0 = (uint32_t)(bs + (g[p].r0 - rm) * st + (g[p].c0 - ca));
-        uint32_t a1 = (uint32_t)(bs + (g[p].r1 - rm) * st + (g[p].c1 - ca));
+        const int last = P.cam_h[g[p].cam] - 1, e = (th.last_shift >> (8 * k)) & 255;
+        uint32_t a0 = (uint32_t)(bs + (g[p].r0 - rm) * st + (g[p].c0 - ca) +
+                                 (g[p].r0 == last ? e : 0));
+        uint32_t a1 = (uint32_t)(bs + (g[p].r1 - rm) * st + (g[p].c1 - ca) +
+                                 (g[p].r1 == last ? e : 0));
         if ((g[p].w0 | g[p].w1) == 0u || !th.fits) a0 = a1 = 0u;
         d[p * kDescWords + 0] = (a0 & 0xffffu) | (a1 << 16);
         d[p * kDescWords + 1] = g[p].w0;
@@ -497,74 +512,101 @@ __device__ __forceinline__ uint2 lds_window(const uint8_t *smem, uint32_t a)
     return r;
 }
 
-// s_waitcnt vmcnt(n) for a run-time n (clamped to 15: waiting for fewer outstanding is stricter).
-__device__ __forceinline__ void wait_vmcnt_le(int n)
-{
-    switch (n < 0 ? 0 : (n > 15 ? 15 : n)) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
-    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
-    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
-    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-    case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
-    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-}
-
-// Issues the LDS-DMA loads of capture f's footprint rows into `slot` (rows split over the block's
-// waves; lanes = 16-byte chunks of a row).  Chunks that would cross the end of a camera frame are
-// copied byte by byte instead (only the bytes inside the frame).
 // Block-uniform value read from LDS (broadcast read + readfirstlane -> SGPR).
 __device__ __forceinline__ int uni(const int &v) { return __builtin_amdgcn_readfirstlane(v); }
 
-// Issues the LDS-DMA loads of capture f's footprint rows into `slot` (rows split over the block's
-// waves; lanes = 16-byte chunks of a row).  Chunks that would cross the end of a camera frame are
-// copied byte by byte instead (only the bytes inside the frame).  h lives in LDS.
+// The LDS-DMA jobs of one wave: its footprint rows (j = wave, wave + 8, ...), resolved once per
+// block into scalar registers (compile-time indexed), so a capture costs one address add and one
+// global_load_lds_dwordx4 per row.  Per row: the frame-0 source address of its first 16-byte
+// chunk and one packed word, LDS offset (bits 0-15) | 16-byte chunks (16-23).  Every chunk lies
+// inside its camera frame (TileHdr::last_shift).
+struct WaveJobs {
+    const uint8_t *src[kJobsPerWave];
+    uint32_t w[kJobsPerWave];
+    int n;
+};
+
 template <int CN>
-__device__ __forceinline__ void stage_capture(const KParams &P, const TileHdr &h, uint8_t *slot,
-                                              int f, int lane, int wave, int njobs)
+__device__ __forceinline__ WaveJobs wave_jobs(const KParams &P, const TileHdr &h, int wave)
 {
-    for (int j = wave; j < njobs; j += kWavesPerBlock) {
-        int k = 0;
-        while (k < kTileCams - 1 && j >= uni(h.jobstart[k + 1])) k++;
-        const int c = uni(h.cam[k]);
-        const int row = j - uni(h.jobstart[k]);
-        const int stride = uni(h.stride[k]);
-        const int64_t pitch = (int64_t)P.cam_w[c] * CN;
-        const int64_t fbytes = pitch * P.cam_h[c];
-        const int64_t goff = (int64_t)(uni(h.rmin[k]) + row) * pitch + uni(h.cal[k]) + 16 * lane;
-        const uint8_t *src = P.cams[c] + (int64_t)f * P.cam_fstride[0];
-        lds_u8 *dst = ((lds_u8 *)slot) + uni(h.base[k]) + row * stride;
-        if (16 * lane < stride) {
-            if (goff + 16 <= fbytes) {
-                __builtin_amdgcn_global_load_lds(src + goff, dst, 16, 0, 0);
-            } else {
-                for (int b = 0; b < 16; b++)
-                    if (goff + b < fbytes) dst[16 * lane + b] = src[goff + b];
-            }
+    WaveJobs J;
+    const int njobs = uni(h.njobs);
+    J.n = 0;
+#pragma unroll
+    for (int jj = 0; jj < kJobsPerWave; jj++) {
+        const int j = wave + jj * kWavesPerBlock;
+        J.src[jj] = nullptr;
+        J.w[jj] = 0;
+        if (j < njobs) {
+            int k = 0;
+            while (k < kTileCams - 1 && j >= uni(h.jobstart[k + 1])) k++;
+            const int c = uni(h.cam[k]);
+            const int row = j - uni(h.jobstart[k]);
+            const int stride = uni(h.stride[k]);
+            const int64_t pitch = (int64_t)P.cam_w[c] * CN;
+            const int r = uni(h.rmin[k]) + row;
+            const int e = r == P.cam_h[c] - 1 ? (uni(h.last_shift) >> (8 * k)) & 255 : 0;
+            J.src[jj] = P.cams[c] + (int64_t)r * pitch + uni(h.cal[k]) - e;
+            J.w[jj] = (uint32_t)(uni(h.base[k]) + row * stride) | ((uint32_t)(stride >> 4) << 16);
+            J.n = jj + 1;
+        }
+    }
+    return J;
+}
+
+// Issues capture f's footprint rows into `slot`: one LDS-DMA wave instruction per row (lane =
+// 16-byte chunk).
+__device__ __forceinline__ void stage_capture(const WaveJobs &J, uint8_t *slot, int64_t foff,
+                                              int lane)
+{
+#pragma unroll
+    for (int jj = 0; jj < kJobsPerWave; jj++) {
+        if (jj < J.n) {
+            const uint32_t w = J.w[jj];
+            // LDS destination: wave-uniform row base (M0); the hardware adds 16 * lane
+            if (lane < (int)(w >> 16))
+                __builtin_amdgcn_global_load_lds(J.src[jj] + foff + 16 * lane,
+                                                 ((lds_u8 *)slot) + (w & 0xffffu), 16, 0, 0);
         }
     }
 }
 
+// s_waitcnt vmcnt(n) + lgkmcnt(0) for a block-uniform run-time n (n clamped to 11 by the caller;
+// waiting for fewer outstanding operations is always safe).
+__device__ __forceinline__ void wait_vmcnt_le(int n)
+{
+    switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7) lgkmcnt(0)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9) lgkmcnt(0)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(11) lgkmcnt(0)" ::: "memory"); break;
+    }
+}
+
+// grid (8 * ceil(tiles / 8)), block (64, 8).  XCD-aware tile order: workgroups are dealt
+// round-robin over the 8 XCDs (b % 8 share one), so XCD x gets the contiguous band of tiles
+// [x * per, (x+1) * per), walked row-major; vertically adjacent tiles, whose footprints overlap
+// by a few source rows, then run at about the same time on the same L2.  (Placement affects
+// speed only.)
 template <int CN>
 __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *tiles,
                                             const uint32_t *desc, int n_frames, uint8_t *smem)
 {
-    // threadIdx.y is the wave index (blockDim.x == 64): make that provable to the compiler so
-    // job/camera lookups stay scalar and the LDS-DMA base (M0) needs no waterfall
     const int lane = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(threadIdx.y);
     const int tid = wave * kWave + lane;
-    const int tile = blockIdx.y * gridDim.x + blockIdx.x;
+    const int gx = (P.out_w + kTileW - 1) / kTileW, gy = (P.out_h + kTileH - 1) / kTileH;
+    const int n_tiles = gx * gy, per = (n_tiles + 7) >> 3;
+    const int tile = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+    if (tile >= n_tiles) return;
+    const int bx = tile % gx, by = tile / gx;
     // the tile header, copied once into LDS (the kernel also stores to global memory, so the
     // compiler cannot serve `tiles` from the scalar cache)
     TileHdr &h = *reinterpret_cast<TileHdr *>(smem);
@@ -573,8 +615,8 @@ __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *til
         reinterpret_cast<int *>(&h)[tid] = reinterpret_cast<const int *>(&tiles[tile])[tid];
     __syncthreads();
     if (!uni(h.fits)) return;                  // handled by the direct-gather launch
-    const int xg = (blockIdx.x * kWave + lane) * kPx;
-    const int y = blockIdx.y * kTileH + wave;
+    const int xg = (bx * kWave + lane) * kPx;
+    const int y = by * kTileH + wave;
     const bool live = xg < P.out_w && y < P.out_h;
     const int npx = live ? min(kPx, P.out_w - xg) : 0;
     uint32_t d[kPx * kDescWords];
@@ -590,24 +632,28 @@ __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *til
             d[4 * i + 3] = v.w;
         }
     }
+    const WaveJobs J = wave_jobs<CN>(P, h, wave);
     const int ring = uni(h.ring), buf_bytes = uni(h.buf_bytes), njobs = uni(h.njobs);
-    // VMEM instructions this wave issues per capture: D footprint rows (LDS-DMA), S >= 1 store
-    const int D = wave < njobs ? (njobs - 1 - wave) / kWavesPerBlock + 1 : 0;
-    const int S = y < P.out_h ? 1 : 0;
+    const int d_min = njobs / kWavesPerBlock;
+    const int s_all = (by + 1) * kTileH <= P.out_h ? 1 : 0;   // every wave stores each capture
+    const int waitn = min((ring - 2) * (d_min + s_all) + s_all, 11);
     uint8_t *dst = P.out + (int64_t)min(y, P.out_h - 1) * P.out_pitch + (int64_t)xg * CN;
     const bool wide = npx == kPx && (((uintptr_t)dst | (uintptr_t)P.out_fstride) & 3) == 0;
-
-    // Stream the captures through the ring: while capture f is gathered from slot f % ring,
-    // captures f+1 .. f+ring-1 are in flight.  One barrier per capture.
+    const int64_t fstride = P.cam_fstride[0];
     for (int q = 0; q < ring - 1 && q < n_frames; q++)
-        stage_capture<CN>(P, h, ring0 + q * buf_bytes, q, lane, wave, njobs);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        stage_capture(J, ring0 + q * buf_bytes, (int64_t)q * fstride, lane);
+    wait_vmcnt_le(0);
     __builtin_amdgcn_s_barrier();
+    // Steady state: WAITN = VMEM instructions this wave has certainly issued after the DMA of
+    // capture f+1 ((ring-2) later captures x (D_min rows + S_all stores) + this capture's S_all
+    // stores); vmcnt counts in issue order, so vmcnt(WAITN) means capture f+1 has landed for
+    // this wave, and the barrier makes it so for the block.  Tail captures wait for everything.
+    int slot_f = 0, slot_a = ring - 1;     // slots of capture f and of capture f + ring - 1
     for (int f = 0; f < n_frames; f++) {
         const int ahead = f + ring - 1;
-        if (ahead < n_frames)
-            stage_capture<CN>(P, h, ring0 + (ahead % ring) * buf_bytes, ahead, lane, wave, njobs);
-        const uint8_t *b = ring0 + (f % ring) * buf_bytes;
+        const bool full = ahead < n_frames;
+        if (full) stage_capture(J, ring0 + slot_a * buf_bytes, (int64_t)ahead * fstride, lane);
+        const uint8_t *b = ring0 + slot_f * buf_bytes;
         if (live) {
             OutWords w;
 #pragma unroll
@@ -633,26 +679,27 @@ __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *til
                     o[bb] = (uint8_t)(w.at(bb >> 2) >> (8 * (bb & 3)));
             }
         }
-        // Capture f+1 must have landed before the barrier; later captures' DMA may stay in
-        // flight.  vmcnt counts this wave's VMEM instructions in issue order: younger than
-        // DMA(f+1) are at least, per later iteration, its D DMA + S store instructions, and this
-        // iteration's S stores -> waiting for "<= younger" outstanding is exact or stricter.
-        const int younger = min(n_frames - 1 - f, ring - 2) * (D + S) + S;
-        wait_vmcnt_le(f + 1 < n_frames ? younger : 0);
+        wait_vmcnt_le(full ? waitn : 0);
         __builtin_amdgcn_s_barrier();
+        slot_f = slot_f + 1 == ring ? 0 : slot_f + 1;
+        slot_a = slot_a + 1 == ring ? 0 : slot_a + 1;
     }
 }
 
-// Direct global gather for the tiles prepare could not fit in LDS (list in fallback[1..]).
+// Direct global gather for the tiles prepare could not fit in LDS (list in fallback[1..]):
+// grid (tiles, ceil(frames / kDirectFrames)), launched on a side stream next to the streaming
+// kernel, so these few tiles cost no extra time on the critical path.
 template <int CN, int INTERP, bool OFF32>
 __device__ __forceinline__ void direct_tile(const KParams &P, const int *fallback, int n_frames)
 {
     const int tile = fallback[1 + blockIdx.x];
+    const int f0 = blockIdx.y * kDirectFrames;
     const int gx = (P.out_w + kTileW - 1) / kTileW;
     const int tx = tile % gx, ty = tile / gx;
     const int xg = (tx * kWave + threadIdx.x) * kPx;
     const int y = ty * kTileH + threadIdx.y;
-    if (xg < P.out_w && y < P.out_h) stitch_direct<CN, INTERP, OFF32>(P, n_frames, xg, y);
+    if (xg < P.out_w && y < P.out_h)
+        stitch_direct<CN, INTERP, OFF32>(P, f0, min(n_frames, f0 + kDirectFrames), xg, y);
 }
 
 // Footprint marking: mask[cam][pixel] = 1 for every source pixel the mosaic reads with a
@@ -697,9 +744,9 @@ __device__ __forceinline__ void footprint_mark(const KParams &P, uint8_t *const 
 }  // namespace mcs
 
 // ---------------------------------------------------------------------------------------------
-// Entry points (names looked up by mcs_capi.cpp).  Block shapes: prepare and stream (64, 8, 1)
-// over the tile grid (ceil(out_w/256), ceil(out_h/8)), stream with kLdsRing bytes of dynamic
-// LDS; direct (64, 8, 1) over the fallback tile list; footprint (256, 1, 1) with grid
+// Entry points (names looked up by mcs_capi.cpp).  Block shapes: prepare (64, 8, 1) over the tile
+// grid (ceil(out_w/256), ceil(out_h/8)); stream (64, 8, 1) over 8 * ceil(tiles / 8) blocks with
+// kLdsStream bytes of dynamic LDS; direct (64, 8, 1) over the fallback tile list; footprint (256, 1, 1) with grid
 // (ceil(out_w/256), out_h).
 #define MCS_PREPARE_ENTRY(CN, IN)                                                              \
     extern "C" __global__ __launch_bounds__(512) void mcs_prepare_c##CN##_i##IN(               \
@@ -707,8 +754,13 @@ __device__ __forceinline__ void footprint_mark(const KParams &P, uint8_t *const 
     {                                                                                          \
         mcs::prepare_tile<CN, IN>(P, tiles, desc, fallback);                                   \
     }
+#ifdef MCS_STREAM_WAVES_PER_EU   // experiment knob: occupancy target of the streaming kernel
+#define MCS_STREAM_ATTR __attribute__((amdgpu_waves_per_eu(MCS_STREAM_WAVES_PER_EU)))
+#else
+#define MCS_STREAM_ATTR
+#endif
 #define MCS_STREAM_ENTRY(CN)                                                                   \
-    extern "C" __global__ __launch_bounds__(512) void mcs_stream_c##CN(                        \
+    extern "C" __global__ __launch_bounds__(512) MCS_STREAM_ATTR void mcs_stream_c##CN(        \
         const mcs::KParams P, const mcs::TileHdr *tiles, const uint32_t *desc, int n_frames)  \
     {                                                                                          \
         extern __shared__ __attribute__((aligned(16))) uint8_t smem[];                         \

@@ -67,7 +67,11 @@ struct TileHdr {
     int ncam, njobs, ring, buf_bytes;
     int cam[kTileCams], rmin[kTileCams], cal[kTileCams], stride[kTileCams], base[kTileCams];
     int jobstart[kTileCams + 1];
-    int pad_[2];
+    // per camera slot k, byte k: how far the DMA of the camera frame's LAST row starts earlier
+    // than cal, so its last 16-byte chunk ends at the frame end (0: no shift); pixels reading
+    // that row add it to their LDS window address
+    int last_shift;
+    int pad_;
 };
 static_assert(sizeof(TileHdr) == 128, "TileHdr layout");
 
@@ -95,6 +99,8 @@ struct KDirectArgs {
 // LDS of a streaming block: the tile header, then a ring of capture footprints, as many slots (up
 // to kMaxRing, at least 2) as fit in kLdsRing bytes.
 constexpr int kLdsRing = 40832;
+constexpr int kDirectFrames = 4;    // captures per direct-gather block
+constexpr int kJobsPerWave = 4;     // footprint rows per wave per capture (more rows -> direct path)
 constexpr int kLdsSlack = 16;      // window reads run up to 8 bytes past a row's last byte
 constexpr int kMaxRing = 4;
 constexpr int kLdsStream = (int)sizeof(TileHdr) + kLdsRing;   // 40960 bytes: 4 blocks per CU
