@@ -37,7 +37,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--frames", type=int, default=32, help="rig captures per launch (per GPU)")
+    ap.add_argument("--frames", type=int, default=64,
+                    help="rig captures per launch (per GPU); SURVEY.md 8d: >= 64 per launch")
     ap.add_argument("--cams", type=int, default=4)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)

@@ -79,7 +79,7 @@ def _build_to(LIB: str, HSACO: str, defines, verbose: bool) -> str:
                 'mcs_hsaco_end:\n    .byte 0\n    .section .note.GNU-stack,"",@progbits\n'
                 % HSACO)
     try:
-        _run([CXX, *HOST_FLAGS, *INC, "-o", LIB + ".tmp",
+        _run([CXX, *HOST_FLAGS, *["-D" + d for d in defines], *INC, "-o", LIB + ".tmp",
               *[os.path.join(CSRC, s) for s in HOST_SRC], blob, "-ldl", "-lpthread"], verbose)
     finally:
         os.remove(blob)

@@ -230,7 +230,8 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
         const unsigned n_tiles = (unsigned)(p->gx * p->gy);
         const unsigned grid = 8u * ((n_tiles + 7u) / 8u);
         HIP_TRY(A->hipModuleLaunchKernel(k->stream[p->fd.channels], grid, 1, 1, mcs::kWave,
-                                         mcs::kWavesPerBlock, 1, mcs::kLdsStream, s, nullptr, cfg));
+                                         mcs::kWavesPerBlock, 1,
+                                         mcs::lds_stream_bytes(p->fd.channels), s, nullptr, cfg));
     }
     if (p->n_fallback > 0) HIP_TRY(A->hipStreamWaitEvent(s, p->ev_join, 0));
     return MCS_OK;

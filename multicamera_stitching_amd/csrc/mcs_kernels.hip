@@ -379,12 +379,19 @@ __device__ __forceinline__ void stitch_direct(const KParams &P, int f0, int n_fr
 // one source footprint per camera (rows x 16-byte chunks: the union of all its row windows),
 // lays the footprints out as one LDS slot, and stores a TileHdr plus each pixel's LDS window
 // addresses and weights.  Tiles that do not fit (more than kTileCams cameras, a slot larger than
-// kLdsRing / 2, rows wider than 1 KiB) are listed for the direct-gather kernel instead.
+// half the ring, rows wider than 1 KiB) are listed for the direct-gather kernel instead.
 //
 // stream (every launch): per capture, each footprint row is ONE global_load_lds_dwordx4 wave
 // instruction (LDS-DMA: wide, contiguous, no registers) into a ring of slots, several captures in
 // flight; pixels read their 8-byte windows from LDS with aligned ds_read2_b32 + ds_read_b32 and
 // v_alignbyte, blend with v_dot2_u32_u16, and store 12 contiguous bytes per lane.
+
+// Output pixel group of (lane, wave) in tile (bx, by): first pixel column xg, row y.
+__device__ __forceinline__ void tile_pixel(int bx, int by, int lane, int wave, int &xg, int &y)
+{
+    xg = (bx * kLanesPerRow + lane % kLanesPerRow) * kPx;
+    y = by * kTileH + wave * kRowsPerWave + lane / kLanesPerRow;
+}
 
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
@@ -402,8 +409,8 @@ __device__ __forceinline__ void prepare_tile(const KParams &P, TileHdr *tiles, u
     const int lane = threadIdx.x, wave = threadIdx.y;
     const int tid = wave * kWave + lane;
     const int tile = blockIdx.y * gridDim.x + blockIdx.x;
-    const int xg = (blockIdx.x * kWave + lane) * kPx;
-    const int y = blockIdx.y * kTileH + wave;
+    int xg, y;
+    tile_pixel(blockIdx.x, blockIdx.y, lane, wave, xg, y);
     const bool live = xg < P.out_w && y < P.out_h;
     const int npx = live ? min(kPx, P.out_w - xg) : 0;
     if (tid < MCS_MAX_CAMS) {
@@ -469,7 +476,7 @@ __device__ __forceinline__ void prepare_tile(const KParams &P, TileHdr *tiles, u
         th.njobs = jobs;
         const int buf = (total + kLdsSlack + 15) & ~15;
         th.buf_bytes = buf;
-        th.ring = min(kMaxRing, kLdsRing / buf);
+        th.ring = min(kMaxRing, lds_ring_bytes(CN) / buf);
         th.fits = fits && th.ring >= 2 && total < 65536 - kLdsSlack &&
                   jobs <= kJobsPerWave * kWavesPerBlock;
         th.last_shift = shifts;
@@ -511,6 +518,15 @@ __device__ __forceinline__ uint2 lds_window(const uint8_t *smem, uint32_t a)
     r.y = __builtin_amdgcn_alignbyte(x2, x1, sh);
     return r;
 }
+
+// Experiment knobs: cache policy of the footprint DMA (aux bits: 2 = nt) and of mosaic stores.
+#ifndef MCS_DMA_AUX
+#define MCS_DMA_AUX 0
+#endif
+#ifndef MCS_STORE_NT
+#define MCS_STORE_NT 0
+#endif
+
 
 // Block-uniform value read from LDS (broadcast read + readfirstlane -> SGPR).
 __device__ __forceinline__ int uni(const int &v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -566,12 +582,13 @@ __device__ __forceinline__ void stage_capture(const WaveJobs &J, uint8_t *slot, 
             // LDS destination: wave-uniform row base (M0); the hardware adds 16 * lane
             if (lane < (int)(w >> 16))
                 __builtin_amdgcn_global_load_lds(J.src[jj] + foff + 16 * lane,
-                                                 ((lds_u8 *)slot) + (w & 0xffffu), 16, 0, 0);
+                                                 ((lds_u8 *)slot) + (w & 0xffffu), 16, 0,
+                                                 MCS_DMA_AUX);
         }
     }
 }
 
-// s_waitcnt vmcnt(n) + lgkmcnt(0) for a block-uniform run-time n (n clamped to 11 by the caller;
+// s_waitcnt vmcnt(n) + lgkmcnt(0) for a block-uniform run-time n (n clamped to 15 by the caller;
 // waiting for fewer outstanding operations is always safe).
 __device__ __forceinline__ void wait_vmcnt_le(int n)
 {
@@ -587,7 +604,11 @@ __device__ __forceinline__ void wait_vmcnt_le(int n)
     case 8: asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory"); break;
     case 9: asm volatile("s_waitcnt vmcnt(9) lgkmcnt(0)" ::: "memory"); break;
     case 10: asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(11) lgkmcnt(0)" ::: "memory"); break;
+    case 11: asm volatile("s_waitcnt vmcnt(11) lgkmcnt(0)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)" ::: "memory"); break;
+    case 13: asm volatile("s_waitcnt vmcnt(13) lgkmcnt(0)" ::: "memory"); break;
+    case 14: asm volatile("s_waitcnt vmcnt(14) lgkmcnt(0)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(15) lgkmcnt(0)" ::: "memory"); break;
     }
 }
 
@@ -615,8 +636,8 @@ __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *til
         reinterpret_cast<int *>(&h)[tid] = reinterpret_cast<const int *>(&tiles[tile])[tid];
     __syncthreads();
     if (!uni(h.fits)) return;                  // handled by the direct-gather launch
-    const int xg = (bx * kWave + lane) * kPx;
-    const int y = by * kTileH + wave;
+    int xg, y;
+    tile_pixel(bx, by, lane, wave, xg, y);
     const bool live = xg < P.out_w && y < P.out_h;
     const int npx = live ? min(kPx, P.out_w - xg) : 0;
     uint32_t d[kPx * kDescWords];
@@ -635,8 +656,7 @@ __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *til
     const WaveJobs J = wave_jobs<CN>(P, h, wave);
     const int ring = uni(h.ring), buf_bytes = uni(h.buf_bytes), njobs = uni(h.njobs);
     const int d_min = njobs / kWavesPerBlock;
-    const int s_all = (by + 1) * kTileH <= P.out_h ? 1 : 0;   // every wave stores each capture
-    const int waitn = min((ring - 2) * (d_min + s_all) + s_all, 11);
+    const int waitn = min((ring - 2) * d_min, 15);
     uint8_t *dst = P.out + (int64_t)min(y, P.out_h - 1) * P.out_pitch + (int64_t)xg * CN;
     const bool wide = npx == kPx && (((uintptr_t)dst | (uintptr_t)P.out_fstride) & 3) == 0;
     const int64_t fstride = P.cam_fstride[0];
@@ -644,10 +664,12 @@ __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *til
         stage_capture(J, ring0 + q * buf_bytes, (int64_t)q * fstride, lane);
     wait_vmcnt_le(0);
     __builtin_amdgcn_s_barrier();
-    // Steady state: WAITN = VMEM instructions this wave has certainly issued after the DMA of
-    // capture f+1 ((ring-2) later captures x (D_min rows + S_all stores) + this capture's S_all
-    // stores); vmcnt counts in issue order, so vmcnt(WAITN) means capture f+1 has landed for
-    // this wave, and the barrier makes it so for the block.  Tail captures wait for everything.
+    // Steady state: waitn = DMA instructions this wave has certainly issued after those of
+    // capture f+1 ((ring-2) later captures x D_min rows).  The DMAs (loads) complete in issue
+    // order among themselves, so with at most waitn VMEM operations of any kind outstanding,
+    // capture f+1 has landed for this wave (stores are not counted: loads and stores may complete
+    // out of order with respect to each other); the barrier makes it so for the block.  Tail
+    // captures wait for everything.
     int slot_f = 0, slot_a = ring - 1;     // slots of capture f and of capture f + ring - 1
     for (int f = 0; f < n_frames; f++) {
         const int ahead = f + ring - 1;
@@ -673,7 +695,13 @@ __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *til
             if (wide) {
                 uint32_t *o32 = reinterpret_cast<uint32_t *>(o);
 #pragma unroll
-                for (int i = 0; i < CN; i++) o32[i] = w.at(i);
+                for (int i = 0; i < CN; i++) {
+#if MCS_STORE_NT
+                    __builtin_nontemporal_store(w.at(i), &o32[i]);
+#else
+                    o32[i] = w.at(i);
+#endif
+                }
             } else {
                 for (int bb = 0; bb < npx * CN; bb++)
                     o[bb] = (uint8_t)(w.at(bb >> 2) >> (8 * (bb & 3)));
@@ -696,8 +724,8 @@ __device__ __forceinline__ void direct_tile(const KParams &P, const int *fallbac
     const int f0 = blockIdx.y * kDirectFrames;
     const int gx = (P.out_w + kTileW - 1) / kTileW;
     const int tx = tile % gx, ty = tile / gx;
-    const int xg = (tx * kWave + threadIdx.x) * kPx;
-    const int y = ty * kTileH + threadIdx.y;
+    int xg, y;
+    tile_pixel(tx, ty, threadIdx.x, threadIdx.y, xg, y);
     if (xg < P.out_w && y < P.out_h)
         stitch_direct<CN, INTERP, OFF32>(P, f0, min(n_frames, f0 + kDirectFrames), xg, y);
 }
@@ -746,7 +774,8 @@ __device__ __forceinline__ void footprint_mark(const KParams &P, uint8_t *const 
 // ---------------------------------------------------------------------------------------------
 // Entry points (names looked up by mcs_capi.cpp).  Block shapes: prepare (64, 8, 1) over the tile
 // grid (ceil(out_w/256), ceil(out_h/8)); stream (64, 8, 1) over 8 * ceil(tiles / 8) blocks with
-// kLdsStream bytes of dynamic LDS; direct (64, 8, 1) over the fallback tile list; footprint (256, 1, 1) with grid
+// lds_stream_bytes(CN) of dynamic LDS; direct (64, 8, 1) over the fallback tile list; footprint
+// (256, 1, 1) with grid
 // (ceil(out_w/256), out_h).
 #define MCS_PREPARE_ENTRY(CN, IN)                                                              \
     extern "C" __global__ __launch_bounds__(512) void mcs_prepare_c##CN##_i##IN(               \

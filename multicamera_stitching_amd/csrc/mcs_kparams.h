@@ -47,15 +47,22 @@ struct KFootprintArgs {
     unsigned long long *counts;
 };
 
-// Tiling of the stitch kernel (must match the kernel): a block is 256 px x 8 rows, one row per
-// wave, 4 consecutive pixels per lane.
+// Tiling of the stitch kernel (host and device share it): a block is 8 waves; a wave covers
+// kRowsPerWave output rows of kWave / kRowsPerWave lanes, 4 consecutive pixels per lane.  Taller
+// tiles re-fetch fewer source rows (the footprints of vertically adjacent tiles overlap by the
+// bilinear row and the homography's slant); tools/footprint_model.py.
+#ifndef MCS_ROWS_PER_WAVE
+#define MCS_ROWS_PER_WAVE 2
+#endif
 constexpr int kPx = 4;             // output pixels per lane
 constexpr int kWave = 64;
-constexpr int kWavesPerBlock = 8;  // one row per wave
-constexpr int kTileW = kPx * kWave;
-constexpr int kTileH = kWavesPerBlock;
+constexpr int kWavesPerBlock = 8;
+constexpr int kRowsPerWave = MCS_ROWS_PER_WAVE;
+constexpr int kLanesPerRow = kWave / kRowsPerWave;
+constexpr int kTileW = kPx * kLanesPerRow;
+constexpr int kTileH = kWavesPerBlock * kRowsPerWave;
 
-// Prepared per-plan tables (mcs_plan_prepare): one TileHdr per 256 x 8 tile, and per pixel of the
+// Prepared per-plan tables (mcs_plan_prepare): one TileHdr per tile, and per pixel of the
 // tile three u32 -- the LDS byte addresses of its two row windows (16 bits each) and the packed
 // u16 weight pairs (w00, w01), (w10, w11) -- stored thread-major so each lane loads its 4 pixels
 // as 48 contiguous bytes.
@@ -96,13 +103,15 @@ struct KDirectArgs {
     int pad_;
 };
 
-// LDS of a streaming block: the tile header, then a ring of capture footprints, as many slots (up
-// to kMaxRing, at least 2) as fit in kLdsRing bytes.
-constexpr int kLdsRing = 40832;
 constexpr int kDirectFrames = 4;    // captures per direct-gather block
-constexpr int kJobsPerWave = 4;     // footprint rows per wave per capture (more rows -> direct path)
+constexpr int kJobsPerWave = 2 + 2 * kRowsPerWave;   // footprint rows per wave per capture
+                                                    // (more rows -> direct path)
 constexpr int kLdsSlack = 16;      // window reads run up to 8 bytes past a row's last byte
-constexpr int kMaxRing = 4;
-constexpr int kLdsStream = (int)sizeof(TileHdr) + kLdsRing;   // 40960 bytes: 4 blocks per CU
+constexpr int kMaxRing = 6;
+// LDS of a streaming block: the tile header, then a ring of capture footprints, as many slots
+// (2..kMaxRing) as fit.  Sized per channel count to the occupancy the kernel's registers allow:
+// 3 blocks per CU for 3-4 channels (52 KiB each of the CU's 160 KiB), 4 for 1-2 channels.
+constexpr int lds_stream_bytes(int cn) { return cn >= 3 ? 53248 : 40960; }
+constexpr int lds_ring_bytes(int cn) { return lds_stream_bytes(cn) - (int)sizeof(TileHdr); }
 
 }  // namespace mcs

@@ -1,0 +1,63 @@
+"""Summarise tools/gpu_pmc.sh output: per-launch averages of every counter for the streaming
+kernel, HBM bytes per launch (FETCH_SIZE x 2 per the gfx950 correction in MI355X_MICROARCH.md,
++ WRITE_SIZE; both KiB-denominated), derived ratios.  Writes profiles/pmc_latest.json (read by
+bench.py's roofline.traffic when the workload matches) and prints a text summary."""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PMC = os.path.join(ROOT, "gpurun_out", "pmc")
+
+
+def main(kernel_prefix="mcs_stream_c3", workload=None, out=None):
+    vals = defaultdict(lambda: defaultdict(float))     # dispatch -> counter -> summed value
+    names = {}
+    for f in sorted(glob.glob(os.path.join(PMC, "pass*", "**", "*counter_collection.csv"),
+                              recursive=True)):
+        p = f.split(os.sep)[len(PMC.split(os.sep))]
+        for r in csv.DictReader(open(f)):
+            if not r["Kernel_Name"].startswith(kernel_prefix):
+                continue
+            key = (p, int(r["Dispatch_Id"]))
+            vals[key][r["Counter_Name"]] += float(r["Counter_Value"])
+            names[key] = r["Kernel_Name"]
+    per_counter = defaultdict(list)
+    for key, cs in vals.items():
+        for c, v in cs.items():
+            per_counter[c].append(v)
+    avg = {c: sum(v) / len(v) for c, v in per_counter.items()}
+    res = {"kernel": kernel_prefix, "workload": workload, "counters_per_launch": avg}
+    if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
+        fetch = avg["FETCH_SIZE"] * 1024 * 2
+        write = avg["WRITE_SIZE"] * 1024
+        res.update(fetch_bytes_per_launch=fetch, write_bytes_per_launch=write,
+                   hbm_bytes_per_launch=int(fetch + write))
+    if "SQ_WAVE_CYCLES" in avg:
+        wc = avg["SQ_WAVE_CYCLES"]
+        for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU",
+                  "SQ_ACTIVE_INST_LDS"):
+            if c in avg:
+                res[c + "_frac"] = avg[c] / wc
+    if "SQ_WAVES" in avg:
+        for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD",
+                  "SQ_INSTS_VMEM_WR", "SQ_INSTS_SMEM"):
+            if c in avg:
+                res[c + "_per_wave"] = avg[c] / avg["SQ_WAVES"]
+    if "SQ_LDS_BANK_CONFLICT" in avg and "SQ_LDS_IDX_ACTIVE" in avg:
+        res["lds_bank_conflict_frac"] = avg["SQ_LDS_BANK_CONFLICT"] / max(avg["SQ_LDS_IDX_ACTIVE"], 1)
+    if "TCC_HIT_sum" in avg:
+        res["l2_hit_rate"] = avg["TCC_HIT_sum"] / max(avg["TCC_HIT_sum"] + avg["TCC_MISS_sum"], 1)
+    text = json.dumps(res, indent=1, sort_keys=True)
+    print(text)
+    if out:
+        with open(out, "w") as f:
+            f.write(text + "\n")
+
+
+if __name__ == "__main__":
+    wl = sys.argv[1] if len(sys.argv) > 1 else "4x1920x1080x3-linear-super0-F64"
+    main(workload=wl, out=os.path.join(ROOT, "profiles", "pmc_latest.json"))
