@@ -113,6 +113,22 @@ int mcs_plan_stats(const mcs_plan *plan, int64_t *stats, int n);
  * buffer.  Synchronous: H2D -> kernel -> D2H on the plan's stream. */
 int mcs_stitch_host(mcs_plan *plan, const uint8_t *const *cams, uint8_t *out);
 
+/* The same with the frames' actual sizes (cam_w[i] x cam_h[i], same channel count): a frame off
+ * its calibrated size is first resized to it on the device with cv2.resize(INTER_LINEAR)
+ * arithmetic, as StitcherBase.stitch does before warping (StitcherClass.py:226-233).  NULL
+ * cam_w/cam_h = calibrated sizes (== mcs_stitch_host). */
+int mcs_stitch_host_sized(mcs_plan *plan, const uint8_t *const *cams, const int *cam_w,
+                          const int *cam_h, uint8_t *out);
+
+/* cv2.resize(src, (dst_w, dst_h), interpolation=cv2.INTER_LINEAR) (replaces the call at
+ * StitcherClass.py:229,233) on n_frames device-resident u8 images of `channels` interleaved
+ * channels; frame f of src starts at d_src + f*src_frame_stride (0 = src_pitch*src_h), rows at
+ * src_pitch; likewise dst.  Same size = copy (as OpenCV).  Enqueued on `stream` of `device`. */
+int mcs_resize_linear_device(const uint8_t *d_src, int src_w, int src_h, int64_t src_pitch,
+                             int64_t src_frame_stride, uint8_t *d_dst, int dst_w, int dst_h,
+                             int64_t dst_pitch, int64_t dst_frame_stride, int channels,
+                             int n_frames, int device, void *stream);
+
 /* Device-resident batch: n_frames rigs.  d_cams[i] + f*cam_frame_stride[i] is frame f of camera
  * i (dense rows, pitch = w*C); d_out + f*out_frame_stride + y*out_pitch is output row y of frame
  * f.  Enqueued on `stream` (a hipStream_t of the process's HIP runtime; NULL = the null

@@ -202,7 +202,6 @@ class Stitcher(_Transient, Debugger):
         cams = [images_dic[label] for label in self.img_labels]
         if all(sb.cachedAH is None for sb in self.stitchers):
             return cams[0]   # every stage returns its B unchanged (:255-256)
-        cams = _conform_cameras(self, self.stitchers, cams)
         return _run_chain(self, self.stitchers, cams)
 
     # ------------------------------------------------------------------ persistence
@@ -283,8 +282,7 @@ class StitcherBase(_Transient, Debugger):
             return imageB
         if draw_descriptors:
             _warn_draw(self)
-        cams = _conform_cameras(self, [self], [imageB, imageA])
-        return _run_chain(self, [self], cams)
+        return _run_chain(self, [self], [imageB, imageA])
 
     def calibrate(self, images, ratio=0.75, reprojThresh=4.0, xoffset=10, yoffset=10,
                   homography=None, use_features=True):
@@ -380,40 +378,43 @@ def _get_plan(owner, chain, cam0_shape, channels, interp=None, device=None):
 
 
 def _conform_cameras(owner, chain, cams):
-    """Apply the reference's shape checks (:226-233) to the chain's camera inputs.
+    """The reference's shape checks (:226-233) for the chain's inputs.
 
-    Inputs of the calibrated (h, w) that differ only in channel count go through unchanged:
-    cv2.resize to the same size is a copy.  A true size mismatch needs the INTER_LINEAR resize
-    pre-pass, which is not on the GPU yet.
+    A frame whose shape differs from its calibrated one is logged as the reference logs it and is
+    resized on the GPU to the calibrated (h, w) with cv2.resize(INTER_LINEAR) arithmetic, keeping
+    its channel count (a same-size "resize" is a copy).  Returns the frames, the calibrated
+    (h, w) of camera 0, and each frame's (w, h).
     """
     ch = {_channels(c) for c in cams}
     if len(ch) != 1:
         raise ValueError("cameras with different channel counts cannot be pasted together "
                          "(numpy broadcast error in the reference)")
-    out = []
-    for i, c in enumerate(cams):
-        if i == 0:
-            want = chain[0].BimgSize if chain[0].cachedAH is not None else None
-        else:
-            sb = chain[i - 1]
-            want = sb.AimgSize if sb.cachedAH is not None else None
-        if want is not None and tuple(c.shape) != tuple(want):
-            if tuple(c.shape[:2]) != tuple(want[:2]):
-                owner.debugger(DEBUG_LEVEL_0, "[STITCHER] image {} size {} should be {}".format(
-                    i, c.shape, want), log_type="warn")
-                raise NotImplementedError(
-                    "camera size {} differs from calibrated {}: the cv2.resize(INTER_LINEAR) "
-                    "pre-pass is not implemented on the GPU path yet".format(c.shape, want))
-        out.append(c)
-    return out
+    tail = tuple(cams[0].shape[2:])         # () for 2-D frames, (C,) for H x W x C
+    cam0_hw = None
+    b_shape = tuple(cams[0].shape)          # what imageB is at each stage
+    for k, sb in enumerate(chain):
+        if sb.cachedAH is None:
+            continue                         # passthrough: returns B untouched (:255-256)
+        if cam0_hw is None:
+            cam0_hw = tuple(sb.BimgSize[:2])
+        if b_shape != tuple(sb.BimgSize):
+            owner.debugger(DEBUG_LEVEL_0, "[STITCHER][{}] ImageB size should be {}, Image will be "
+                           "resized".format(sb.sid, sb.BimgSize), log_type="warn")
+        a = cams[k + 1]
+        if tuple(a.shape) != tuple(sb.AimgSize):
+            owner.debugger(DEBUG_LEVEL_0, "[STITCHER][{}] ImageA size should be {}, Image will be "
+                           "resized".format(sb.sid, sb.AimgSize), log_type="warn")
+        b_shape = _stage_out_shape(sb, _shape_only(tuple(sb.BimgSize[:2]) + tail))
+    sizes = [(int(c.shape[1]), int(c.shape[0])) for c in cams]
+    return cams, cam0_hw, sizes
 
 
 def _run_chain(owner, chain, cams):
+    cams, cam0_hw, sizes = _conform_cameras(owner, chain, cams)
     cache = owner._cache()
     with cache.lock:
-        cam0_shape = cams[0].shape
-        plan = _get_plan(owner, chain, cam0_shape, _channels(cams[0]))
-        return plan.stitch_host(cams)
+        plan = _get_plan(owner, chain, cam0_hw, _channels(cams[0]))
+        return plan.stitch_host(cams, sizes)
 
 
 def _stage_out_shape(sb, imageB):

@@ -31,7 +31,7 @@ EXPORTS = (
     "mcs_version", "mcs_abi_version", "mcs_last_error", "mcs_device_count", "mcs_hip_runtime",
     "mcs_plan_create", "mcs_plan_destroy", "mcs_plan_out_shape", "mcs_plan_describe",
     "mcs_stitch_host", "mcs_stitch_device", "mcs_plan_footprint", "mcs_plan_prepare",
-    "mcs_plan_stats",
+    "mcs_plan_stats", "mcs_stitch_host_sized", "mcs_resize_linear_device",
 )
 
 
@@ -155,6 +155,12 @@ def load() -> ctypes.CDLL:
         L.mcs_plan_describe.restype = I
         L.mcs_stitch_host.argtypes = [P, ctypes.POINTER(P), P]
         L.mcs_stitch_host.restype = I
+        L.mcs_stitch_host_sized.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(I),
+                                            ctypes.POINTER(I), P]
+        L.mcs_stitch_host_sized.restype = I
+        i64 = ctypes.c_int64
+        L.mcs_resize_linear_device.argtypes = [P, I, I, i64, i64, P, I, I, i64, i64, I, I, I, P]
+        L.mcs_resize_linear_device.restype = I
         L.mcs_stitch_device.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_int64), P,
                                         ctypes.c_int64, ctypes.c_int64, I, P]
         L.mcs_stitch_device.restype = I
@@ -249,12 +255,21 @@ class Plan:
             "cam_h": [fd.cam_h[i] for i in range(fd.n_cams)],
         }
 
-    def stitch_host(self, cams) -> np.ndarray:
-        """cams: list of dense u8 arrays of the calibrated shapes (sorted-label order)."""
+    def stitch_host(self, cams, sizes=None) -> np.ndarray:
+        """cams: dense u8 arrays in sorted-label order.  sizes: their (w, h) when some differ
+        from the calibrated ones (those are resized on the device first, :226-233)."""
         cams = [np.ascontiguousarray(c, dtype=np.uint8) for c in cams]
         out = np.empty(self.out_shape(), np.uint8)
         ptrs = (ctypes.c_void_p * len(cams))(*[c.ctypes.data for c in cams])
-        check(self._lib.mcs_stitch_host(self._h, ptrs, out.ctypes.data_as(ctypes.c_void_p)))
+        outp = out.ctypes.data_as(ctypes.c_void_p)
+        fd = self.flat
+        if sizes is None or all((w, h) == (fd.cam_w[i], fd.cam_h[i])
+                                for i, (w, h) in enumerate(sizes)):
+            check(self._lib.mcs_stitch_host(self._h, ptrs, outp))
+        else:
+            ws = (ctypes.c_int * len(sizes))(*[int(w) for w, _ in sizes])
+            hs = (ctypes.c_int * len(sizes))(*[int(h) for _, h in sizes])
+            check(self._lib.mcs_stitch_host_sized(self._h, ptrs, ws, hs, outp))
         return out
 
     def stitch_device(self, cam_ptrs, cam_frame_strides, out_ptr: int, out_pitch: int,
@@ -281,3 +296,15 @@ class Plan:
         arr = (ctypes.c_int64 * MCS_MAX_CAMS)()
         check(self._lib.mcs_plan_footprint(self._h, arr, MCS_MAX_CAMS))
         return [int(arr[i]) for i in range(self.n_cams)]
+
+
+def resize_linear_device(src_ptr: int, src_w: int, src_h: int, dst_ptr: int, dst_w: int,
+                         dst_h: int, channels: int, n_frames: int = 1, src_pitch: int = 0,
+                         dst_pitch: int = 0, src_frame_stride: int = 0,
+                         dst_frame_stride: int = 0, device: int = 0, stream: int = 0):
+    """cv2.resize(..., interpolation=INTER_LINEAR) of device-resident u8 images (mcs.h)."""
+    L = load()
+    check(L.mcs_resize_linear_device(
+        src_ptr, src_w, src_h, src_pitch or src_w * channels, src_frame_stride, dst_ptr, dst_w,
+        dst_h, dst_pitch or dst_w * channels, dst_frame_stride, channels, n_frames, device,
+        stream or None))

@@ -33,6 +33,9 @@ struct mcs_plan {
     // side stream for the direct-gather tiles, forked from / joined to the caller's stream
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    // host path with frames off their calibrated size: upload buffers for the resize pre-pass
+    uint8_t *d_raw[MCS_MAX_CAMS] = {};
+    size_t raw_bytes[MCS_MAX_CAMS] = {};
 };
 
 #define MCS_VERSION_STRING "mcs 0.1.0 (gfx950 code object, HIP module launch)"
@@ -56,6 +59,7 @@ struct Kernels {
     hipFunction_t stream[5] = {};         // [channels]
     hipFunction_t direct[5][2][2] = {};   // [channels][interp][32-bit offsets]
     hipFunction_t footprint[2] = {};
+    hipFunction_t resize[5] = {};         // [channels]
 };
 Kernels g_k[kMaxDevices];
 std::mutex g_k_mu;
@@ -73,6 +77,8 @@ int kernels(const Api *A, int device, const Kernels **out)
         for (int c = 1; c <= 4; c++) {
             snprintf(name, sizeof(name), "mcs_stream_c%d", c);
             HIP_TRY(A->hipModuleGetFunction(&k.stream[c], m, name));
+            snprintf(name, sizeof(name), "mcs_resize_c%d", c);
+            HIP_TRY(A->hipModuleGetFunction(&k.resize[c], m, name));
             for (int i = 0; i < 2; i++) {
                 snprintf(name, sizeof(name), "mcs_prepare_c%d_i%d", c, i);
                 HIP_TRY(A->hipModuleGetFunction(&k.prepare[c][i], m, name));
@@ -247,6 +253,41 @@ int ensure_side(const Api *A, mcs_plan *p)
     return MCS_OK;
 }
 
+// cv2.resize(INTER_LINEAR) of n_frames device images (same size: OpenCV copies).
+int launch_resize(const Api *A, const Kernels *k, const uint8_t *src, int sw, int sh,
+                  int64_t src_pitch, int64_t src_fstride, uint8_t *dst, int dw, int dh,
+                  int64_t dst_pitch, int64_t dst_fstride, int C, int n_frames, hipStream_t s)
+{
+    if (sw == dw && sh == dh) {
+        for (int f = 0; f < n_frames; f++)
+            HIP_TRY(A->hipMemcpy2DAsync(dst + f * dst_fstride, (size_t)dst_pitch,
+                                        src + f * src_fstride, (size_t)src_pitch, (size_t)dw * C,
+                                        dh, hipMemcpyDeviceToDevice, s));
+        return MCS_OK;
+    }
+    mcs::KResizeArgs a;
+    a.src = src;
+    a.dst = dst;
+    a.src_pitch = src_pitch;
+    a.src_fstride = src_fstride;
+    a.dst_pitch = dst_pitch;
+    a.dst_fstride = dst_fstride;
+    a.scale_x = 1. / ((double)dw / sw);
+    a.scale_y = 1. / ((double)dh / sh);
+    a.sw = sw;
+    a.sh = sh;
+    a.dw = dw;
+    a.dh = dh;
+    a.n_frames = n_frames;
+    a.area2x = a.scale_x == 2. && a.scale_y == 2.;
+    size_t sz = sizeof(a);
+    void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, (void *)&a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz,
+                   HIP_LAUNCH_PARAM_END};
+    HIP_TRY(A->hipModuleLaunchKernel(k->resize[C], (dw + mcs::kResizeBlock - 1) / mcs::kResizeBlock,
+                                     dh, n_frames, mcs::kResizeBlock, 1, 1, 0, s, nullptr, cfg));
+    return MCS_OK;
+}
+
 int launch_stitch(const Api *A, mcs_plan *p, const mcs::KParams &kp, int n_frames, hipStream_t s)
 {
     if (kp.out_w <= 0 || kp.out_h <= 0 || n_frames <= 0) return MCS_OK;
@@ -336,6 +377,8 @@ int mcs_plan_destroy(mcs_plan *p)
             for (int i = 0; i < MCS_MAX_CAMS; i++)
                 if (p->d_cams[i]) (void)A->hipFree(p->d_cams[i]);
             if (p->d_out) (void)A->hipFree(p->d_out);
+            for (int i = 0; i < MCS_MAX_CAMS; i++)
+                if (p->d_raw[i]) (void)A->hipFree(p->d_raw[i]);
             if (p->d_tiles) (void)A->hipFree(p->d_tiles);
             if (p->d_desc) (void)A->hipFree(p->d_desc);
             if (p->d_fallback) (void)A->hipFree(p->d_fallback);
@@ -368,6 +411,12 @@ int mcs_plan_describe(const mcs_plan *p, mcs_flat_desc *out)
 
 int mcs_stitch_host(mcs_plan *p, const uint8_t *const *cams, uint8_t *out)
 {
+    return mcs_stitch_host_sized(p, cams, nullptr, nullptr, out);
+}
+
+int mcs_stitch_host_sized(mcs_plan *p, const uint8_t *const *cams, const int *cam_w,
+                          const int *cam_h, uint8_t *out)
+{
     mcs::clear_error();
     if (!p || !cams || !out) return mcs::fail(MCS_E_INVALID, "NULL plan/cams/out");
     const Api *A = mcs::rt::api();
@@ -381,14 +430,39 @@ int mcs_stitch_host(mcs_plan *p, const uint8_t *const *cams, uint8_t *out)
     rc = ensure_host_buffers(A, p);
     if (rc) return rc;
     if (p->fd.out_w <= 0 || p->fd.out_h <= 0) return MCS_OK;
-    // only cameras that contribute are uploaded (a passthrough stage's A is never read)
+    const Kernels *k = nullptr;
+    rc = kernels(A, p->device, &k);
+    if (rc) return rc;
+    // only cameras that contribute are uploaded (a passthrough stage's A is never read); a frame
+    // off its calibrated size is resized on the device first (StitcherClass.py:226-233)
     bool need[MCS_MAX_CAMS];
     need_mask(p->fd, need);
     for (int i = 0; i < p->fd.n_cams; i++) {
         if (!need[i]) continue;
         if (!cams[i]) return mcs::fail(MCS_E_INVALID, "cams[%d] NULL", i);
-        const size_t bytes = (size_t)p->fd.cam_w[i] * p->fd.cam_h[i] * C;
-        HIP_TRY(A->hipMemcpyAsync(p->d_cams[i], cams[i], bytes, hipMemcpyHostToDevice, p->stream));
+        const int cw = p->fd.cam_w[i], ch = p->fd.cam_h[i];
+        const int w = cam_w ? cam_w[i] : cw, h = cam_h ? cam_h[i] : ch;
+        if (w <= 0 || h <= 0) return mcs::fail(MCS_E_INVALID, "cams[%d] size %dx%d", i, w, h);
+        if (w == cw && h == ch) {
+            HIP_TRY(A->hipMemcpyAsync(p->d_cams[i], cams[i], (size_t)cw * ch * C,
+                                      hipMemcpyHostToDevice, p->stream));
+            continue;
+        }
+        const size_t bytes = (size_t)w * h * C;
+        if (p->raw_bytes[i] < bytes) {
+            if (p->d_raw[i]) {
+                HIP_TRY(A->hipStreamSynchronize(p->stream));
+                HIP_TRY(A->hipFree(p->d_raw[i]));
+                p->d_raw[i] = nullptr;
+                p->raw_bytes[i] = 0;
+            }
+            HIP_TRY(A->hipMalloc((void **)&p->d_raw[i], bytes));
+            p->raw_bytes[i] = bytes;
+        }
+        HIP_TRY(A->hipMemcpyAsync(p->d_raw[i], cams[i], bytes, hipMemcpyHostToDevice, p->stream));
+        rc = launch_resize(A, k, p->d_raw[i], w, h, (int64_t)w * C, 0, p->d_cams[i], cw, ch,
+                           (int64_t)cw * C, 0, C, 1, p->stream);
+        if (rc) return rc;
     }
     mcs::KParams kp = p->kp;
     for (int i = 0; i < p->fd.n_cams; i++) {
@@ -405,6 +479,35 @@ int mcs_stitch_host(mcs_plan *p, const uint8_t *const *cams, uint8_t *out)
                                 hipMemcpyDeviceToHost, p->stream));
     HIP_TRY(A->hipStreamSynchronize(p->stream));
     return MCS_OK;
+}
+
+int mcs_resize_linear_device(const uint8_t *d_src, int src_w, int src_h, int64_t src_pitch,
+                             int64_t src_frame_stride, uint8_t *d_dst, int dst_w, int dst_h,
+                             int64_t dst_pitch, int64_t dst_frame_stride, int channels,
+                             int n_frames, int device, void *stream)
+{
+    mcs::clear_error();
+    if (!d_src || !d_dst) return mcs::fail(MCS_E_INVALID, "NULL src/dst");
+    if (channels < 1 || channels > 4) return mcs::fail(MCS_E_UNSUPPORTED, "channels=%d", channels);
+    if (src_w <= 0 || src_h <= 0 || dst_w <= 0 || dst_h <= 0)
+        return mcs::fail(MCS_E_INVALID, "sizes %dx%d -> %dx%d", src_w, src_h, dst_w, dst_h);
+    if (dst_h > 65535 || n_frames < 0 || n_frames > 65535)
+        return mcs::fail(MCS_E_INVALID, "dst_h=%d n_frames=%d", dst_h, n_frames);
+    if (src_pitch < (int64_t)src_w * channels || dst_pitch < (int64_t)dst_w * channels)
+        return mcs::fail(MCS_E_INVALID, "pitch smaller than a row");
+    if (n_frames == 0) return MCS_OK;
+    const Api *A = mcs::rt::api();
+    if (!A) return MCS_E_HIP;
+    DeviceGuard g(A, device);
+    if (g.err != hipSuccess)
+        return mcs::fail(MCS_E_HIP, "hipSetDevice(%d): %s", device, A->hipGetErrorString(g.err));
+    const Kernels *k = nullptr;
+    int rc = kernels(A, device, &k);
+    if (rc) return rc;
+    const int64_t sfs = src_frame_stride ? src_frame_stride : src_pitch * src_h;
+    const int64_t dfs = dst_frame_stride ? dst_frame_stride : dst_pitch * dst_h;
+    return launch_resize(A, k, d_src, src_w, src_h, src_pitch, sfs, d_dst, dst_w, dst_h, dst_pitch,
+                         dfs, channels, n_frames, (hipStream_t)stream);
 }
 
 int mcs_stitch_device(mcs_plan *p, const uint8_t *const *d_cams, const int64_t *cam_frame_stride,

@@ -769,6 +769,62 @@ __device__ __forceinline__ void footprint_mark(const KParams &P, uint8_t *const 
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// cv2.resize(src, (dw, dh), interpolation=INTER_LINEAR) for u8 images: the reference's pre-warp
+// resize of frames that do not have their calibrated shape (StitcherClass.py:226-233).  OpenCV
+// 3.4 resize.cpp arithmetic (restated in oracle/orc_resize.c): per-axis source index and 11-bit
+// coefficients from float coordinates (computed here exactly as on the host: IEEE double, then
+// float, no contraction), horizontal taps into int, vertical pass
+// ((b0 * (D0 >> 4)) >> 16) + ((b1 * (D1 >> 4)) >> 16) + 2 >> 2.  An exact 2x downscale is
+// OpenCV's INTER_AREA fast path.  HBM-bound (reads each source byte ~once through L2, writes
+// the destination once); one thread per destination pixel, all channels.
+__device__ __forceinline__ void resize_axis(int d, double scale, int ssize, bool is_x, int &s,
+                                            int &c0, int &c1)
+{
+    float f = (float)((d + 0.5) * scale - 0.5);
+    int si = (int)floorf(f);
+    f -= (float)si;
+    if (is_x) {
+        if (si < 0) f = 0.f, si = 0;
+        if (si >= ssize - 1) f = 0.f, si = ssize - 1;
+    }
+    s = si;
+    c0 = __float2int_rn((1.f - f) * 2048.f);
+    c1 = __float2int_rn(f * 2048.f);
+}
+
+template <int CN>
+__device__ __forceinline__ void resize_px(const KResizeArgs &a)
+{
+    const int x = blockIdx.x * kResizeBlock + threadIdx.x, y = blockIdx.y, f = blockIdx.z;
+    if (x >= a.dw) return;
+    const uint8_t *src = a.src + (int64_t)f * a.src_fstride;
+    uint8_t *dst = a.dst + (int64_t)f * a.dst_fstride + (int64_t)y * a.dst_pitch + (int64_t)x * CN;
+    if (a.area2x) {
+        const uint8_t *s0 = src + (int64_t)(2 * y) * a.src_pitch + (int64_t)(2 * x) * CN;
+        const uint8_t *s1 = s0 + a.src_pitch;
+#pragma unroll
+        for (int k = 0; k < CN; k++) {
+            const int sum = s0[k] + s0[CN + k] + s1[k] + s1[CN + k];
+            dst[k] = (uint8_t)(CN == 2 ? __float2int_rn((float)sum * 0.25f) : (sum + 2) >> 2);
+        }
+        return;
+    }
+    int sx, a0, a1, sy, b0, b1;
+    resize_axis(x, a.scale_x, a.sw, true, sx, a0, a1);
+    resize_axis(y, a.scale_y, a.sh, false, sy, b0, b1);
+    const int r0 = min(max(sy, 0), a.sh - 1), r1 = min(max(sy + 1, 0), a.sh - 1);
+    const uint8_t *p0 = src + (int64_t)r0 * a.src_pitch + (int64_t)sx * CN;
+    const uint8_t *p1 = src + (int64_t)r1 * a.src_pitch + (int64_t)sx * CN;
+    const bool one = sx >= a.sw - 1;
+#pragma unroll
+    for (int k = 0; k < CN; k++) {
+        const int d0 = one ? p0[k] * 2048 : p0[k] * a0 + p0[CN + k] * a1;
+        const int d1 = one ? p1[k] * 2048 : p1[k] * a0 + p1[CN + k] * a1;
+        dst[k] = (uint8_t)((((b0 * (d0 >> 4)) >> 16) + ((b1 * (d1 >> 4)) >> 16) + 2) >> 2);
+    }
+}
+
 }  // namespace mcs
 
 // ---------------------------------------------------------------------------------------------
@@ -813,6 +869,17 @@ MCS_ENTRIES(1)
 MCS_ENTRIES(2)
 MCS_ENTRIES(3)
 MCS_ENTRIES(4)
+
+// grid (ceil(dw / kResizeBlock), dh, n_frames), block (kResizeBlock)
+#define MCS_RESIZE_ENTRY(CN)                                                                   \
+    extern "C" __global__ __launch_bounds__(256) void mcs_resize_c##CN(const mcs::KResizeArgs a) \
+    {                                                                                          \
+        mcs::resize_px<CN>(a);                                                                 \
+    }
+MCS_RESIZE_ENTRY(1)
+MCS_RESIZE_ENTRY(2)
+MCS_RESIZE_ENTRY(3)
+MCS_RESIZE_ENTRY(4)
 
 extern "C" __global__ __launch_bounds__(256) void mcs_footprint_i0(const mcs::KParams P,
                                                                    uint8_t *const *masks,

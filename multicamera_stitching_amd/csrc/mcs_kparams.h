@@ -103,6 +103,18 @@ struct KDirectArgs {
     int pad_;
 };
 
+// cv2.resize(INTER_LINEAR) pre-pass (StitcherClass.py:226-233): n_frames images per launch.
+struct KResizeArgs {
+    const uint8_t *src;
+    uint8_t *dst;
+    int64_t src_pitch, src_fstride, dst_pitch, dst_fstride;
+    double scale_x, scale_y;       // 1. / ((double)dst / src), as OpenCV computes them
+    int sw, sh, dw, dh;
+    int n_frames;
+    int area2x;                    // exact 2x downscale: OpenCV switches to INTER_AREA's 2x2 mean
+};
+constexpr int kResizeBlock = 256;
+
 constexpr int kDirectFrames = 4;    // captures per direct-gather block
 constexpr int kJobsPerWave = 2 + 2 * kRowsPerWave;   // footprint rows per wave per capture
                                                     // (more rows -> direct path)

@@ -1,4 +1,5 @@
-"""TEST INFRASTRUCTURE ONLY -- ctypes wrapper around the CPU restatement in mcs_oracle.c.
+"""TEST INFRASTRUCTURE ONLY -- ctypes wrapper around the CPU restatements in mcs_oracle.c and
+orc_resize.c.
 
 Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module;
 the product path (multicamera_stitching_amd) never does.  See mcs_oracle.c for what each
@@ -61,6 +62,10 @@ def lib():
         L.orc_bilinear_weights.argtypes = [ctypes.c_int, ctypes.c_int, P]
         L.orc_num_threads.restype = ctypes.c_int
         L.orc_set_num_threads.argtypes = [ctypes.c_int]
+        L.orc_resize_linear.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_long,
+                                        ctypes.c_int, P, ctypes.c_int, ctypes.c_int, ctypes.c_long]
+        L.orc_resize_linear.restype = ctypes.c_int
+        L.orc_resize_axis.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P]
         _lib = L
     return _lib
 
@@ -110,6 +115,26 @@ def warp_perspective(src: np.ndarray, M, dsize, interp: int = INTER_LINEAR,
     lib().orc_warp_perspective(_p(src), sw, sh, sw * cn, cn, _p(dst), W, H, W * cn, _p(m),
                                interp, 1 if inverse_map else 0)
     return dst
+
+
+def resize_linear(src: np.ndarray, dsize) -> np.ndarray:
+    """cv2.resize(src, dsize=(W, H), interpolation=cv2.INTER_LINEAR) (orc_resize.c)."""
+    src = np.ascontiguousarray(src, dtype=np.uint8)
+    cn = 1 if src.ndim == 2 else src.shape[2]
+    sh, sw = src.shape[:2]
+    W, H = int(dsize[0]), int(dsize[1])
+    dst = np.zeros((H, W, cn) if src.ndim == 3 else (H, W), np.uint8)
+    if lib().orc_resize_linear(_p(src), sw, sh, sw * cn, cn, _p(dst), W, H, W * cn) != 0:
+        raise ValueError("orc_resize_linear failed")
+    return dst
+
+
+def resize_axis(ssize: int, dsize: int, is_x: bool):
+    """OpenCV resize() per-axis source index and 11-bit coefficient pairs."""
+    ofs = np.zeros(dsize, np.int32)
+    coef = np.zeros(2 * dsize, np.int16)
+    lib().orc_resize_axis(ssize, dsize, 1 if is_x else 0, _p(ofs), _p(coef))
+    return ofs, coef.reshape(dsize, 2)
 
 
 def _stage_array(stages):

@@ -11,9 +11,10 @@ geometry (cachedAH patch, Apts/Bpts, ABSize, super-mode limits), the chain order
 crop semantics, the passthrough branch and the pickle layout.
 
 What is substituted (the reference's third-party dependencies, absent from this image):
-  * cv2.warpPerspective -> the CPU restatement oracle/mcs_oracle.c (bilinear, BORDER_CONSTANT 0).
+  * cv2.warpPerspective -> the CPU restatement oracle/mcs_oracle.c (bilinear, BORDER_CONSTANT 0),
+    cv2.resize(INTER_LINEAR) -> oracle/orc_resize.c (each call's shapes are recorded).
     So the *pixel arithmetic* in these fixtures is our restatement of OpenCV 3.4, not OpenCV;
-    the fixtures pin the orchestration around it.
+    the fixtures pin the orchestration around it (which frames are resized, to what size, when).
   * SIFT / BF matcher / findHomography: detectAndDescribe and matchKeypoints are replaced so that
     each stage receives a chosen homography (the inputs recorded in the fixture).
   * extended_rospylogs.Debugger: a no-op logger.
@@ -48,6 +49,9 @@ class Py2Dict(dict):
         return list(super().keys())
 
 
+RESIZE_LOG = []
+
+
 def _install_stubs():
     erl = types.ModuleType("extended_rospylogs")
 
@@ -76,8 +80,11 @@ def _install_stubs():
         return oracle.warp_perspective(src, np.asarray(M, np.float64), dsize,
                                        interp=flags & 7 if flags is not None else 1)
 
-    def resize(*a, **k):
-        raise RuntimeError("cv2.resize reached: fixture inputs must have calibrated sizes")
+    def resize(src, dsize, dst=None, fx=None, fy=None, interpolation=1):
+        # the reference's pre-warp resize (StitcherClass.py:226-233) -> CPU restatement
+        assert interpolation == cv2.INTER_LINEAR and fx is None and fy is None
+        RESIZE_LOG.append({"src": list(src.shape), "dsize": [int(dsize[0]), int(dsize[1])]})
+        return oracle.resize_linear(src, dsize)
 
     cv2.warpPerspective = warpPerspective
     cv2.resize = resize
@@ -97,8 +104,11 @@ def load_reference():
     return mod
 
 
-def run_case(SC, name, frames, labels, super_mode, provider, pickle_out=None):
-    """provider(stage_index, stitcher) -> H (or None for a failed match)."""
+def run_case(SC, name, frames, labels, super_mode, provider, pickle_out=None,
+             stitch_frames=None):
+    """provider(stage_index, stitcher) -> H (or None for a failed match).  stitch_frames: the
+    frames passed to Stitcher.stitch after calibrating on `frames` (default: the same); frames
+    off their calibrated shape take the reference's cv2.resize branch."""
     images = Py2Dict(zip(labels, frames))
     st = SC.Stitcher(images, super_mode=super_mode)
     stage_of = {s.sid: i for i, s in enumerate(st.stitchers)}
@@ -119,7 +129,10 @@ def run_case(SC, name, frames, labels, super_mode, provider, pickle_out=None):
     SC.StitcherBase.detectAndDescribe = detectAndDescribe
     SC.StitcherBase.matchKeypoints = matchKeypoints
     st.calibrate_stitcher(images, save=pickle_out is not None, save_path=pickle_out or "")
-    out = st.stitch(images)
+    del RESIZE_LOG[:]
+    out = st.stitch(Py2Dict(zip(labels, stitch_frames)) if stitch_frames is not None else images)
+    resize_calls = list(RESIZE_LOG)
+    assert stitch_frames is not None or not resize_calls
     stages = []
     for i, s in enumerate(st.stitchers):
         d = {"sid": s.sid, "H_in": raw_H.get(i)}
@@ -149,8 +162,11 @@ def run_case(SC, name, frames, labels, super_mode, provider, pickle_out=None):
         "stages": stages,
         "out_shape": list(out.shape),
         "str": [str(s) for s in st.stitchers],
+        "resize_calls": resize_calls,
     }
     arrays = {"cam%d" % i: f for i, f in enumerate(frames)}
+    if stitch_frames is not None:
+        arrays.update({"scam%d" % i: f for i, f in enumerate(stitch_frames)})
     arrays["out"] = np.ascontiguousarray(out)
     np.savez_compressed(os.path.join(HERE, name + ".npz"), **arrays)
     with open(os.path.join(HERE, name + ".json"), "w") as f:
@@ -218,6 +234,21 @@ def main():
     Hs10 = [[[1.02, 0.01, 9.5], [0.0, 0.99, 1.25], [1e-3, 0.0, 1.0]]]
     f10 = rig.make_frames(2, 20, 10, 3, seed=10)
     run_case(SC, "tiny_blocks", f10, ["CAM1", "CAM2"], False, list_provider(Hs10))
+    # 11-13: frames off their calibrated shape -> the reference's cv2.resize(INTER_LINEAR)
+    # branch (StitcherClass.py:226-233) before each warp
+    C11 = rig.camera_models(3, 72, 48, seed=11, rot_deg=2.0, persp=2e-4)
+    f11 = rig.make_frames(3, 72, 48, 3, seed=11)
+    s11 = [f11[0]] + rig.make_frames(2, 53, 37, 3, seed=111)      # cameras 2, 3 smaller
+    run_case(SC, "resize_up", f11, rig.labels(3), False, rig_provider(C11), stitch_frames=s11)
+    s12 = rig.make_frames(3, 144, 96, 3, seed=112)                # exact 2x: INTER_AREA path
+    run_case(SC, "resize_half", f11, rig.labels(3), True, rig_provider(C11), stitch_frames=s12)
+    # MediaPlayer: 1-channel W x H (transposed) frames against 3-channel calibration
+    # (view.py:409): every stage resizes, the whole chain runs single-channel
+    C13 = rig.camera_models(3, 64, 40, seed=13, rot_deg=1.5, persp=1e-4)
+    f13 = rig.make_frames(3, 64, 40, 3, seed=13)
+    s13 = [np.ascontiguousarray(f.T) for f in rig.make_frames(3, 64, 40, 1, seed=113)]
+    run_case(SC, "resize_transposed_gray", f13, rig.labels(3), False, rig_provider(C13),
+             stitch_frames=s13)
 
 
 if __name__ == "__main__":

@@ -14,10 +14,43 @@ def names():
 
 
 def load(name):
+    """(meta, calibration frames by label, reference output)."""
+    meta, frames, _, out = load_full(name)
+    return meta, frames, out
+
+
+def load_full(name):
+    """(meta, calibration frames, frames passed to Stitcher.stitch, reference output).  The two
+    frame sets differ for the resize cases (frames off their calibrated shape)."""
     meta = json.load(open(os.path.join(GOLDEN, name + ".json")))
     z = np.load(os.path.join(GOLDEN, name + ".npz"))
     frames = {lab: z["cam%d" % i] for i, lab in enumerate(meta["labels"])}
-    return meta, frames, z["out"]
+    stitch = {lab: z["scam%d" % i] if "scam%d" % i in z else frames[lab]
+              for i, lab in enumerate(meta["labels"])}
+    return meta, frames, stitch, z["out"]
+
+
+def calibrated_hw(meta):
+    """Calibrated (h, w) of each camera in sorted-label order (None: never read)."""
+    st = meta["stages"]
+    hw = [None] * (len(st) + 1)
+    for i, s in enumerate(st):
+        if s["calibrated"]:
+            if hw[0] is None:
+                hw[0] = tuple(s["BimgSize"][:2])
+            hw[i + 1] = tuple(s["AimgSize"][:2])
+    return hw
+
+
+def resized_for_oracle(meta, cams):
+    """The frames as the reference's stages see them after its cv2.resize branch (:226-233)."""
+    from oracle import oracle
+    out = []
+    for c, hw in zip(cams, calibrated_hw(meta)):
+        if hw is not None and tuple(c.shape[:2]) != hw:
+            c = oracle.resize_linear(c, (hw[1], hw[0]))
+        out.append(c)
+    return out
 
 
 def sorted_cams(meta, frames):
@@ -42,10 +75,11 @@ def stage_desc(s, meta, cams, i):
     return d
 
 
-def plan_for(meta, cams, interp=1, device=0):
+def plan_for(meta, cams, interp=1, device=0, channels=None):
+    """Plan of the fixture's chain; cams: calibration frames (sorted-label order)."""
     from multicamera_stitching_amd import _capi
     descs = [stage_desc(s, meta, cams, i) for i, s in enumerate(meta["stages"])]
-    ch = 1 if cams[0].ndim == 2 else cams[0].shape[2]
+    ch = channels or (1 if cams[0].ndim == 2 else cams[0].shape[2])
     return _capi.Plan(descs, cams[0].shape[1], cams[0].shape[0], ch, interp, device)
 
 

@@ -26,22 +26,23 @@ def _diff(a, b):
 
 @pytest.mark.parametrize("name", goldens.names())
 def test_golden_via_capi(name):
-    meta, frames, out = goldens.load(name)
+    meta, calib, frames, out = goldens.load_full(name)
     cams = goldens.sorted_cams(meta, frames)
-    plan = goldens.plan_for(meta, cams)
-    got = plan.stitch_host(cams)
-    assert _diff(got, out) == 0
+    ch = 1 if cams[0].ndim == 2 else cams[0].shape[2]
+    plan = goldens.plan_for(meta, goldens.sorted_cams(meta, calib), channels=ch)
+    got = plan.stitch_host(cams, [(c.shape[1], c.shape[0]) for c in cams])
+    assert _diff(got.reshape(out.shape), out) == 0
 
 
 @pytest.mark.parametrize("name", goldens.names())
 def test_golden_via_dropin(name):
     """Calibrate our Stitcher with the fixture's homographies, stitch, compare to the reference."""
     from multicamera_stitching_amd.StitcherClass import Stitcher
-    meta, frames, out = goldens.load(name)
-    st = Stitcher(dict(frames), super_mode=meta["super_mode"])
+    meta, calib, frames, out = goldens.load_full(name)
+    st = Stitcher(dict(calib), super_mode=meta["super_mode"])
     assert [str(v) for v in st.img_labels] == meta["img_labels"]
     Hs = [s["H_in"] for s in meta["stages"]]
-    st.calibrate_stitcher(dict(frames), save=False, homographies=Hs)
+    st.calibrate_stitcher(dict(calib), save=False, homographies=Hs)
     got = st.stitch(dict(frames))
     assert _diff(got, out) == 0
     # the per-stage path (StitcherBase.stitch, used during feature calibration) agrees too
@@ -231,3 +232,53 @@ def test_frame_end_rows_stream_through_lds(ch, w, h):
     for f in range(F):
         want = oracle.cascade_stitch(stages, batch[f], oracle.INTER_LINEAR)
         assert _diff(got[f].reshape(want.shape), want) == 0
+
+
+
+@pytest.mark.parametrize("ch", [1, 2, 3, 4])
+@pytest.mark.parametrize("src,dst", [((53, 37), (72, 48)), ((144, 96), (72, 48)),
+                                     ((40, 64), (64, 40)), ((1080, 1920), (1920, 1080)),
+                                     ((7, 5), (3, 2)), ((31, 17), (31, 17)), ((2, 2), (9, 1))])
+def test_resize_linear_device_vs_oracle(ch, src, dst):
+    """mcs_resize_linear_device == cv2.resize(INTER_LINEAR) restatement: up, down, exact 2x
+    (INTER_AREA path), transposed MediaPlayer frames, tiny, identity -- batch of 3 frames."""
+    import torch
+    from multicamera_stitching_amd import _capi
+    (sw, sh), (dw, dh) = src, dst
+    rng = np.random.default_rng(sw * 7 + dw + ch)
+    F = 3
+    frames = rng.integers(0, 256, (F, sh, sw, ch), dtype=np.uint8)
+    d_src = torch.from_numpy(frames).cuda()
+    d_dst = torch.full((F, dh, dw * ch + 8), 77, dtype=torch.uint8, device="cuda")
+    _capi.resize_linear_device(d_src.data_ptr(), sw, sh, d_dst.data_ptr(), dw, dh, ch,
+                               n_frames=F, dst_pitch=dw * ch + 8,
+                               dst_frame_stride=d_dst[0].numel())
+    torch.cuda.synchronize()
+    got = d_dst.cpu().numpy()
+    for f in range(F):
+        want = oracle.resize_linear(frames[f], (dw, dh)).reshape(dh, dw * ch)
+        assert _diff(got[f, :, :dw * ch], want) == 0
+        assert (got[f, :, dw * ch:] == 77).all()
+
+
+def test_dropin_off_size_frames_resized_on_gpu():
+    """Stitcher.stitch with frames of another size (and MediaPlayer's transposed single-channel
+    frames) == resize restatement + cascade, through one mcs_stitch_host_sized call."""
+    from multicamera_stitching_amd import rig
+    from multicamera_stitching_amd.StitcherClass import Stitcher
+    w, h = 160, 96
+    frames = rig.make_frames(3, w, h, 3, seed=41)
+    images = dict(zip(rig.labels(3), frames))
+    Hs = [[[0.99, 0.01, 121.3], [-0.01, 1.0, 2.6], [1e-5, 0, 1]],
+          [[1.0, -0.02, 240.7], [0.01, 0.99, -1.4], [0, 1e-5, 1]]]
+    st = Stitcher(images)
+    st.calibrate_stitcher(images, save=False, homographies=Hs)
+    stages = [dict(H=np.asarray(sb.cachedAH), canvas_w=sb.ABSize[0], canvas_h=sb.ABSize[1],
+                   bx=sb.Bpts[0][0], by=sb.Bpts[0][1], super_mode=False,
+                   x_limits=sb.x_limits, y_limits=sb.y_limits) for sb in st.stitchers]
+    for shots in (rig.make_frames(3, 211, 130, 3, seed=42),
+                  [np.ascontiguousarray(f.T) for f in rig.make_frames(3, w, h, 1, seed=43)]):
+        got = st.stitch(dict(zip(rig.labels(3), shots)))
+        cams = [oracle.resize_linear(c, (w, h)) for c in shots]
+        want = oracle.cascade_stitch(stages, cams)
+        assert _diff(got, want) == 0

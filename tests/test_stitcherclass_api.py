@@ -155,3 +155,22 @@ def test_missing_library_fails_loudly(tmp_path):
             "c._lib = None\ntry:\n    c.load()\nexcept ImportError as e:\n    print('raised', e)")
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, cwd=ROOT)
     assert "raised" in out.stdout and "no CPU fallback" in out.stdout
+
+
+def test_off_size_frames_log_the_reference_warnings(caplog):
+    """Frames off their calibrated shape produce the reference's per-stage warnings
+    (StitcherClass.py:226-233) and are sized for the GPU resize pre-pass."""
+    from multicamera_stitching_amd.StitcherClass import _conform_cameras
+    imgs = images()
+    st = Stitcher(imgs)
+    st.calibrate_stitcher(imgs, save=False, homographies=[[[1, 0, 30], [0, 1, 2], [0, 0, 1]],
+                                                          [[1, 0, 60], [0, 1, -3], [0, 0, 1]]])
+    shots = [np.zeros((30, 40, 3), np.uint8), np.zeros((25, 33, 3), np.uint8),
+             np.zeros((30, 40, 3), np.uint8)]
+    with caplog.at_level(logging.WARNING, logger="multicamera_stitching_amd"):
+        cams, cam0_hw, sizes = _conform_cameras(st, st.stitchers, shots)
+    assert cam0_hw == (30, 40) and sizes == [(40, 30), (33, 25), (40, 30)]
+    assert "ImageA size should be (30, 40, 3), Image will be resized" in caplog.text
+    assert caplog.text.count("Image will be resized") == 1
+    with pytest.raises(ValueError):
+        _conform_cameras(st, st.stitchers, [shots[0], shots[1][..., 0], shots[2]])
