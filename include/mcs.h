@@ -141,6 +141,21 @@ int mcs_stitch_device(mcs_plan *plan, const uint8_t *const *d_cams,
  * byte count): touched_px[i] for i < n_cams.  Runs a one-off marking kernel. */
 int mcs_plan_footprint(mcs_plan *plan, int64_t *touched_px, int n_cams);
 
+/* ---- Matching (per-frame estimation path) -------------------------------
+ * Brute-force k=2 nearest neighbours of each query descriptor among the train descriptors under
+ * the Hamming distance, as cv2.BFMatcher(cv2.NORM_HAMMING).knnMatch(query, train, k=2) (the
+ * reference's matcher is the float-L2 BFMatcher at StitcherClass.py:405-448; with binary ORB
+ * descriptors it becomes this).  Descriptors: 32 bytes (256 bits) each, dense.  Output per query
+ * q: idx2[2q], idx2[2q+1] = train indices of the best and second best, dist2[...] their
+ * distances (ties: the lower train index first, as OpenCV); -1/-1 where n_train < 2 leaves no
+ * candidate.  n_train < 2^23.  Device pointers, enqueued on `stream` of `device`. */
+int mcs_match_hamming_knn2(const uint8_t *d_query, int n_query, const uint8_t *d_train,
+                           int n_train, int32_t *d_idx2, int32_t *d_dist2, int device,
+                           void *stream);
+/* The same on host buffers (synchronous; allocates and frees its device buffers). */
+int mcs_match_hamming_knn2_host(const uint8_t *query, int n_query, const uint8_t *train,
+                                int n_train, int32_t *idx2, int32_t *dist2, int device);
+
 #ifdef __cplusplus
 }
 #endif

@@ -32,6 +32,7 @@ EXPORTS = (
     "mcs_plan_create", "mcs_plan_destroy", "mcs_plan_out_shape", "mcs_plan_describe",
     "mcs_stitch_host", "mcs_stitch_device", "mcs_plan_footprint", "mcs_plan_prepare",
     "mcs_plan_stats", "mcs_stitch_host_sized", "mcs_resize_linear_device",
+    "mcs_match_hamming_knn2", "mcs_match_hamming_knn2_host",
 )
 
 
@@ -161,6 +162,10 @@ def load() -> ctypes.CDLL:
         i64 = ctypes.c_int64
         L.mcs_resize_linear_device.argtypes = [P, I, I, i64, i64, P, I, I, i64, i64, I, I, I, P]
         L.mcs_resize_linear_device.restype = I
+        L.mcs_match_hamming_knn2.argtypes = [P, I, P, I, P, P, I, P]
+        L.mcs_match_hamming_knn2.restype = I
+        L.mcs_match_hamming_knn2_host.argtypes = [P, I, P, I, P, P, I]
+        L.mcs_match_hamming_knn2_host.restype = I
         L.mcs_stitch_device.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_int64), P,
                                         ctypes.c_int64, ctypes.c_int64, I, P]
         L.mcs_stitch_device.restype = I
@@ -308,3 +313,23 @@ def resize_linear_device(src_ptr: int, src_w: int, src_h: int, dst_ptr: int, dst
         src_ptr, src_w, src_h, src_pitch or src_w * channels, src_frame_stride, dst_ptr, dst_w,
         dst_h, dst_pitch or dst_w * channels, dst_frame_stride, channels, n_frames, device,
         stream or None))
+
+
+def match_hamming_knn2(query, train, device: int = 0):
+    """BFMatcher(NORM_HAMMING).knnMatch(query, train, k=2) on the GPU for host arrays of
+    N x 32-byte descriptors: (idx (nq, 2), dist (nq, 2)) int32, -1 where no candidate."""
+    L = load()
+    q = np.ascontiguousarray(query, dtype=np.uint8).reshape(-1, 32)
+    t = np.ascontiguousarray(train, dtype=np.uint8).reshape(-1, 32)
+    idx = np.empty((q.shape[0], 2), np.int32)
+    dist = np.empty((q.shape[0], 2), np.int32)
+    check(L.mcs_match_hamming_knn2_host(q.ctypes.data, q.shape[0], t.ctypes.data, t.shape[0],
+                                        idx.ctypes.data, dist.ctypes.data, device))
+    return idx, dist
+
+
+def match_hamming_knn2_device(q_ptr: int, nq: int, t_ptr: int, nt: int, idx_ptr: int,
+                              dist_ptr: int, device: int = 0, stream: int = 0):
+    """Device-pointer form (enqueued on `stream`)."""
+    check(load().mcs_match_hamming_knn2(q_ptr, nq, t_ptr, nt, idx_ptr, dist_ptr, device,
+                                        stream or None))

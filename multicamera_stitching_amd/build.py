@@ -1,10 +1,10 @@
 """Builds libmcs.so in-tree.
 
 Two steps:
-  1. hipcc compiles csrc/mcs_kernels.hip device-only for gfx950 into a code object
-     (mcs_kernels.gfx950.hsaco);
-  2. g++ compiles the host side (plan builder, HIP runtime binding, C ABI) and embeds that code
-     object (.incbin) into libmcs.so.  libmcs links no HIP runtime: it binds to the one the process
+  1. hipcc compiles each device source device-only for gfx950 into a code object
+     (csrc/mcs_kernels.hip: the stitch path; csrc/mcs_features.hip: matching/estimation);
+  2. g++ compiles the host side (plan builder, HIP runtime binding, C ABI) and embeds those code
+     objects (.incbin) into libmcs.so.  libmcs links no HIP runtime: it binds to the one the process
      already has (PyTorch's) or to ROCm's (csrc/hip_rt.h explains why).
 
 The library is the product path: the Python drop-in refuses to run without it.
@@ -21,13 +21,14 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libmcs.so")
 ARCH = os.environ.get("MCS_OFFLOAD_ARCH", "gfx950")
+# device sources -> embedded code objects (blob symbol mcs_hsaco_<name>_start)
+DEVICE = {"stitch": "mcs_kernels.hip", "features": "mcs_features.hip"}
 HSACO = os.path.join(HERE, f"mcs_kernels.{ARCH}.hsaco")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.environ.get("HIPCC", os.path.join(ROCM, "bin", "hipcc"))
 CXX = os.environ.get("CXX", "g++")
-DEVICE_SRC = "mcs_kernels.hip"
-HOST_SRC = ["mcs_plan.cpp", "hip_rt.cpp", "mcs_capi.cpp"]
-HEADERS = ["mcs_kparams.h", "mcs_common.h", "hip_rt.h"]
+HOST_SRC = ["mcs_plan.cpp", "hip_rt.cpp", "mcs_runtime.cpp", "mcs_capi.cpp", "mcs_features.cpp"]
+HEADERS = ["mcs_kparams.h", "mcs_fparams.h", "mcs_common.h", "hip_rt.h"]
 INC = ["-I" + os.path.join(ROOT, "include"), "-I" + CSRC]
 
 DEVICE_FLAGS = [
@@ -48,7 +49,7 @@ def _stale() -> bool:
     if not (os.path.exists(LIB) and os.path.exists(HSACO)):
         return True
     t = min(os.path.getmtime(LIB), os.path.getmtime(HSACO))
-    deps = [os.path.join(CSRC, s) for s in [DEVICE_SRC, *HOST_SRC, *HEADERS]]
+    deps = [os.path.join(CSRC, s) for s in [*DEVICE.values(), *HOST_SRC, *HEADERS]]
     deps += [os.path.join(ROOT, "include", "mcs.h"), __file__]
     return any(os.path.getmtime(d) > t for d in deps)
 
@@ -69,15 +70,20 @@ def build(force: bool = False, verbose: bool = False, lib: str = None, defines=(
 
 
 def _build_to(LIB: str, HSACO: str, defines, verbose: bool) -> str:
-    _run([HIPCC, *DEVICE_FLAGS, *["-D" + d for d in defines], *INC, "-o", HSACO + ".tmp",
-          os.path.join(CSRC, DEVICE_SRC)], verbose)
-    os.replace(HSACO + ".tmp", HSACO)
+    objs = {}
+    for name, src in DEVICE.items():
+        out = HSACO if name == "stitch" else HSACO.replace("mcs_kernels", "mcs_" + name)
+        _run([HIPCC, *DEVICE_FLAGS, *["-D" + d for d in defines], *INC, "-o", out + ".tmp",
+              os.path.join(CSRC, src)], verbose)
+        os.replace(out + ".tmp", out)
+        objs[name] = out
     blob = LIB + ".blob.S"
     with open(blob, "w") as f:
-        f.write('    .section .rodata\n    .balign 4096\n    .globl mcs_hsaco_start\n'
-                'mcs_hsaco_start:\n    .incbin "%s"\n    .globl mcs_hsaco_end\n'
-                'mcs_hsaco_end:\n    .byte 0\n    .section .note.GNU-stack,"",@progbits\n'
-                % HSACO)
+        f.write("    .section .rodata\n")
+        for name, path in objs.items():
+            f.write('    .balign 4096\n    .globl mcs_hsaco_%s_start\nmcs_hsaco_%s_start:\n'
+                    '    .incbin "%s"\n    .byte 0\n' % (name, name, path))
+        f.write('    .section .note.GNU-stack,"",@progbits\n')
     try:
         _run([CXX, *HOST_FLAGS, *["-D" + d for d in defines], *INC, "-o", LIB + ".tmp",
               *[os.path.join(CSRC, s) for s in HOST_SRC], blob, "-ldl", "-lpthread"], verbose)

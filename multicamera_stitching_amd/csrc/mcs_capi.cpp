@@ -11,10 +11,6 @@
 #include "hip_rt.h"
 #include "mcs_common.h"
 
-// gfx950 code object of mcs_kernels.hip, embedded by the build (mcs_blob.S)
-extern "C" const unsigned char mcs_hsaco_start[];
-extern "C" const unsigned char mcs_hsaco_end[];
-
 struct mcs_plan {
     mcs_flat_desc fd;
     mcs::KParams kp;
@@ -40,21 +36,14 @@ struct mcs_plan {
 
 #define MCS_VERSION_STRING "mcs 0.1.0 (gfx950 code object, HIP module launch)"
 
-#define HIP_TRY(expr)                                                                          \
-    do {                                                                                       \
-        hipError_t e_ = (expr);                                                                \
-        if (e_ != hipSuccess)                                                                  \
-            return mcs::fail(MCS_E_HIP, "%s failed: %s", #expr, A->hipGetErrorString(e_));   \
-    } while (0)
-
 namespace {
 
+using mcs::DeviceGuard;
+using mcs::kMaxDevices;
 using mcs::rt::Api;
 
-constexpr int kMaxDevices = 64;
-
 struct Kernels {
-    hipModule_t mod = nullptr;
+    bool loaded = false;
     hipFunction_t prepare[5][2] = {};     // [channels][interp]
     hipFunction_t stream[5] = {};         // [channels]
     hipFunction_t direct[5][2][2] = {};   // [channels][interp][32-bit offsets]
@@ -64,53 +53,40 @@ struct Kernels {
 Kernels g_k[kMaxDevices];
 std::mutex g_k_mu;
 
-// Loads the embedded code object on the current device (once per device).
+// The stitch module's kernels on `device` (looked up once per device).
 int kernels(const Api *A, int device, const Kernels **out)
 {
     if (device < 0 || device >= kMaxDevices) return mcs::fail(MCS_E_INVALID, "device %d", device);
     std::lock_guard<std::mutex> lk(g_k_mu);
     Kernels &k = g_k[device];
-    if (!k.mod) {
-        hipModule_t m = nullptr;
-        HIP_TRY(A->hipModuleLoadData(&m, mcs_hsaco_start));
+    if (!k.loaded) {
+        auto fn = [&](const char *name, hipFunction_t *f) {
+            return mcs::module_function(A, device, mcs::kModStitch, name, f);
+        };
         char name[64];
-        for (int c = 1; c <= 4; c++) {
+        int rc = MCS_OK;
+        for (int c = 1; c <= 4 && rc == MCS_OK; c++) {
             snprintf(name, sizeof(name), "mcs_stream_c%d", c);
-            HIP_TRY(A->hipModuleGetFunction(&k.stream[c], m, name));
+            rc = fn(name, &k.stream[c]);
             snprintf(name, sizeof(name), "mcs_resize_c%d", c);
-            HIP_TRY(A->hipModuleGetFunction(&k.resize[c], m, name));
-            for (int i = 0; i < 2; i++) {
+            if (rc == MCS_OK) rc = fn(name, &k.resize[c]);
+            for (int i = 0; i < 2 && rc == MCS_OK; i++) {
                 snprintf(name, sizeof(name), "mcs_prepare_c%d_i%d", c, i);
-                HIP_TRY(A->hipModuleGetFunction(&k.prepare[c][i], m, name));
-                for (int o = 0; o < 2; o++) {
+                rc = fn(name, &k.prepare[c][i]);
+                for (int o = 0; o < 2 && rc == MCS_OK; o++) {
                     snprintf(name, sizeof(name), "mcs_direct_c%d_i%d_o%d", c, i, o ? 32 : 64);
-                    HIP_TRY(A->hipModuleGetFunction(&k.direct[c][i][o], m, name));
+                    rc = fn(name, &k.direct[c][i][o]);
                 }
             }
         }
-        HIP_TRY(A->hipModuleGetFunction(&k.footprint[0], m, "mcs_footprint_i0"));
-        HIP_TRY(A->hipModuleGetFunction(&k.footprint[1], m, "mcs_footprint_i1"));
-        k.mod = m;
+        if (rc == MCS_OK) rc = fn("mcs_footprint_i0", &k.footprint[0]);
+        if (rc == MCS_OK) rc = fn("mcs_footprint_i1", &k.footprint[1]);
+        if (rc) return rc;
+        k.loaded = true;
     }
     *out = &k;
     return MCS_OK;
 }
-
-// Makes the plan's device current for the duration of a call and restores the caller's.
-struct DeviceGuard {
-    const Api *A;
-    int prev = -1;
-    hipError_t err = hipSuccess;
-    DeviceGuard(const Api *a, int dev) : A(a)
-    {
-        err = A->hipGetDevice(&prev);
-        if (err == hipSuccess && prev != dev) err = A->hipSetDevice(dev);
-    }
-    ~DeviceGuard()
-    {
-        if (prev >= 0) (void)A->hipSetDevice(prev);
-    }
-};
 
 int ensure_stream(const Api *A, mcs_plan *p)
 {

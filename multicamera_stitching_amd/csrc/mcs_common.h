@@ -4,8 +4,17 @@
 
 #include <stdint.h>
 
+#include "hip_rt.h"
 #include "mcs.h"
 #include "mcs_kparams.h"
+
+// Returns MCS_E_HIP with the HIP error text when `expr` fails (needs `A`, the bound runtime).
+#define HIP_TRY(expr)                                                                          \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess)                                                                  \
+            return mcs::fail(MCS_E_HIP, "%s failed: %s", #expr, A->hipGetErrorString(e_));   \
+    } while (0)
 
 namespace mcs {
 
@@ -17,5 +26,27 @@ void invert3x3_cv(const double *m, double *out);
 int build_flat(const mcs_stage_desc *stages, int n_stages, int cam0_w, int cam0_h, int channels,
                int interp, mcs_flat_desc *fd);
 void fill_kparams(const mcs_flat_desc &fd, KParams *kp);
+
+// Embedded gfx950 code objects (one per device source, see build.py) and their kernels.
+enum Module { kModStitch = 0, kModFeatures = 1, kNumModules = 2 };
+constexpr int kMaxDevices = 64;
+// Loads module `m` on `device` once (the device must be current) and looks up `name`.
+int module_function(const rt::Api *A, int device, Module m, const char *name, hipFunction_t *out);
+
+// Makes `dev` current for the duration of a call and restores the caller's device.
+struct DeviceGuard {
+    const rt::Api *A;
+    int prev = -1;
+    hipError_t err = hipSuccess;
+    DeviceGuard(const rt::Api *a, int dev) : A(a)
+    {
+        err = A->hipGetDevice(&prev);
+        if (err == hipSuccess && prev != dev) err = A->hipSetDevice(dev);
+    }
+    ~DeviceGuard()
+    {
+        if (prev >= 0) (void)A->hipSetDevice(prev);
+    }
+};
 
 }  // namespace mcs

@@ -1,0 +1,23 @@
+// mcs_fparams.h -- kernel argument blocks of the feature/estimation module (mcs_features.hip),
+// shared by the host (g++) and the device compile.
+#pragma once
+
+#include <stdint.h>
+
+namespace mcs {
+
+// Brute-force Hamming kNN-2 over 256-bit descriptors (BFMatcher(NORM_HAMMING).knnMatch(k=2),
+// the per-frame matcher of SURVEY.md 8 NS-4; reference counterpart StitcherClass.py:405-448).
+constexpr int kDescBytes = 32;
+constexpr int kKnnQueriesPerBlock = 64;   // one query per lane
+constexpr int kKnnKeyShift = 23;          // key = distance << 23 | train index
+constexpr int kKnnMaxTrain = 1 << kKnnKeyShift;
+struct KHammingArgs {
+    const uint32_t *query;   // nq x 8 words
+    const uint32_t *train;   // nt x 8 words
+    uint32_t *keys;          // nq x 2 (best, second) -> finalised into idx
+    int32_t *dist;           // nq x 2
+    int nq, nt, per_chunk, pad_;
+};
+
+}  // namespace mcs

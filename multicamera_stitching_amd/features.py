@@ -65,3 +65,14 @@ def match_keypoints(owner, kpsA, kpsB, featuresA, featuresB, ratio=0.75, reprojT
         ptsB = np.float32([kpsB[i] for (i, _) in matches])
         H, status = cv2.findHomography(ptsA, ptsB, cv2.RANSAC, reprojThresh)
     return H, matches, status
+
+
+def ratio_matches(idx, dist, ratio=0.75):
+    """Lowe's ratio test over knnMatch(k=2) results, as StitcherClass.py:427-433: query q is kept
+    as (trainIdx, queryIdx) when it has two candidates and d0 < d1 * ratio (strict), in query
+    order.  idx/dist: (nq, 2) arrays as returned by _capi.match_hamming_knn2."""
+    idx = np.asarray(idx)
+    dist = np.asarray(dist)
+    ok = (idx[:, 1] >= 0) & (dist[:, 0].astype(np.float64) < dist[:, 1].astype(np.float64) * ratio)
+    q = np.nonzero(ok)[0]
+    return [(int(idx[i, 0]), int(i)) for i in q]

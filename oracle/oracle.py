@@ -66,6 +66,8 @@ def lib():
                                         ctypes.c_int, P, ctypes.c_int, ctypes.c_int, ctypes.c_long]
         L.orc_resize_linear.restype = ctypes.c_int
         L.orc_resize_axis.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P]
+        L.orc_hamming_knn2.argtypes = [P, ctypes.c_int, P, ctypes.c_int, P, P]
+        L.orc_hamming_knn2.restype = None
         _lib = L
     return _lib
 
@@ -135,6 +137,17 @@ def resize_axis(ssize: int, dsize: int, is_x: bool):
     coef = np.zeros(2 * dsize, np.int16)
     lib().orc_resize_axis(ssize, dsize, 1 if is_x else 0, _p(ofs), _p(coef))
     return ofs, coef.reshape(dsize, 2)
+
+
+def hamming_knn2(query: np.ndarray, train: np.ndarray):
+    """BFMatcher(NORM_HAMMING).knnMatch(query, train, k=2) on N x 32-byte descriptors
+    (orc_match.c): (idx (nq, 2), dist (nq, 2)), -1 where no candidate."""
+    q = np.ascontiguousarray(query, dtype=np.uint8).reshape(-1, 32)
+    t = np.ascontiguousarray(train, dtype=np.uint8).reshape(-1, 32)
+    idx = np.empty((q.shape[0], 2), np.int32)
+    dist = np.empty((q.shape[0], 2), np.int32)
+    lib().orc_hamming_knn2(_p(q), q.shape[0], _p(t), t.shape[0], _p(idx), _p(dist))
+    return idx, dist
 
 
 def _stage_array(stages):

@@ -40,8 +40,10 @@ def test_no_hip_runtime_linked_and_code_object_embedded():
     assert "amdhip64" not in out          # bound at run time (csrc/hip_rt.h)
     blob = open(_capi.LIB_PATH, "rb").read()
     assert b"amdgcn-amd-amdhsa--gfx950" in blob
-    for k in (b"mcs_stream_c3", b"mcs_prepare_c3_i1", b"mcs_direct_c3_i1_o32"):
+    for k in (b"mcs_stream_c3", b"mcs_prepare_c3_i1", b"mcs_direct_c3_i1_o32", b"mcs_resize_c3",
+              b"mcs_hamming_knn2"):
         assert k in blob
+    assert blob.count(b"amdgcn-amd-amdhsa--gfx950") >= 2   # stitch + features code objects
 
 
 def test_version_and_abi():
