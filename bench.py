@@ -1,20 +1,23 @@
 #!/usr/bin/env python3
 """Benchmark of the stitch hot path: stitched MPix/s on a synthetic 4 x 1920x1080 rig.
 
-One "step" = one launch of the gather kernel over a batch of --frames rig captures that are
-already resident in HBM (4 camera frames each), producing --frames mosaics.  This is the work of
-Stitcher.stitch (PostScripts/Stitcher/StitcherClass.py:114-136) for each capture: bilinear
-warpPerspective of cameras 2..4 + overwrite paste of the growing mosaic, bit-exact to the CPU
-oracle (checked on frame 0 every run: "max_abs_diff").
+Workload (BASELINE.json configs[1]): 4 x 1920x1080 BGR cameras, precomputed homographies,
+bilinear warp + 3-level multi-band blend (--blend multiband, the default); --blend none is the
+reference's own per-stage semantics (warpPerspective + overwrite paste, StitcherClass.py:211-256)
+and --blend feather the linear feather blend.  One "step" = one stitch launch over --frames rig
+captures already resident in HBM (4 camera frames each), producing --frames mosaics: the
+streaming gather kernel over every tile, then (blend modes) the blend kernel over the tiles the
+blend changes.  Frame 0 is checked against the CPU restatement every run ("max_abs_diff").
 
 Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one process per GPU, each
 stitching its own captures (rig frames are independent: weak scaling, no data-path collective);
 barrier + synchronize around the timed region, time = max over ranks.
 
-Extra fields: "roofline" (HBM-bound gather; algorithmic bytes = mosaic bytes written + source
-bytes the mosaic actually reads, per launch, over the kernel's average duration measured with HIP
-events on its stream) and "cpu_baseline" (the reference-structured C restatement of the cascade,
-oracle/mcs_oracle.c, on the host cores, rank 0 only, bounded sample).
+Extra fields: "roofline" (HBM-bound; algorithmic bytes = mosaic bytes written + source bytes the
+mosaic reads, per launch, over the launch's average duration measured with HIP events on its
+stream; a lower bound for the blend modes, whose seam tiles re-read their neighbourhoods),
+"kernels" (the same launch without the blend pass, for the blend's share), and "cpu_baseline"
+(the C restatement in oracle/, on the host cores, rank 0 only, bounded sample).
 """
 from __future__ import annotations
 
@@ -45,6 +48,8 @@ def parse():
     ap.add_argument("--channels", type=int, default=3)
     ap.add_argument("--interp", choices=["linear", "nearest"], default="linear")
     ap.add_argument("--super-mode", action="store_true")
+    ap.add_argument("--blend", choices=["multiband", "feather", "none"], default="multiband",
+                    help="multiband = BASELINE configs[1]; none = the reference's paste")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--gather", action="store_true",
                     help="after timing, gather one mosaic per rank onto rank 0 (RCCL)")
@@ -78,6 +83,9 @@ def main():
     descs = [_stage_desc(sb) for sb in st.stitchers]
     plan = _capi.Plan(descs, args.width, args.height, args.channels, interp,
                       device=torch.cuda.current_device())
+    blend = {"none": _capi.MCS_BLEND_NONE, "feather": _capi.MCS_BLEND_FEATHER,
+             "multiband": _capi.MCS_BLEND_MULTIBAND}[args.blend]
+    plan.set_blend(blend)
     C = args.channels
     F = args.frames
     out_w, out_h = plan.out_w, plan.out_h
@@ -135,6 +143,31 @@ def main():
 
     mpix_per_launch = F * out_w * out_h / 1e6
     value = world * mpix_per_launch * args.steps / elapsed
+    frame0 = d_out[0, :, :out_w * C].reshape(out_h, out_w, C).cpu().numpy() if rank == 0 else None
+
+    # the same launch with the reference's paste (no blend pass): the blend's share of the time
+    paste_ms = None
+    if blend != _capi.MCS_BLEND_NONE:
+        ref = _capi.Plan(descs, args.width, args.height, args.channels, interp,
+                         device=torch.cuda.current_device())
+        ref.prepare(stream.cuda_stream)
+
+        def step_ref():
+            ref.stitch_device([t.data_ptr() for t in d_cams], [t[0].numel() for t in d_cams],
+                              d_out.data_ptr(), pitch, d_out[0].numel(), F, stream.cuda_stream)
+        for _ in range(args.warmup):
+            step_ref()
+        torch.cuda.synchronize()
+        evr = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(args.steps)]
+        for i in range(args.steps):
+            evr[i][0].record(stream)
+            step_ref()
+            evr[i][1].record(stream)
+        torch.cuda.synchronize()
+        paste_ms = shard.max_over_ranks([float(np.mean([a.elapsed_time(b) for a, b in evr]))],
+                                        device=dev)[0]
+        ref.close()
 
     # algorithmic bytes per launch: mosaic written once + the source pixels it reads, once
     fp = plan.footprint()
@@ -142,7 +175,8 @@ def main():
     bytes_per_launch = F * bytes_per_frame
     achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
     traffic = None
-    workload = f"{args.cams}x{args.width}x{args.height}x{C}-{args.interp}-super{int(args.super_mode)}-F{F}"
+    workload = (f"{args.cams}x{args.width}x{args.height}x{C}-{args.interp}-"
+                f"super{int(args.super_mode)}-F{F}-{args.blend}")
     try:
         pm = json.load(open(args.pmc_json))
         if pm.get("workload") == workload:
@@ -152,11 +186,10 @@ def main():
 
     result = None
     if rank == 0:
-        frame0 = d_out[0, :, :out_w * C].reshape(out_h, out_w, C).cpu().numpy()
         cpu = None
         max_abs = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu, max_abs = cpu_baseline(st, cams, frame0, args, interp, out_w, out_h)
+            cpu, max_abs = cpu_baseline(st, cams, frame0, args, interp, out_w, out_h, plan, blend)
         result = {
             "metric": "stitched MPix/sec (4-cam 1080p rig)",
             "value": round(value, 3),
@@ -172,9 +205,12 @@ def main():
             "data": "synthetic",
             "config": {
                 "workload": ("C2 rig: %d x %dx%d BGR cameras, precomputed homographies, "
-                             "%s warpPerspective + overwrite paste (reference StitcherClass "
-                             "semantics, no blend)" % (args.cams, args.width, args.height,
-                                                       args.interp)),
+                             "%s warpPerspective + %s" % (
+                                 args.cams, args.width, args.height, args.interp,
+                                 {"multiband": "3-level multi-band blend (SURVEY.md 8 NS-1)",
+                     "feather": "linear feather blend (SURVEY.md 8 NS-2)",
+                     "none": "overwrite paste (the reference's StitcherClass semantics)"}[args.blend])),
+                "blend": args.blend,
                 "mosaic": [out_h, out_w, C],
                 "frames_per_step": F,
                 "super_mode": bool(args.super_mode),
@@ -185,10 +221,15 @@ def main():
             "plan": {"prepare_ms_once": round(prep_ms, 3), "tiles": plan_stats["tiles"],
                      "lds_tiles": plan_stats["lds_tiles"],
                      "direct_tiles": plan_stats["direct_tiles"],
+                     "blend_tiles_32px": plan_stats["blend_tiles"],
                      "table_mb": round(plan_stats["table_bytes"] / 1e6, 2)},
+            "kernels": {"launch_ms": round(launch_ms, 4),
+                        "paste_only_launch_ms": None if paste_ms is None else round(paste_ms, 4)},
             "roofline": {
                 "bound": "hbm",
-                "kernel": "mcs_stream_c3 (+ mcs_direct for direct tiles)",
+                "kernel": "mcs_stream_c%d%s (one launch)" % (
+                    C, {"multiband": " + mcs_multiband_c%d_i1" % C,
+                        "feather": " + mcs_feather_c%d_i1" % C, "none": ""}[args.blend]),
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -206,20 +247,33 @@ def main():
     return result
 
 
-def cpu_baseline(st, cams, frame0, args, interp, out_w, out_h):
-    """Reference-structured cascade on host cores (oracle/mcs_oracle.c), bounded sample."""
+def cpu_baseline(st, cams, frame0, args, interp, out_w, out_h, plan, blend):
+    """The same workload on host cores (oracle/, C restatement), bounded sample.  Paste: the
+    reference-structured cascade (per-stage warp into full canvases + paste, StitcherClass.py);
+    blend modes: the flattened restatement of the blend (orc_blend.c)."""
     from oracle import oracle
     threads = min(16, os.cpu_count() or 1)
     oracle.set_threads(threads)
-    stages = [dict(H=np.asarray(sb.cachedAH), canvas_w=sb.ABSize[0], canvas_h=sb.ABSize[1],
-                   bx=sb.Bpts[0][0], by=sb.Bpts[0][1], super_mode=sb.super_mode,
-                   x_limits=sb.x_limits, y_limits=sb.y_limits) for sb in st.stitchers]
-    want = oracle.cascade_stitch(stages, cams, interp)
+    if blend == 0:
+        stages = [dict(H=np.asarray(sb.cachedAH), canvas_w=sb.ABSize[0], canvas_h=sb.ABSize[1],
+                       bx=sb.Bpts[0][0], by=sb.Bpts[0][1], super_mode=sb.super_mode,
+                       x_limits=sb.x_limits, y_limits=sb.y_limits) for sb in st.stitchers]
+
+        def run():
+            return oracle.cascade_stitch(stages, cams, interp)
+        what = "cascaded per-stage warpPerspective+paste"
+    else:
+        flat = plan.describe()
+
+        def run():
+            return oracle.blend_stitch(flat, cams, blend, interp)
+        what = {1: "feather", 2: "3-level multi-band"}[blend] + " blend (orc_blend.c)"
+    want = run()
     max_abs = int(np.abs(want.astype(np.int16) - frame0.astype(np.int16)).max())
     n = 0
     t0 = time.perf_counter()
     while True:
-        oracle.cascade_stitch(stages, cams, interp)
+        run()
         n += 1
         dt = time.perf_counter() - t0
         if dt >= args.cpu_seconds or n >= 5000:
@@ -229,8 +283,8 @@ def cpu_baseline(st, cams, frame0, args, interp, out_w, out_h):
         "unit": "MPix/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{n} captures of the same rig through the cascaded per-stage "
-                  f"warpPerspective+paste C restatement, {dt:.1f} s, OpenMP {threads} threads",
+        "sample": f"{n} captures of the same rig through the {what} C restatement, "
+                  f"{dt:.1f} s, OpenMP {threads} threads",
     }, max_abs
 
 

@@ -40,6 +40,13 @@ enum {
 };
 
 enum { MCS_INTER_NEAREST = 0, MCS_INTER_LINEAR = 1 };
+/* How overlapping cameras combine (mcs_plan_set_blend).  NONE is the reference: B pasted over
+ * the warped A (StitcherClass.py:240-241).  FEATHER / MULTIBAND (no
+ * reference implementation; specified in oracle/orc_blend.c): every pixel belongs to the
+ * covering camera farthest from its own image edge; FEATHER averages the covering cameras
+ * weighted by that edge distance, MULTIBAND blends a 3-level Laplacian pyramid across those
+ * ownership seams. */
+enum { MCS_BLEND_NONE = 0, MCS_BLEND_FEATHER = 1, MCS_BLEND_MULTIBAND = 2 };
 
 #define MCS_MAX_STAGES 15
 #define MCS_MAX_CAMS (MCS_MAX_STAGES + 1)
@@ -105,8 +112,15 @@ int mcs_plan_describe(const mcs_plan *plan, mcs_flat_desc *out);
  * call it on first use.  stream: hipStream_t or NULL for the plan's own stream. */
 int mcs_plan_prepare(mcs_plan *plan, void *stream);
 
-/* stats[0..4] = prepared, tiles, tiles on the LDS path, tiles on the direct path, table bytes. */
+/* stats[0..6] = prepared, tiles, tiles on the LDS path, tiles on the direct path, table bytes,
+ * blend mode, 32-px tiles the blend kernels recompute per frame. */
 int mcs_plan_stats(const mcs_plan *plan, int64_t *stats, int n);
+
+/* Blend mode of the plan (MCS_BLEND_*; default NONE = the reference's paste).  Changing it drops
+ * the prepared tables (rebuilt by mcs_plan_prepare or the next stitch).  FEATHER / MULTIBAND
+ * replace the reference's paste with the blends of SURVEY.md 8 NS-2 / NS-1; MULTIBAND supports
+ * up to 4 cameras meeting within 16 px (else MCS_E_UNSUPPORTED at prepare). */
+int mcs_plan_set_blend(mcs_plan *plan, int mode);
 
 /* Stitcher.stitch on host arrays (drop-in path, :114-136): cams[i] is the i-th camera in
  * sorted-label order, dense HxWxC u8 of the calibrated size; out is a dense out_h x out_w x C

@@ -22,6 +22,9 @@ MCS_E_SHAPE = -4
 MCS_E_UNSUPPORTED = -5
 MCS_INTER_NEAREST = 0
 MCS_INTER_LINEAR = 1
+MCS_BLEND_NONE = 0
+MCS_BLEND_FEATHER = 1
+MCS_BLEND_MULTIBAND = 2
 MCS_MAX_STAGES = 15
 MCS_MAX_CAMS = MCS_MAX_STAGES + 1
 ABI_VERSION = 1
@@ -32,7 +35,7 @@ EXPORTS = (
     "mcs_plan_create", "mcs_plan_destroy", "mcs_plan_out_shape", "mcs_plan_describe",
     "mcs_stitch_host", "mcs_stitch_device", "mcs_plan_footprint", "mcs_plan_prepare",
     "mcs_plan_stats", "mcs_stitch_host_sized", "mcs_resize_linear_device",
-    "mcs_match_hamming_knn2", "mcs_match_hamming_knn2_host",
+    "mcs_match_hamming_knn2", "mcs_match_hamming_knn2_host", "mcs_plan_set_blend",
 )
 
 
@@ -162,6 +165,8 @@ def load() -> ctypes.CDLL:
         i64 = ctypes.c_int64
         L.mcs_resize_linear_device.argtypes = [P, I, I, i64, i64, P, I, I, i64, i64, I, I, I, P]
         L.mcs_resize_linear_device.restype = I
+        L.mcs_plan_set_blend.argtypes = [P, I]
+        L.mcs_plan_set_blend.restype = I
         L.mcs_match_hamming_knn2.argtypes = [P, I, P, I, P, P, I, P]
         L.mcs_match_hamming_knn2.restype = I
         L.mcs_match_hamming_knn2_host.argtypes = [P, I, P, I, P, P, I]
@@ -292,10 +297,16 @@ class Plan:
         check(self._lib.mcs_plan_prepare(self._h, ctypes.c_void_p(int(stream))))
 
     def stats(self) -> dict:
-        arr = (ctypes.c_int64 * 5)()
-        check(self._lib.mcs_plan_stats(self._h, arr, 5))
+        arr = (ctypes.c_int64 * 7)()
+        check(self._lib.mcs_plan_stats(self._h, arr, 7))
         return {"prepared": bool(arr[0]), "tiles": arr[1], "lds_tiles": arr[2],
-                "direct_tiles": arr[3], "table_bytes": arr[4]}
+                "direct_tiles": arr[3], "table_bytes": arr[4], "blend": arr[5],
+                "blend_tiles": arr[6]}
+
+    def set_blend(self, mode: int):
+        """MCS_BLEND_NONE (reference paste), MCS_BLEND_FEATHER or MCS_BLEND_MULTIBAND."""
+        check(self._lib.mcs_plan_set_blend(self._h, int(mode)))
+        return self
 
     def footprint(self):
         arr = (ctypes.c_int64 * MCS_MAX_CAMS)()

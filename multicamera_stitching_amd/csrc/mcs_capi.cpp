@@ -32,6 +32,12 @@ struct mcs_plan {
     // host path with frames off their calibrated size: upload buffers for the resize pre-pass
     uint8_t *d_raw[MCS_MAX_CAMS] = {};
     size_t raw_bytes[MCS_MAX_CAMS] = {};
+    // blended modes (mcs_plan_set_blend): owner map, 32-px tile info, per-frame tile list
+    int blend = MCS_BLEND_NONE;
+    int n_blend = 0, mb_slots = 0;
+    uint8_t *d_owner = nullptr;
+    uint32_t *d_binfo = nullptr;
+    int *d_blist = nullptr;
 };
 
 #define MCS_VERSION_STRING "mcs 0.1.0 (gfx950 code object, HIP module launch)"
@@ -49,6 +55,10 @@ struct Kernels {
     hipFunction_t direct[5][2][2] = {};   // [channels][interp][32-bit offsets]
     hipFunction_t footprint[2] = {};
     hipFunction_t resize[5] = {};         // [channels]
+    hipFunction_t blend_owner[2] = {};    // [interp]
+    hipFunction_t blend_classify = nullptr;
+    hipFunction_t feather[5][2] = {};     // [channels][interp]
+    hipFunction_t multiband[5][2][2] = {};   // [channels][interp][<= 2 owners : <= 4]
 };
 Kernels g_k[kMaxDevices];
 std::mutex g_k_mu;
@@ -73,6 +83,12 @@ int kernels(const Api *A, int device, const Kernels **out)
             for (int i = 0; i < 2 && rc == MCS_OK; i++) {
                 snprintf(name, sizeof(name), "mcs_prepare_c%d_i%d", c, i);
                 rc = fn(name, &k.prepare[c][i]);
+                snprintf(name, sizeof(name), "mcs_feather_c%d_i%d", c, i);
+                if (rc == MCS_OK) rc = fn(name, &k.feather[c][i]);
+                snprintf(name, sizeof(name), "mcs_multiband_c%d_i%d_s2", c, i);
+                if (rc == MCS_OK) rc = fn(name, &k.multiband[c][i][0]);
+                snprintf(name, sizeof(name), "mcs_multiband_c%d_i%d_s4", c, i);
+                if (rc == MCS_OK) rc = fn(name, &k.multiband[c][i][1]);
                 for (int o = 0; o < 2 && rc == MCS_OK; o++) {
                     snprintf(name, sizeof(name), "mcs_direct_c%d_i%d_o%d", c, i, o ? 32 : 64);
                     rc = fn(name, &k.direct[c][i][o]);
@@ -81,6 +97,9 @@ int kernels(const Api *A, int device, const Kernels **out)
         }
         if (rc == MCS_OK) rc = fn("mcs_footprint_i0", &k.footprint[0]);
         if (rc == MCS_OK) rc = fn("mcs_footprint_i1", &k.footprint[1]);
+        if (rc == MCS_OK) rc = fn("mcs_blend_owner_i0", &k.blend_owner[0]);
+        if (rc == MCS_OK) rc = fn("mcs_blend_owner_i1", &k.blend_owner[1]);
+        if (rc == MCS_OK) rc = fn("mcs_blend_classify", &k.blend_classify);
         if (rc) return rc;
         k.loaded = true;
     }
@@ -137,6 +156,70 @@ bool offset_base(const mcs_plan *p, const mcs::KParams &kp, const uint8_t **base
     return off32;
 }
 
+int launch_args(const Api *A, hipFunction_t f, unsigned gx, unsigned gy, unsigned bx,
+                unsigned by, void *args, size_t sz, hipStream_t s)
+{
+    void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz,
+                   HIP_LAUNCH_PARAM_END};
+    HIP_TRY(A->hipModuleLaunchKernel(f, gx, gy, 1, bx, by, 1, 0, s, nullptr, cfg));
+    return MCS_OK;
+}
+
+// Blended modes: the owner map and the list of 32-px tiles the blend kernels recompute.
+int prepare_blend(const Api *A, mcs_plan *p, const Kernels *k, hipStream_t s)
+{
+    const int W = p->fd.out_w, H = p->fd.out_h;
+    const int bx = (W + mcs::kBlendTile - 1) / mcs::kBlendTile;
+    const int by = (H + mcs::kBlendTile - 1) / mcs::kBlendTile;
+    const size_t nt = (size_t)bx * by;
+    HIP_TRY(A->hipMalloc((void **)&p->d_owner, (size_t)W * H));
+    HIP_TRY(A->hipMalloc((void **)&p->d_binfo, nt * 2 * sizeof(uint32_t)));
+    HIP_TRY(A->hipMalloc((void **)&p->d_blist, (2 * nt + 3) * sizeof(int)));
+    HIP_TRY(A->hipMemsetAsync(p->d_blist, 0, (2 * nt + 3) * sizeof(int), s));
+    mcs::KBlendPrepArgs a;
+    a.P = p->kp;
+    a.owner = p->d_owner;
+    a.info = p->d_binfo;
+    a.list = p->d_blist;
+    a.overflow = p->d_blist + 2 * nt + 1;
+    a.mode = p->blend;
+    a.pad_ = 0;
+    int rc = launch_args(A, k->blend_owner[p->fd.interp], bx, by, 256, 1, &a, sizeof(a), s);
+    if (rc == MCS_OK) rc = launch_args(A, k->blend_classify, (unsigned)nt, 1, 256, 1, &a,
+                                       sizeof(a), s);
+    if (rc) return rc;
+    int n = 0, tail[2] = {0, 0};
+    HIP_TRY(A->hipMemcpyAsync(&n, p->d_blist, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(A->hipMemcpyAsync(tail, p->d_blist + 2 * nt + 1, 2 * sizeof(int),
+                              hipMemcpyDeviceToHost, s));
+    HIP_TRY(A->hipStreamSynchronize(s));
+    const int overflow = tail[0];
+    p->mb_slots = tail[1];
+    if (overflow)
+        return mcs::fail(MCS_E_UNSUPPORTED, "multi-band: %d tiles have more than %d cameras "
+                         "meeting within %d px", overflow, mcs::kBlendSlots, mcs::kBlendHalo);
+    p->n_blend = n;
+    return MCS_OK;
+}
+
+// Frees the prepared tables (after a blend-mode change they are rebuilt on next use).
+void release_tables(const Api *A, mcs_plan *p)
+{
+    if (p->stream) (void)A->hipStreamSynchronize(p->stream);
+    if (p->side) (void)A->hipStreamSynchronize(p->side);
+    for (void *q : {(void *)p->d_tiles, (void *)p->d_desc, (void *)p->d_fallback,
+                    (void *)p->d_owner, (void *)p->d_binfo, (void *)p->d_blist})
+        if (q) (void)A->hipFree(q);
+    p->d_tiles = nullptr;
+    p->d_desc = nullptr;
+    p->d_fallback = nullptr;
+    p->d_owner = nullptr;
+    p->d_binfo = nullptr;
+    p->d_blist = nullptr;
+    p->prepared = false;
+    p->n_fallback = p->n_blend = 0;
+}
+
 // Prepared tables of a plan: one prepare launch, then the fallback-tile count is read back.
 // Allocates and synchronises: call before graph capture (the stitch entry points call it lazily).
 int prepare(const Api *A, mcs_plan *p, hipStream_t s)
@@ -151,6 +234,10 @@ int prepare(const Api *A, mcs_plan *p, hipStream_t s)
     if (tiles == 0) {
         p->prepared = true;
         return MCS_OK;
+    }
+    if (p->blend != MCS_BLEND_NONE) {
+        rc = prepare_blend(A, p, k, s);
+        if (rc) return rc;
     }
     HIP_TRY(A->hipMalloc((void **)&p->d_tiles, tiles * sizeof(mcs::TileHdr)));
     HIP_TRY(A->hipMalloc((void **)&p->d_desc, tiles * mcs::kTilePx * mcs::kDescWords * 4));
@@ -216,6 +303,27 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
                                          mcs::lds_stream_bytes(p->fd.channels), s, nullptr, cfg));
     }
     if (p->n_fallback > 0) HIP_TRY(A->hipStreamWaitEvent(s, p->ev_join, 0));
+    if (p->n_blend > 0) {
+        // recompute the blended tiles over the owner-sampled mosaic (same stream: ordered)
+        mcs::KBlendArgs b;
+        b.P = P;
+        b.owner = p->d_owner;
+        b.list = p->d_blist;
+        b.n_frames = n_frames;
+        b.pad_ = 0;
+        int rc;
+        if (p->blend == MCS_BLEND_FEATHER)
+            rc = launch_args(A, k->feather[p->fd.channels][p->fd.interp], p->n_blend, n_frames,
+                             256, 1, &b, sizeof(b), s);
+        else
+        {
+            const bool two = p->mb_slots <= 2;
+            rc = launch_args(A, k->multiband[p->fd.channels][p->fd.interp][two ? 0 : 1],
+                             p->n_blend, (n_frames + mcs::kMbFrames - 1) / mcs::kMbFrames,
+                             two ? mcs::kMbThreads2 : mcs::kMbThreads4, 1, &b, sizeof(b), s);
+        }
+        if (rc) return rc;
+    }
     return MCS_OK;
 }
 
@@ -358,6 +466,9 @@ int mcs_plan_destroy(mcs_plan *p)
             if (p->d_tiles) (void)A->hipFree(p->d_tiles);
             if (p->d_desc) (void)A->hipFree(p->d_desc);
             if (p->d_fallback) (void)A->hipFree(p->d_fallback);
+            if (p->d_owner) (void)A->hipFree(p->d_owner);
+            if (p->d_binfo) (void)A->hipFree(p->d_binfo);
+            if (p->d_blist) (void)A->hipFree(p->d_blist);
             if (p->side) (void)A->hipStreamSynchronize(p->side);
             if (p->stream) (void)A->hipStreamDestroy(p->stream);
             if (p->side) (void)A->hipStreamDestroy(p->side);
@@ -534,14 +645,33 @@ int mcs_plan_prepare(mcs_plan *p, void *stream)
     return prepare(A, p, s);
 }
 
+int mcs_plan_set_blend(mcs_plan *p, int mode)
+{
+    mcs::clear_error();
+    if (!p) return mcs::fail(MCS_E_INVALID, "NULL plan");
+    if (mode != MCS_BLEND_NONE && mode != MCS_BLEND_FEATHER && mode != MCS_BLEND_MULTIBAND)
+        return mcs::fail(MCS_E_INVALID, "blend mode %d", mode);
+    if (mode == p->blend) return MCS_OK;
+    if (p->prepared) {
+        const Api *A = mcs::rt::api();
+        if (!A) return MCS_E_HIP;
+        DeviceGuard g(A, p->device);
+        release_tables(A, p);
+    }
+    p->blend = mode;
+    p->kp.blend = mode;
+    return MCS_OK;
+}
+
 int mcs_plan_stats(const mcs_plan *p, int64_t *stats, int n)
 {
     if (!p || !stats) return mcs::fail(MCS_E_INVALID, "NULL plan/stats");
     const int64_t tiles = (int64_t)p->gx * p->gy;
-    const int64_t v[5] = {p->prepared ? 1 : 0, tiles, tiles - p->n_fallback, p->n_fallback,
+    const int64_t v[7] = {p->prepared ? 1 : 0, tiles, tiles - p->n_fallback, p->n_fallback,
                           tiles * (int64_t)(sizeof(mcs::TileHdr) +
-                                            mcs::kTilePx * mcs::kDescWords * 4)};
-    for (int i = 0; i < n; i++) stats[i] = i < 5 ? v[i] : 0;
+                                            mcs::kTilePx * mcs::kDescWords * 4),
+                          p->blend, p->n_blend};
+    for (int i = 0; i < n; i++) stats[i] = i < 7 ? v[i] : 0;
     return MCS_OK;
 }
 

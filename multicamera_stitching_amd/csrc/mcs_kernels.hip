@@ -142,6 +142,22 @@ __device__ __forceinline__ int owner(const KParams &P, int x, int y)
     return sel;
 }
 
+}  // namespace mcs
+
+#include "mcs_blend.h"
+
+namespace mcs {
+
+// Stage sampled by output pixel (x, y): the paste rule (owner()) or, in the blended modes, the
+// blend owner; -1 = camera 0, -2 = no camera (blended modes only).
+template <int INTERP>
+__device__ __forceinline__ int pixel_stage(const KParams &P, int x, int y)
+{
+    if (P.blend == MCS_BLEND_NONE) return owner(P, x, y);
+    const int s = blend_owner<INTERP>(P, x, y, nullptr);
+    return s == kBlendNone ? -2 : s - 1;
+}
+
 // The lane's 4*CN output bytes as four scalar words (scalars, not an array: small arrays become
 // <N x i32> vectors whose poison-lane phis the gfx950 backend has miscompiled, see sample()).
 struct OutWords {
@@ -234,9 +250,14 @@ template <int CN, int INTERP>
 __device__ __forceinline__ Geo describe_geo(const KParams &P, int x, int y)
 {
     Geo g;
-    const int s = owner(P, x, y);
+    const int s = pixel_stage<INTERP>(P, x, y);
     int sw, sh, X, Y;
-    if (s < 0) {                 // camera 0 pasted whole: a copy (weights 32768, 0, 0, 0)
+    if (s == -2) {               // no camera: all weights 0 (the border value)
+        g.cam = 0;
+        sw = P.cam0_w;
+        sh = P.cam0_h;
+        X = Y = -(1 << 20);
+    } else if (s < 0) {          // camera 0 pasted whole: a copy (weights 32768, 0, 0, 0)
         g.cam = 0;
         sw = P.cam0_w;
         sh = P.cam0_h;
@@ -739,7 +760,8 @@ __device__ __forceinline__ void footprint_mark(const KParams &P, uint8_t *const 
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y;
     if (x >= P.out_w || y >= P.out_h) return;
-    const int s = owner(P, x, y);
+    const int s = pixel_stage<INTERP>(P, x, y);
+    if (s == -2) return;
     auto mark = [&](int cam, int sx, int sy, int w, int h) {
         if ((unsigned)sx < (unsigned)w && (unsigned)sy < (unsigned)h) {
             uint8_t *m = masks[cam] + (int64_t)sy * w + sx;
@@ -869,6 +891,47 @@ MCS_ENTRIES(1)
 MCS_ENTRIES(2)
 MCS_ENTRIES(3)
 MCS_ENTRIES(4)
+
+// Blended modes (mcs_blend.h).  Prepare: owner map + tile info over the 32-px blend grid, then
+// the classification into the per-frame tile list; per frame: feather / multiband over it.
+#define MCS_BLEND_PREP_ENTRY(IN)                                                               \
+    extern "C" __global__ __launch_bounds__(256) void mcs_blend_owner_i##IN(                  \
+        const mcs::KBlendPrepArgs a)                                                           \
+    {                                                                                          \
+        mcs::blend_owner_tile<IN>(a.P, a.owner, a.info);                                       \
+    }
+MCS_BLEND_PREP_ENTRY(0)
+MCS_BLEND_PREP_ENTRY(1)
+extern "C" __global__ __launch_bounds__(256) void mcs_blend_classify(const mcs::KBlendPrepArgs a)
+{
+    mcs::blend_classify(a.P, a.mode, a.owner, a.info, a.list, a.overflow);
+}
+#define MCS_BLEND_ENTRY(CN, IN)                                                                \
+    extern "C" __global__ __launch_bounds__(256) void mcs_feather_c##CN##_i##IN(               \
+        const mcs::KBlendArgs a)                                                               \
+    {                                                                                          \
+        mcs::feather_tile<CN, IN>(a);                                                          \
+    }                                                                                          \
+    extern "C" __global__ __launch_bounds__(512) void mcs_multiband_c##CN##_i##IN##_s2(        \
+        const mcs::KBlendArgs a)                                                               \
+    {                                                                                          \
+        __shared__ mcs::MbLds<CN, 2> lds;                                                      \
+        mcs::multiband_tile<CN, IN, 2>(a, lds);                                                \
+    }                                                                                          \
+    extern "C" __global__ __launch_bounds__(1024) void mcs_multiband_c##CN##_i##IN##_s4(       \
+        const mcs::KBlendArgs a)                                                               \
+    {                                                                                          \
+        __shared__ mcs::MbLds<CN, 4> lds;                                                      \
+        mcs::multiband_tile<CN, IN, 4>(a, lds);                                                \
+    }
+MCS_BLEND_ENTRY(1, 0)
+MCS_BLEND_ENTRY(1, 1)
+MCS_BLEND_ENTRY(2, 0)
+MCS_BLEND_ENTRY(2, 1)
+MCS_BLEND_ENTRY(3, 0)
+MCS_BLEND_ENTRY(3, 1)
+MCS_BLEND_ENTRY(4, 0)
+MCS_BLEND_ENTRY(4, 1)
 
 // grid (ceil(dw / kResizeBlock), dh, n_frames), block (kResizeBlock)
 #define MCS_RESIZE_ENTRY(CN)                                                                   \

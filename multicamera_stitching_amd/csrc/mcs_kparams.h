@@ -26,7 +26,7 @@ struct KParams {
     int out_w, out_h;
     int cam0_offx, cam0_offy;
     int cam0_w, cam0_h;
-    int pad_;
+    int blend;                     // MCS_BLEND_*: which camera owns a pixel (paste or blend rule)
     const uint8_t *cams[MCS_MAX_CAMS];
     int64_t cam_fstride[MCS_MAX_CAMS];
     uint8_t *out;
@@ -114,6 +114,30 @@ struct KResizeArgs {
     int area2x;                    // exact 2x downscale: OpenCV switches to INTER_AREA's 2x2 mean
 };
 constexpr int kResizeBlock = 256;
+
+// Blended modes (mcs_blend.h): 32 x 32 output tiles, 16-px pyramid halo, <= 4 owners per
+// multi-band neighbourhood, owner map byte 255 = no camera.
+constexpr int kBlendTile = 32;
+constexpr int kBlendHalo = 16;
+constexpr int kBlendSlots = 4;
+constexpr int kBlendNone = 255;
+constexpr int kMbThreads2 = 512;   // multi-band block, <= 2 owners per tile (2 blocks per CU)
+constexpr int kMbThreads4 = 1024;  // multi-band block, 3-4 owners per tile
+constexpr int kMbFrames = 4;       // captures per multi-band block (source maps reused)
+struct KBlendPrepArgs {
+    KParams P;
+    uint8_t *owner;
+    uint32_t *info;
+    int *list;
+    int *overflow;
+    int mode, pad_;
+};
+struct KBlendArgs {
+    KParams P;
+    const uint8_t *owner;
+    const int *list;
+    int n_frames, pad_;
+};
 
 constexpr int kDirectFrames = 4;    // captures per direct-gather block
 constexpr int kJobsPerWave = 2 + 2 * kRowsPerWave;   // footprint rows per wave per capture

@@ -102,6 +102,40 @@ def make_frames(n_cams, width, height, channels=3, seed=0):
     return [texture(height, width, channels, seed=seed * 131 + k) for k in range(n_cams)]
 
 
+def world_frames(C, width, height, channels=3, seed=0):
+    """Camera frames rendered from ONE shared world texture through the camera models C (so
+    overlaps agree up to interpolation, as with a real rig); float bilinear, numpy."""
+    corners = np.array([[0, 0, 1], [width - 1, 0, 1], [0, height - 1, 1],
+                        [width - 1, height - 1, 1]], np.float64).T
+    pts = []
+    for Ck in C:
+        q = Ck @ corners
+        pts.append(q[:2] / q[2])
+    pts = np.concatenate(pts, axis=1)
+    x0, y0 = np.floor(pts.min(axis=1)) - 2
+    x1, y1 = np.ceil(pts.max(axis=1)) + 2
+    world = texture(int(y1 - y0) + 1, int(x1 - x0) + 1, channels, seed=seed).astype(np.float64)
+    if world.ndim == 2:
+        world = world[..., None]
+    v, u = np.mgrid[0:height, 0:width].astype(np.float64)
+    frames = []
+    for Ck in C:
+        X = Ck[0, 0] * u + Ck[0, 1] * v + Ck[0, 2]
+        Y = Ck[1, 0] * u + Ck[1, 1] * v + Ck[1, 2]
+        W = Ck[2, 0] * u + Ck[2, 1] * v + Ck[2, 2]
+        X = X / W - x0
+        Y = Y / W - y0
+        xi = np.clip(np.floor(X).astype(np.int64), 0, world.shape[1] - 2)
+        yi = np.clip(np.floor(Y).astype(np.int64), 0, world.shape[0] - 2)
+        fx = np.clip(X - xi, 0, 1)[..., None]
+        fy = np.clip(Y - yi, 0, 1)[..., None]
+        img = (world[yi, xi] * (1 - fx) * (1 - fy) + world[yi, xi + 1] * fx * (1 - fy) +
+               world[yi + 1, xi] * (1 - fx) * fy + world[yi + 1, xi + 1] * fx * fy)
+        img = np.clip(np.rint(img), 1, 255).astype(np.uint8)
+        frames.append(img if channels > 1 else img[..., 0])
+    return frames
+
+
 def labels(n_cams):
     return ["CAM{}".format(i + 1) for i in range(n_cams)]
 

@@ -403,6 +403,52 @@ int orc_flat_stitch(int n_stages, const int *off_x, const int *off_y, const int 
     return 0;
 }
 
+/* Stage map of one canvas pixel (X, Y) in 1/32-px fixed point, evaluated like the cascade:
+ * block-start X0 of its OpenCV block, per-pixel W; integer coordinates x 32 for nearest.
+ * Shared with orc_blend.c. */
+void orc__stage_xy(const double *M, int bw0, int interp, int X, int Y, int *x32, int *y32)
+{
+    int xb = (X / bw0) * bw0;
+    double X0 = M[0] * xb + M[1] * Y + M[2];
+    double Y0 = M[3] * xb + M[4] * Y + M[5];
+    double W0 = M[6] * xb + M[7] * Y + M[8];
+    int x1 = X - xb;
+    double W = W0 + M[6] * x1;
+    if (interp == ORC_INTER_NEAREST) {
+        W = W ? 1. / W : 0;
+        *x32 = sat_i16(sat_i32_round((X0 + M[0] * x1) * W)) * 32;
+        *y32 = sat_i16(sat_i32_round((Y0 + M[3] * x1) * W)) * 32;
+    } else {
+        W = W ? INTER_TAB_SIZE / W : 0;
+        int Xi = sat_i32_round((X0 + M[0] * x1) * W);
+        int Yi = sat_i32_round((Y0 + M[3] * x1) * W);
+        *x32 = sat_i16(Xi >> INTER_BITS) * 32 + (Xi & 31);
+        *y32 = sat_i16(Yi >> INTER_BITS) * 32 + (Yi & 31);
+    }
+}
+
+/* Bilinear sample at (x32, y32) with BORDER_REPLICATE (taps clamped into the image), the
+ * remapBilinear fixed-point arithmetic (weights of the initInterTab2D table). */
+void orc__sample_replicate(const uint8_t *src, int sw, int sh, int cn, int x32, int y32,
+                           uint8_t *d)
+{
+    bilinear_tab();
+    int sx = x32 >> 5, sy = y32 >> 5;
+    const short *w = g_bilin[(y32 & 31) * INTER_TAB_SIZE + (x32 & 31)];
+    int xa = sx < 0 ? 0 : (sx >= sw ? sw - 1 : sx);
+    int xb = sx + 1 < 0 ? 0 : (sx + 1 >= sw ? sw - 1 : sx + 1);
+    int ya = sy < 0 ? 0 : (sy >= sh ? sh - 1 : sy);
+    int yb = sy + 1 < 0 ? 0 : (sy + 1 >= sh ? sh - 1 : sy + 1);
+    long st = (long)sw * cn;
+    for (int k = 0; k < cn; k++) {
+        int v0 = src[ya * st + (long)xa * cn + k], v1 = src[ya * st + (long)xb * cn + k];
+        int v2 = src[yb * st + (long)xa * cn + k], v3 = src[yb * st + (long)xb * cn + k];
+        int s = v0 * w[0] + v1 * w[1] + v2 * w[2] + v3 * w[3];
+        int r = (s + (1 << (COEF_BITS - 1))) >> COEF_BITS;
+        d[k] = (uint8_t)(r < 0 ? 0 : (r > 255 ? 255 : r));
+    }
+}
+
 /* Single-pixel coordinate probe (known-answer tests). */
 void orc_map_pixel(const double *Minv, int interp, int xb, int x1, int y, int *X, int *Y)
 {

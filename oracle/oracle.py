@@ -68,6 +68,10 @@ def lib():
         L.orc_resize_axis.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P]
         L.orc_hamming_knn2.argtypes = [P, ctypes.c_int, P, ctypes.c_int, P, P]
         L.orc_hamming_knn2.restype = None
+        L.orc_blend_stitch.argtypes = [ctypes.c_int, P, P, P, P, P, P, P, P, ctypes.c_int,
+                                       ctypes.c_int, ctypes.c_int, P, ctypes.c_int, ctypes.c_int,
+                                       P]
+        L.orc_blend_stitch.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -214,3 +218,31 @@ def flat_stitch(flat: dict, cams, interp: int = INTER_LINEAR) -> np.ndarray:
     lib().orc_flat_stitch(n, _p(offx), _p(offy), _p(rect), _p(minv), _p(bw0), ptrs, _p(cw),
                           _p(ch), cn, interp, _p(out), ow, oh)
     return out
+
+
+BLEND_FEATHER = 1
+BLEND_MULTIBAND = 2
+
+
+def blend_stitch(flat: dict, cams, mode: int, interp: int = INTER_LINEAR, want_owner=False):
+    """Blended mosaic of the plan's geometry (orc_blend.c: FEATHER = 1, MULTIBAND = 2).
+    flat: mcs_plan_describe dict; cams: all cameras in sorted-label order, calibrated sizes."""
+    n = int(flat["n_stages"])
+    offx = np.ascontiguousarray(flat["off_x"], np.int32)
+    offy = np.ascontiguousarray(flat["off_y"], np.int32)
+    minv = np.ascontiguousarray(flat["minv"], np.float64).reshape(-1)
+    bw0 = np.ascontiguousarray(flat["bw0"], np.int32)
+    scam = np.ascontiguousarray(flat["cam"], np.int32)
+    cams = [np.ascontiguousarray(c, dtype=np.uint8) for c in cams]
+    cn = 1 if cams[0].ndim == 2 else cams[0].shape[2]
+    ow, oh = int(flat["out_w"]), int(flat["out_h"])
+    out = np.zeros((oh, ow, cn) if cams[0].ndim == 3 else (oh, ow), np.uint8)
+    owner = np.zeros((oh, ow), np.uint8)
+    ptrs = (ctypes.c_void_p * len(cams))(*[c.ctypes.data for c in cams])
+    cw = np.array([c.shape[1] for c in cams], np.int32)
+    ch = np.array([c.shape[0] for c in cams], np.int32)
+    rc = lib().orc_blend_stitch(n, _p(offx), _p(offy), _p(minv), _p(bw0), _p(scam), ptrs, _p(cw),
+                                _p(ch), cn, interp, mode, _p(out), ow, oh, _p(owner))
+    if rc != 0:
+        raise ValueError("orc_blend_stitch failed")
+    return (out, owner) if want_owner else out

@@ -1,0 +1,267 @@
+/*
+ * orc_blend.c -- TEST INFRASTRUCTURE ONLY (the parity checker), never the product path.
+ *
+ * CPU restatement of the blended stitch modes.  The reference
+ * has no blending -- StitcherBase.stitch pastes B over the warped A (StitcherClass.py:239-241) --
+ * so there is nothing to pin these against: the specification is ours, and this file is it.
+ * The GPU path (multicamera_stitching_amd/csrc) must reproduce it bit for bit; every quantity
+ * is an integer or an IEEE double computed in the order written here.
+ *
+ * Geometry: the plan's flattened chain (mcs_plan_describe).  Camera "slots": slot 0 = camera 0
+ * (integer offset into the mosaic), slot j+1 = the camera warped by calibrated stage j.  For
+ * output pixel p and slot s, the OpenCV stage map gives a position (x32, y32) in 1/32 px
+ * (orc__stage_xy: the exact cascade arithmetic).
+ *   covered_s(p) : 0 <= x32 <= 32 (w-1) and 0 <= y32 <= 32 (h-1)
+ *   d_s(p)       : min(x32, y32, 32 (w-1) - x32, 32 (h-1) - y32)   (distance to the image edge)
+ *   I_s(p)       : bilinear sample at (x32, y32) with the taps clamped into the image
+ *                  (BORDER_REPLICATE, remapBilinear fixed point); equals the reference-style warp
+ *                  wherever covered
+ *   owner(p)     : the covering slot with the largest d, ties to the lower camera index; none
+ *                  when no slot covers p (output 0, as the reference's border)
+ * FEATHER (NS-2): out = (sum_s d_s I_s + D / 2) / D over covering slots, D = sum_s d_s
+ *   (integer); D == 0 -> I_owner.
+ * MULTIBAND (NS-1), 3 levels, Burt-Adelson with the owner map as the seam masks:
+ *   reduce   g_{l+1}(y, x) = sum_ij w_i w_j g_l(refl(2y+i), refl(2x+j)), w = [1 4 6 4 1],
+ *            in integers: g0 = I (u8), g1 = 256 G1, g2 = 65536 G2; masks m0 = [owner == s],
+ *            m1 = reduce(m0), m2 = reduce(m1);
+ *   expand   taps of output x at the coarser level: even x -> (x/2-1, x/2, x/2+1) x (1, 6, 1),
+ *            odd x -> ((x-1)/2, (x+1)/2) x (4, 4); separable, /64 overall;
+ *   Laplace  L0 = 16384 g0 - E(g1) (= 16384 (G0 - up G1)), L1 = 16384 g1 - E(g2), L2 = g2;
+ *   blend    B0 = L0_owner / 16384, B1 = sum m1 L1 / (sum m1 * 4194304),
+ *            B2 = sum m2 g2 / (sum m2 * 65536)   (double; 0 where the mask sum is 0);
+ *   collapse R1 = B1 + up(B2), R0 = B0 + up(R1), up in double: acc += (uy * ux) * R over the
+ *            taps in the order listed (rows outer), then acc / 64;
+ *   out = clamp(floor(R0 + 0.5), 0, 255) where an owner exists, else 0.
+ *   refl = reflect-101 at each level's own size (BORDER_DEFAULT); sizes n_{l+1} = (n_l + 1) / 2.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define ORC_BLEND_FEATHER 1
+#define ORC_BLEND_MULTIBAND 2
+
+void orc__stage_xy(const double *M, int bw0, int interp, int X, int Y, int *x32, int *y32);
+void orc__sample_replicate(const uint8_t *src, int sw, int sh, int cn, int x32, int y32,
+                           uint8_t *d);
+
+static inline int refl(int i, int n)
+{
+    if (n == 1) return 0;
+    while (i < 0 || i >= n) {
+        if (i < 0) i = -i;
+        if (i >= n) i = 2 * n - 2 - i;
+    }
+    return i;
+}
+
+typedef struct {
+    int n_slots;
+    int cam[16];
+} slots_t;
+
+static void slot_xy(int s, int n_stages, const int *off_x, const int *off_y, const double *minv,
+                    const int *bw0, int interp, int x, int y, int *x32, int *y32)
+{
+    if (s == 0) {
+        *x32 = (x + off_x[n_stages]) * 32;
+        *y32 = (y + off_y[n_stages]) * 32;
+    } else {
+        int j = s - 1;
+        orc__stage_xy(minv + 9 * j, bw0[j], interp, x + off_x[j], y + off_y[j], x32, y32);
+    }
+}
+
+/* reduce: src (n_h x n_w x cn, int32) -> dst (m_h x m_w x cn) */
+static void reduce_i32(const int32_t *src, int nw, int nh, int cn, int32_t *dst, int mw, int mh)
+{
+    static const int w[5] = {1, 4, 6, 4, 1};
+#pragma omp parallel for schedule(static)
+    for (int y = 0; y < mh; y++)
+        for (int x = 0; x < mw; x++)
+            for (int k = 0; k < cn; k++) {
+                int64_t acc = 0;
+                for (int i = 0; i < 5; i++) {
+                    const int32_t *row = src + (long)refl(2 * y + i - 2, nh) * nw * cn;
+                    for (int j = 0; j < 5; j++)
+                        acc += (int64_t)(w[i] * w[j]) * row[(long)refl(2 * x + j - 2, nw) * cn + k];
+                }
+                dst[((long)y * mw + x) * cn + k] = (int32_t)acc;
+            }
+}
+
+/* expand taps of fine index x into a coarse level of size n */
+static inline int exp_taps(int x, int n, int *idx, int *wt)
+{
+    if ((x & 1) == 0) {
+        idx[0] = refl(x / 2 - 1, n), wt[0] = 1;
+        idx[1] = refl(x / 2, n), wt[1] = 6;
+        idx[2] = refl(x / 2 + 1, n), wt[2] = 1;
+        return 3;
+    }
+    idx[0] = refl((x - 1) / 2, n), wt[0] = 4;
+    idx[1] = refl((x + 1) / 2, n), wt[1] = 4;
+    return 2;
+}
+
+/* integer expand of a coarse int32 image evaluated at fine (y, x), channel k: sum u u g */
+static inline int64_t expand_i(const int32_t *g, int gw, int gh, int cn, int y, int x, int k)
+{
+    int iy[3], wy[3], ix[3], wx[3];
+    int ny = exp_taps(y, gh, iy, wy), nx = exp_taps(x, gw, ix, wx);
+    int64_t acc = 0;
+    for (int a = 0; a < ny; a++)
+        for (int b = 0; b < nx; b++)
+            acc += (int64_t)(wy[a] * wx[b]) * g[((long)iy[a] * gw + ix[b]) * cn + k];
+    return acc;
+}
+
+static inline double expand_d(const double *r, int gw, int gh, int cn, int y, int x, int k)
+{
+    int iy[3], wy[3], ix[3], wx[3];
+    int ny = exp_taps(y, gh, iy, wy), nx = exp_taps(x, gw, ix, wx);
+    double acc = 0.0;
+    for (int a = 0; a < ny; a++)
+        for (int b = 0; b < nx; b++)
+            acc += (double)(wy[a] * wx[b]) * r[((long)iy[a] * gw + ix[b]) * cn + k];
+    return acc / 64.0;
+}
+
+int orc_blend_stitch(int n_stages, const int *off_x, const int *off_y, const double *minv,
+                     const int *bw0, const int *stage_cam, const uint8_t *const *cams,
+                     const int *cw, const int *ch, int cn, int interp, int mode, uint8_t *out,
+                     int ow, int oh, uint8_t *owner_out)
+{
+    if (n_stages < 0 || n_stages > 15 || ow <= 0 || oh <= 0) return -1;
+    const int S = n_stages + 1;
+    int scam[16];
+    scam[0] = 0;
+    for (int j = 0; j < n_stages; j++) scam[j + 1] = stage_cam[j];
+    const long npx = (long)ow * oh;
+    uint8_t *owner = (uint8_t *)malloc((size_t)npx);
+    uint8_t *g0 = (uint8_t *)malloc((size_t)npx * cn * S);
+    int32_t *dist = (int32_t *)malloc(sizeof(int32_t) * (size_t)npx * S);
+    if (!owner || !g0 || !dist) { free(owner); free(g0); free(dist); return -1; }
+
+#pragma omp parallel for schedule(static)
+    for (long p = 0; p < npx; p++) {
+        const int y = (int)(p / ow), x = (int)(p % ow);
+        int best = -1, bestd = -1;
+        for (int s = 0; s < S; s++) {
+            const int c = scam[s], w = cw[c], h = ch[c];
+            int x32, y32;
+            slot_xy(s, n_stages, off_x, off_y, minv, bw0, interp, x, y, &x32, &y32);
+            orc__sample_replicate(cams[c], w, h, cn, x32, y32, g0 + ((long)s * npx + p) * cn);
+            int d = -1;
+            if (x32 >= 0 && y32 >= 0 && x32 <= 32 * (w - 1) && y32 <= 32 * (h - 1)) {
+                d = x32;
+                if (y32 < d) d = y32;
+                if (32 * (w - 1) - x32 < d) d = 32 * (w - 1) - x32;
+                if (32 * (h - 1) - y32 < d) d = 32 * (h - 1) - y32;
+                if (d > bestd || (d == bestd && c < scam[best])) best = s, bestd = d;
+            }
+            dist[(long)s * npx + p] = d;
+        }
+        owner[p] = (uint8_t)(best < 0 ? 255 : best);
+    }
+    if (owner_out) memcpy(owner_out, owner, (size_t)npx);
+
+    int rc = 0;
+    if (mode == ORC_BLEND_FEATHER) {
+#pragma omp parallel for schedule(static)
+        for (long p = 0; p < npx; p++) {
+            uint8_t *d = out + p * cn;
+            if (owner[p] == 255) {
+                memset(d, 0, (size_t)cn);
+                continue;
+            }
+            int64_t den = 0;
+            for (int s = 0; s < S; s++)
+                if (dist[(long)s * npx + p] > 0) den += dist[(long)s * npx + p];
+            for (int k = 0; k < cn; k++) {
+                if (den == 0) {
+                    d[k] = g0[((long)owner[p] * npx + p) * cn + k];
+                    continue;
+                }
+                int64_t num = 0;
+                for (int s = 0; s < S; s++) {
+                    const int32_t ds = dist[(long)s * npx + p];
+                    if (ds > 0) num += (int64_t)ds * g0[((long)s * npx + p) * cn + k];
+                }
+                d[k] = (uint8_t)((num + den / 2) / den);
+            }
+        }
+    } else if (mode == ORC_BLEND_MULTIBAND) {
+        const int w1 = (ow + 1) / 2, h1 = (oh + 1) / 2, w2 = (w1 + 1) / 2, h2 = (h1 + 1) / 2;
+        const long n1 = (long)w1 * h1, n2 = (long)w2 * h2;
+        int32_t *t0 = (int32_t *)malloc(sizeof(int32_t) * (size_t)npx * cn);
+        int32_t *g1 = (int32_t *)malloc(sizeof(int32_t) * (size_t)n1 * cn * S);
+        int32_t *g2 = (int32_t *)malloc(sizeof(int32_t) * (size_t)n2 * cn * S);
+        int32_t *m0 = (int32_t *)malloc(sizeof(int32_t) * (size_t)npx);
+        int32_t *m1 = (int32_t *)malloc(sizeof(int32_t) * (size_t)n1 * S);
+        int32_t *m2 = (int32_t *)malloc(sizeof(int32_t) * (size_t)n2 * S);
+        double *b2 = (double *)malloc(sizeof(double) * (size_t)n2 * cn);
+        double *r1 = (double *)malloc(sizeof(double) * (size_t)n1 * cn);
+        if (!t0 || !g1 || !g2 || !m0 || !m1 || !m2 || !b2 || !r1) {
+            rc = -1;
+            goto done;
+        }
+        for (int s = 0; s < S; s++) {
+            for (long i = 0; i < npx * cn; i++) t0[i] = g0[(long)s * npx * cn + i];
+            reduce_i32(t0, ow, oh, cn, g1 + (long)s * n1 * cn, w1, h1);
+            reduce_i32(g1 + (long)s * n1 * cn, w1, h1, cn, g2 + (long)s * n2 * cn, w2, h2);
+            for (long i = 0; i < npx; i++) m0[i] = owner[i] == s;
+            reduce_i32(m0, ow, oh, 1, m1 + (long)s * n1, w1, h1);
+            reduce_i32(m1 + (long)s * n1, w1, h1, 1, m2 + (long)s * n2, w2, h2);
+        }
+#pragma omp parallel for schedule(static)
+        for (long q = 0; q < n2; q++)
+            for (int k = 0; k < cn; k++) {
+                int64_t num = 0, den = 0;
+                for (int s = 0; s < S; s++) {
+                    num += (int64_t)m2[(long)s * n2 + q] * g2[((long)s * n2 + q) * cn + k];
+                    den += m2[(long)s * n2 + q];
+                }
+                b2[q * cn + k] = den ? (double)num / ((double)den * 65536.0) : 0.0;
+            }
+#pragma omp parallel for schedule(static)
+        for (long q = 0; q < n1; q++) {
+            const int y = (int)(q / w1), x = (int)(q % w1);
+            for (int k = 0; k < cn; k++) {
+                int64_t num = 0, den = 0;
+                for (int s = 0; s < S; s++) {
+                    const int64_t l1 = 16384 * (int64_t)g1[((long)s * n1 + q) * cn + k] -
+                                       expand_i(g2 + (long)s * n2 * cn, w2, h2, cn, y, x, k);
+                    num += (int64_t)m1[(long)s * n1 + q] * l1;
+                    den += m1[(long)s * n1 + q];
+                }
+                const double b1 = den ? (double)num / ((double)den * 4194304.0) : 0.0;
+                r1[q * cn + k] = b1 + expand_d(b2, w2, h2, cn, y, x, k);
+            }
+        }
+#pragma omp parallel for schedule(static)
+        for (long p = 0; p < npx; p++) {
+            const int y = (int)(p / ow), x = (int)(p % ow);
+            uint8_t *d = out + p * cn;
+            const int s = owner[p];
+            for (int k = 0; k < cn; k++) {
+                if (s == 255) {
+                    d[k] = 0;
+                    continue;
+                }
+                const int64_t l0 = 16384 * (int64_t)g0[((long)s * npx + p) * cn + k] -
+                                   expand_i(g1 + (long)s * n1 * cn, w1, h1, cn, y, x, k);
+                const double r0 = (double)l0 / 16384.0 + expand_d(r1, w1, h1, cn, y, x, k);
+                const double v = floor(r0 + 0.5);
+                d[k] = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+            }
+        }
+    done:
+        free(t0); free(g1); free(g2); free(m0); free(m1); free(m2); free(b2); free(r1);
+    } else {
+        rc = -1;
+    }
+    free(owner); free(g0); free(dist);
+    return rc;
+}

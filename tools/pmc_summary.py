@@ -10,7 +10,7 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-PMC = os.path.join(ROOT, "gpurun_out", "pmc")
+PMC = os.environ.get("MCS_PMC_DIR", os.path.join(ROOT, "gpurun_out", "pmc"))
 
 
 def main(kernel_prefix="mcs_stream_c3", workload=None, out=None):
@@ -59,5 +59,7 @@ def main(kernel_prefix="mcs_stream_c3", workload=None, out=None):
 
 
 if __name__ == "__main__":
-    wl = sys.argv[1] if len(sys.argv) > 1 else "4x1920x1080x3-linear-super0-F64"
-    main(workload=wl, out=os.path.join(ROOT, "profiles", "pmc_latest.json"))
+    wl = sys.argv[1] if len(sys.argv) > 1 else "4x1920x1080x3-linear-super0-F64-multiband"
+    kernel = sys.argv[2] if len(sys.argv) > 2 else "mcs_stream_c3"
+    out = sys.argv[3] if len(sys.argv) > 3 else os.path.join(ROOT, "profiles", "pmc_latest.json")
+    main(kernel_prefix=kernel, workload=wl, out=out)
