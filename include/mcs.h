@@ -170,6 +170,18 @@ int mcs_match_hamming_knn2(const uint8_t *d_query, int n_query, const uint8_t *d
 int mcs_match_hamming_knn2_host(const uint8_t *query, int n_query, const uint8_t *train,
                                 int n_train, int32_t *idx2, int32_t *dist2, int device);
 
+/* ---- Homography estimation ----------------------------------------------
+ * RANSAC homography of n correspondences src_xy[i] -> dst_xy[i] (float x, y pairs), the role of
+ * cv2.findHomography(ptsA, ptsB, cv2.RANSAC, reprojThresh) at StitcherClass.py:440-441.  `iters`
+ * hypotheses (4-point DLT, FP64) are scored in parallel on the GPU (one workgroup each); the
+ * most-supported one (ties: lowest index) gives the inlier mask, and a least-squares refit over
+ * its inliers gives H (row-major 3x3, H[8] = 1).  Deterministic for a given seed; algorithm
+ * specified in csrc/mcs_ransac_core.h.  *n_inliers = 0 and H = 0 when no model (n < 4 or no
+ * hypothesis with >= 4 inliers), like the reference's H = None.  mask may be NULL. */
+int mcs_ransac_homography_host(const float *src_xy, const float *dst_xy, int n, double thresh,
+                               int iters, uint32_t seed, double *H, uint8_t *mask,
+                               int *n_inliers, int device);
+
 #ifdef __cplusplus
 }
 #endif

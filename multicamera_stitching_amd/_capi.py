@@ -36,6 +36,7 @@ EXPORTS = (
     "mcs_stitch_host", "mcs_stitch_device", "mcs_plan_footprint", "mcs_plan_prepare",
     "mcs_plan_stats", "mcs_stitch_host_sized", "mcs_resize_linear_device",
     "mcs_match_hamming_knn2", "mcs_match_hamming_knn2_host", "mcs_plan_set_blend",
+    "mcs_ransac_homography_host",
 )
 
 
@@ -165,6 +166,9 @@ def load() -> ctypes.CDLL:
         i64 = ctypes.c_int64
         L.mcs_resize_linear_device.argtypes = [P, I, I, i64, i64, P, I, I, i64, i64, I, I, I, P]
         L.mcs_resize_linear_device.restype = I
+        L.mcs_ransac_homography_host.argtypes = [P, P, I, ctypes.c_double, I, ctypes.c_uint32,
+                                                 P, P, ctypes.POINTER(I), I]
+        L.mcs_ransac_homography_host.restype = I
         L.mcs_plan_set_blend.argtypes = [P, I]
         L.mcs_plan_set_blend.restype = I
         L.mcs_match_hamming_knn2.argtypes = [P, I, P, I, P, P, I, P]
@@ -344,3 +348,20 @@ def match_hamming_knn2_device(q_ptr: int, nq: int, t_ptr: int, nt: int, idx_ptr:
     """Device-pointer form (enqueued on `stream`)."""
     check(load().mcs_match_hamming_knn2(q_ptr, nq, t_ptr, nt, idx_ptr, dist_ptr, device,
                                         stream or None))
+
+
+def ransac_homography(src, dst, thresh: float, iters: int = 2000, seed: int = 0,
+                      device: int = 0):
+    """RANSAC homography on the GPU (mcs.h): (H 3x3 or None, status mask (n, 1) uint8), the
+    return shape of cv2.findHomography(src, dst, cv2.RANSAC, thresh)."""
+    L = load()
+    src = np.ascontiguousarray(src, np.float32).reshape(-1, 2)
+    dst = np.ascontiguousarray(dst, np.float32).reshape(-1, 2)
+    n = src.shape[0]
+    H = np.zeros(9, np.float64)
+    mask = np.zeros(n, np.uint8)
+    ninl = ctypes.c_int(0)
+    check(L.mcs_ransac_homography_host(src.ctypes.data, dst.ctypes.data, n, float(thresh),
+                                       int(iters), int(seed) & 0xffffffff, H.ctypes.data,
+                                       mask.ctypes.data, ctypes.byref(ninl), device))
+    return (H.reshape(3, 3) if ninl.value > 0 else None), mask.reshape(-1, 1)

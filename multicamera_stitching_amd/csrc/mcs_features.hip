@@ -18,6 +18,7 @@
 #include <stdint.h>
 
 #include "mcs_fparams.h"
+#include "mcs_ransac_core.h"
 
 namespace mcs {
 
@@ -78,4 +79,62 @@ extern "C" __global__ __launch_bounds__(256) void mcs_hamming_knn2_finalize(
     const bool none = k == kKeyNone;
     a.keys[i] = none ? 0xffffffffu : (k & (kKnnMaxTrain - 1));
     a.dist[i] = none ? -1 : (int32_t)(k >> kKnnKeyShift);
+}
+
+// ---- RANSAC homography (NS-5) ------------------------------------------------------------------
+// grid (iters), block kRansacBlock: thread 0 draws hypothesis k and solves its 4-point model,
+// then the block counts its inliers over all n correspondences (FP64, mcs_ransac_core.h).
+extern "C" __global__ __launch_bounds__(256) void mcs_ransac_score(const mcs::KRansacArgs a)
+{
+    using namespace mcs;
+    __shared__ double h[8];
+    __shared__ int valid;
+    __shared__ int wsum[kRansacBlock / 64];
+    const int k = blockIdx.x, tid = threadIdx.x;
+    if (tid == 0) {
+        int idx[4];
+        double s[8], d[8], hh[8];
+        bool ok = rs_subset(a.seed, (uint32_t)k, (uint32_t)a.n, idx);
+        if (ok) {
+            for (int m = 0; m < 4; m++) {
+                s[2 * m] = a.pts[4 * idx[m]], s[2 * m + 1] = a.pts[4 * idx[m] + 1];
+                d[2 * m] = a.pts[4 * idx[m] + 2], d[2 * m + 1] = a.pts[4 * idx[m] + 3];
+            }
+            ok = rs_model4(s, d, hh);
+        }
+        valid = ok;
+        for (int j = 0; j < 8; j++) {
+            h[j] = ok ? hh[j] : 0.0;
+            a.hyps[(int64_t)k * 8 + j] = ok ? hh[j] : __builtin_nan("");
+        }
+    }
+    __syncthreads();
+    if (!valid) {
+        if (tid == 0) a.scores[k] = -1;
+        return;
+    }
+    int c = 0;
+    for (int i = tid; i < a.n; i += kRansacBlock) {
+        const double *p = a.pts + 4 * (int64_t)i;
+        c += rs_inlier(h, p[0], p[1], p[2], p[3], a.t2) ? 1 : 0;
+    }
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off, 64);
+    if ((tid & 63) == 0) wsum[tid >> 6] = c;
+    __syncthreads();
+    if (tid == 0) {
+        int t = 0;
+        for (int w = 0; w < kRansacBlock / 64; w++) t += wsum[w];
+        a.scores[k] = t;
+    }
+}
+
+// grid (ceil(n / 256)), block 256: inlier mask of hypothesis a.best.
+extern "C" __global__ __launch_bounds__(256) void mcs_ransac_mask(const mcs::KRansacArgs a)
+{
+    using namespace mcs;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.n) return;
+    const double *h = a.hyps + (int64_t)a.best * 8;
+    const double *p = a.pts + 4 * (int64_t)i;
+    a.mask[i] = rs_inlier(h, p[0], p[1], p[2], p[3], a.t2) ? 1 : 0;
 }

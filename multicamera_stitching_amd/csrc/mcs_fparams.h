@@ -20,4 +20,17 @@ struct KHammingArgs {
     int nq, nt, per_chunk, pad_;
 };
 
+// RANSAC homography (mcs_ransac_core.h): one block per hypothesis scores it
+// over all correspondences; a second launch writes the best hypothesis' inlier mask.
+constexpr int kRansacBlock = 256;
+struct KRansacArgs {
+    const double *pts;    // n x 4: x, y (source), u, v (destination)
+    double *hyps;         // iters x 8: h0..h7 (h33 = 1); NaN for a rejected hypothesis
+    int32_t *scores;      // iters: inlier count, -1 for a rejected hypothesis
+    uint8_t *mask;        // n: inliers of hypothesis `best`
+    double t2;            // threshold^2
+    int n, iters, best;
+    uint32_t seed;
+};
+
 }  // namespace mcs

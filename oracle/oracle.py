@@ -72,6 +72,9 @@ def lib():
                                        ctypes.c_int, ctypes.c_int, P, ctypes.c_int, ctypes.c_int,
                                        P]
         L.orc_blend_stitch.restype = ctypes.c_int
+        L.orc_ransac_homography.argtypes = [P, ctypes.c_int, ctypes.c_double, ctypes.c_int,
+                                            ctypes.c_uint32, P, P, P]
+        L.orc_ransac_homography.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -246,3 +249,18 @@ def blend_stitch(flat: dict, cams, mode: int, interp: int = INTER_LINEAR, want_o
     if rc != 0:
         raise ValueError("orc_blend_stitch failed")
     return (out, owner) if want_owner else out
+
+
+def ransac_homography(src, dst, thresh, iters=2000, seed=0):
+    """RANSAC homography per csrc/mcs_ransac_core.h (orc_ransac.c): (H or None, mask, best_k,
+    per-hypothesis scores).  src/dst: (n, 2) float32 (converted to double like the GPU path)."""
+    src = np.asarray(src, np.float32).reshape(-1, 2)
+    dst = np.asarray(dst, np.float32).reshape(-1, 2)
+    pts = np.ascontiguousarray(np.concatenate([src, dst], axis=1).astype(np.float64))
+    n = pts.shape[0]
+    scores = np.zeros(iters, np.int32)
+    mask = np.zeros(n, np.uint8)
+    H = np.zeros(9, np.float64)
+    best = lib().orc_ransac_homography(_p(pts), n, float(thresh), iters, seed & 0xffffffff,
+                                       _p(scores), _p(mask), _p(H))
+    return (None if best < 0 else H.reshape(3, 3)), mask, best, scores
