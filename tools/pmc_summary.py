@@ -13,35 +13,34 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PMC = os.environ.get("MCS_PMC_DIR", os.path.join(ROOT, "gpurun_out", "pmc"))
 
 
-def main(kernel_prefix="mcs_stream_c3", workload=None, out=None):
-    vals = defaultdict(lambda: defaultdict(float))     # dispatch -> counter -> summed value
-    names = {}
+def family_counters(prefix):
+    """Per-dispatch averages of every counter over the dispatches of kernels named prefix*."""
+    vals = defaultdict(lambda: defaultdict(float))     # (pass, dispatch) -> counter -> value
     for f in sorted(glob.glob(os.path.join(PMC, "pass*", "**", "*counter_collection.csv"),
                               recursive=True)):
         p = f.split(os.sep)[len(PMC.split(os.sep))]
         for r in csv.DictReader(open(f)):
-            if not r["Kernel_Name"].startswith(kernel_prefix):
+            if not r["Kernel_Name"].startswith(prefix):
                 continue
-            key = (p, int(r["Dispatch_Id"]))
-            vals[key][r["Counter_Name"]] += float(r["Counter_Value"])
-            names[key] = r["Kernel_Name"]
+            vals[(p, int(r["Dispatch_Id"]))][r["Counter_Name"]] += float(r["Counter_Value"])
     per_counter = defaultdict(list)
-    for key, cs in vals.items():
+    for cs in vals.values():
         for c, v in cs.items():
             per_counter[c].append(v)
-    avg = {c: sum(v) / len(v) for c, v in per_counter.items()}
-    res = {"kernel": kernel_prefix, "workload": workload, "counters_per_launch": avg}
+    return {c: sum(v) / len(v) for c, v in per_counter.items()}
+
+
+def derived(avg):
+    res = {}
     if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
         fetch = avg["FETCH_SIZE"] * 1024 * 2
         write = avg["WRITE_SIZE"] * 1024
-        res.update(fetch_bytes_per_launch=fetch, write_bytes_per_launch=write,
-                   hbm_bytes_per_launch=int(fetch + write))
+        res.update(fetch_bytes=fetch, write_bytes=write, hbm_bytes=int(fetch + write))
     if "SQ_WAVE_CYCLES" in avg:
-        wc = avg["SQ_WAVE_CYCLES"]
         for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU",
                   "SQ_ACTIVE_INST_LDS"):
             if c in avg:
-                res[c + "_frac"] = avg[c] / wc
+                res[c + "_frac"] = avg[c] / avg["SQ_WAVE_CYCLES"]
     if "SQ_WAVES" in avg:
         for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD",
                   "SQ_INSTS_VMEM_WR", "SQ_INSTS_SMEM"):
@@ -51,6 +50,21 @@ def main(kernel_prefix="mcs_stream_c3", workload=None, out=None):
         res["lds_bank_conflict_frac"] = avg["SQ_LDS_BANK_CONFLICT"] / max(avg["SQ_LDS_IDX_ACTIVE"], 1)
     if "TCC_HIT_sum" in avg:
         res["l2_hit_rate"] = avg["TCC_HIT_sum"] / max(avg["TCC_HIT_sum"] + avg["TCC_MISS_sum"], 1)
+    return res
+
+
+def main(prefixes=("mcs_stream_c3",), workload=None, out=None):
+    """One stitch launch = one dispatch of each kernel family in `prefixes`; HBM bytes per launch
+    = the families' per-dispatch FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE, summed."""
+    res = {"kernels": list(prefixes), "workload": workload, "per_kernel": {}}
+    total = 0
+    for pre in prefixes:
+        avg = family_counters(pre)
+        d = derived(avg)
+        d["counters_per_dispatch"] = avg
+        res["per_kernel"][pre] = d
+        total += d.get("hbm_bytes", 0)
+    res["hbm_bytes_per_launch"] = int(total) if total else None
     text = json.dumps(res, indent=1, sort_keys=True)
     print(text)
     if out:
@@ -60,6 +74,6 @@ def main(kernel_prefix="mcs_stream_c3", workload=None, out=None):
 
 if __name__ == "__main__":
     wl = sys.argv[1] if len(sys.argv) > 1 else "4x1920x1080x3-linear-super0-F64-multiband"
-    kernel = sys.argv[2] if len(sys.argv) > 2 else "mcs_stream_c3"
+    kernels = sys.argv[2].split(",") if len(sys.argv) > 2 else ["mcs_stream_c3", "mcs_multiband"]
     out = sys.argv[3] if len(sys.argv) > 3 else os.path.join(ROOT, "profiles", "pmc_latest.json")
-    main(kernel_prefix=kernel, workload=wl, out=out)
+    main(prefixes=kernels, workload=wl, out=out)
