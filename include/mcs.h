@@ -155,6 +155,23 @@ int mcs_stitch_device(mcs_plan *plan, const uint8_t *const *d_cams,
  * byte count): touched_px[i] for i < n_cams.  Runs a one-off marking kernel. */
 int mcs_plan_footprint(mcs_plan *plan, int64_t *touched_px, int n_cams);
 
+/* ---- Streaming (host frames in, host mosaics out) ---------------------
+ * `depth` capture slots, each with pinned host staging and device buffers.  submit: the camera
+ * frames (sorted-label order, calibrated sizes, or NULL after filling mcs_stream_input() in
+ * place) are uploaded on a copy stream, stitched on a compute stream (one hipGraph per slot when
+ * use_graphs), and the mosaic downloaded on a second copy stream -- so consecutive captures
+ * overlap upload, stitch and download.  wait: blocks for that slot's mosaic and copies it to
+ * `out` (out_h x out_w x C, dense); a slot must be collected before it is reused.  The plan
+ * (blend mode included) is fixed for the stream's lifetime; the stream is bound to the device
+ * current at creation. */
+typedef struct mcs_stream mcs_stream;
+int mcs_stream_create(mcs_plan *plan, int depth, int use_graphs, mcs_stream **out);
+uint8_t *mcs_stream_input(mcs_stream *stream, int slot, int cam);
+int mcs_stream_next_slot(const mcs_stream *stream);
+int mcs_stream_submit(mcs_stream *stream, const uint8_t *const *cams, int *slot);
+int mcs_stream_wait(mcs_stream *stream, int slot, uint8_t *out);
+int mcs_stream_destroy(mcs_stream *stream);
+
 /* ---- Matching (per-frame estimation path) -------------------------------
  * Brute-force k=2 nearest neighbours of each query descriptor among the train descriptors under
  * the Hamming distance, as cv2.BFMatcher(cv2.NORM_HAMMING).knnMatch(query, train, k=2) (the

@@ -36,7 +36,8 @@ EXPORTS = (
     "mcs_stitch_host", "mcs_stitch_device", "mcs_plan_footprint", "mcs_plan_prepare",
     "mcs_plan_stats", "mcs_stitch_host_sized", "mcs_resize_linear_device",
     "mcs_match_hamming_knn2", "mcs_match_hamming_knn2_host", "mcs_plan_set_blend",
-    "mcs_ransac_homography_host",
+    "mcs_ransac_homography_host", "mcs_stream_create", "mcs_stream_input", "mcs_stream_next_slot",
+    "mcs_stream_submit", "mcs_stream_wait", "mcs_stream_destroy",
 )
 
 
@@ -169,6 +170,18 @@ def load() -> ctypes.CDLL:
         L.mcs_ransac_homography_host.argtypes = [P, P, I, ctypes.c_double, I, ctypes.c_uint32,
                                                  P, P, ctypes.POINTER(I), I]
         L.mcs_ransac_homography_host.restype = I
+        L.mcs_stream_create.argtypes = [P, I, I, ctypes.POINTER(P)]
+        L.mcs_stream_create.restype = I
+        L.mcs_stream_input.argtypes = [P, I, I]
+        L.mcs_stream_input.restype = P
+        L.mcs_stream_next_slot.argtypes = [P]
+        L.mcs_stream_next_slot.restype = I
+        L.mcs_stream_submit.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(I)]
+        L.mcs_stream_submit.restype = I
+        L.mcs_stream_wait.argtypes = [P, I, P]
+        L.mcs_stream_wait.restype = I
+        L.mcs_stream_destroy.argtypes = [P]
+        L.mcs_stream_destroy.restype = I
         L.mcs_plan_set_blend.argtypes = [P, I]
         L.mcs_plan_set_blend.restype = I
         L.mcs_match_hamming_knn2.argtypes = [P, I, P, I, P, P, I, P]
@@ -365,3 +378,41 @@ def ransac_homography(src, dst, thresh: float, iters: int = 2000, seed: int = 0,
                                        int(iters), int(seed) & 0xffffffff, H.ctypes.data,
                                        mask.ctypes.data, ctypes.byref(ninl), device))
     return (H.reshape(3, 3) if ninl.value > 0 else None), mask.reshape(-1, 1)
+
+
+class StreamPipeline:
+    """Host-frame pipeline over a plan (mcs_stream_*): submit() returns a slot, wait(slot) the
+    mosaic.  Keep at most `depth` captures in flight."""
+
+    def __init__(self, plan: "Plan", depth: int = 3, use_graphs: bool = True):
+        self._lib = load()
+        self.plan = plan
+        self.depth = depth
+        h = ctypes.c_void_p()
+        check(self._lib.mcs_stream_create(plan._h, depth, 1 if use_graphs else 0,
+                                          ctypes.byref(h)))
+        self._h = h
+
+    def submit(self, cams) -> int:
+        cams = [np.ascontiguousarray(c, dtype=np.uint8) for c in cams]
+        ptrs = (ctypes.c_void_p * len(cams))(*[c.ctypes.data for c in cams])
+        slot = ctypes.c_int(-1)
+        check(self._lib.mcs_stream_submit(self._h, ptrs, ctypes.byref(slot)))
+        return slot.value
+
+    def wait(self, slot: int, out=None) -> np.ndarray:
+        if out is None:
+            out = np.empty(self.plan.out_shape(), np.uint8)
+        check(self._lib.mcs_stream_wait(self._h, slot, out.ctypes.data))
+        return out
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.mcs_stream_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -38,6 +38,13 @@ namespace rt {
     X(hipEventElapsedTime, hipError_t, (float *, hipEvent_t, hipEvent_t))                      \
     X(hipModuleLoadData, hipError_t, (hipModule_t *, const void *))                            \
     X(hipModuleUnload, hipError_t, (hipModule_t))                                              \
+    X(hipStreamBeginCapture, hipError_t, (hipStream_t, hipStreamCaptureMode))                  \
+    X(hipStreamEndCapture, hipError_t, (hipStream_t, hipGraph_t *))                            \
+    X(hipGraphInstantiate, hipError_t, (hipGraphExec_t *, hipGraph_t, hipGraphNode_t *, char *, \
+                                        size_t))                                               \
+    X(hipGraphLaunch, hipError_t, (hipGraphExec_t, hipStream_t))                               \
+    X(hipGraphExecDestroy, hipError_t, (hipGraphExec_t))                                       \
+    X(hipGraphDestroy, hipError_t, (hipGraph_t))                                               \
     X(hipModuleGetFunction, hipError_t, (hipFunction_t *, hipModule_t, const char *))         \
     X(hipModuleLaunchKernel, hipError_t,                                                       \
       (hipFunction_t, unsigned int, unsigned int, unsigned int, unsigned int, unsigned int,   \

@@ -1,0 +1,229 @@
+// mcs_stream.cpp -- host-frame streaming pipeline over a plan:
+// double-(or deeper-)buffered pinned staging, H2D on one copy stream, the stitch (captured once
+// per slot into a hipGraph) on the compute stream, D2H on a second copy stream, so that the
+// upload of capture i+1, the stitch of capture i and the download of capture i-1 overlap.  Uses
+// only the public plan API (mcs_stitch_device) plus the bound HIP runtime.
+#include <cstring>
+#include <new>
+
+#include "mcs_common.h"
+
+namespace {
+constexpr int kMaxDepth = 8;
+}
+
+struct mcs_stream {
+    mcs_plan *plan = nullptr;
+    int device = 0, depth = 0, channels = 0, n_cams = 0, next = 0;
+    bool graphs = false;
+    int cam_w[MCS_MAX_CAMS] = {}, cam_h[MCS_MAX_CAMS] = {};
+    size_t cam_off[MCS_MAX_CAMS] = {};
+    size_t in_bytes = 0, out_bytes = 0;
+    int out_w = 0, out_h = 0;
+    hipStream_t up = nullptr, compute = nullptr, down = nullptr;
+    struct Slot {
+        uint8_t *h_in = nullptr, *h_out = nullptr, *d_in = nullptr, *d_out = nullptr;
+        hipEvent_t ev_in = nullptr, ev_k = nullptr, ev_out = nullptr;
+        hipGraphExec_t exec = nullptr;
+        bool busy = false;
+    } slot[kMaxDepth];
+};
+
+namespace {
+
+using mcs::rt::Api;
+
+int stitch_slot(mcs_stream *s, int i, hipStream_t st)
+{
+    const uint8_t *cams[MCS_MAX_CAMS];
+    int64_t strides[MCS_MAX_CAMS];
+    for (int c = 0; c < s->n_cams; c++) {
+        cams[c] = s->slot[i].d_in + s->cam_off[c];
+        strides[c] = (int64_t)s->cam_w[c] * s->cam_h[c] * s->channels;
+    }
+    const int64_t pitch = (int64_t)s->out_w * s->channels;
+    return mcs_stitch_device(s->plan, cams, strides, s->slot[i].d_out, pitch,
+                             pitch * s->out_h, 1, st);
+}
+
+void release(const Api *A, mcs_stream *s)
+{
+    for (void *q : {(void *)s->up, (void *)s->compute, (void *)s->down})
+        if (q) (void)A->hipStreamSynchronize((hipStream_t)q);
+    for (int i = 0; i < kMaxDepth; i++) {
+        mcs_stream::Slot &sl = s->slot[i];
+        if (sl.exec) (void)A->hipGraphExecDestroy(sl.exec);
+        if (sl.h_in) (void)A->hipHostFree(sl.h_in);
+        if (sl.h_out) (void)A->hipHostFree(sl.h_out);
+        if (sl.d_in) (void)A->hipFree(sl.d_in);
+        if (sl.d_out) (void)A->hipFree(sl.d_out);
+        for (hipEvent_t e : {sl.ev_in, sl.ev_k, sl.ev_out})
+            if (e) (void)A->hipEventDestroy(e);
+    }
+    for (hipStream_t q : {s->up, s->compute, s->down})
+        if (q) (void)A->hipStreamDestroy(q);
+}
+
+int build(const Api *A, mcs_stream *s)
+{
+    HIP_TRY(A->hipStreamCreateWithFlags(&s->up, hipStreamNonBlocking));
+    HIP_TRY(A->hipStreamCreateWithFlags(&s->compute, hipStreamNonBlocking));
+    HIP_TRY(A->hipStreamCreateWithFlags(&s->down, hipStreamNonBlocking));
+    for (int i = 0; i < s->depth; i++) {
+        mcs_stream::Slot &sl = s->slot[i];
+        HIP_TRY(A->hipHostMalloc((void **)&sl.h_in, s->in_bytes, 0));
+        HIP_TRY(A->hipHostMalloc((void **)&sl.h_out, s->out_bytes, 0));
+        HIP_TRY(A->hipMalloc((void **)&sl.d_in, s->in_bytes));
+        HIP_TRY(A->hipMalloc((void **)&sl.d_out, s->out_bytes));
+        HIP_TRY(A->hipEventCreateWithFlags(&sl.ev_in, hipEventDisableTiming));
+        HIP_TRY(A->hipEventCreateWithFlags(&sl.ev_k, hipEventDisableTiming));
+        HIP_TRY(A->hipEventCreateWithFlags(&sl.ev_out, hipEventDisableTiming));
+    }
+    // tables, modules and side streams exist before any capture: one plain run
+    int rc = mcs_plan_prepare(s->plan, s->compute);
+    if (rc == MCS_OK) rc = stitch_slot(s, 0, s->compute);
+    if (rc) return rc;
+    HIP_TRY(A->hipStreamSynchronize(s->compute));
+    if (!s->graphs) return MCS_OK;
+    for (int i = 0; i < s->depth; i++) {
+        hipGraph_t g = nullptr;
+        HIP_TRY(A->hipStreamBeginCapture(s->compute, hipStreamCaptureModeThreadLocal));
+        rc = stitch_slot(s, i, s->compute);
+        const hipError_t e = A->hipStreamEndCapture(s->compute, &g);
+        if (rc) {
+            if (g) (void)A->hipGraphDestroy(g);
+            return rc;
+        }
+        if (e != hipSuccess)
+            return mcs::fail(MCS_E_HIP, "stream capture: %s", A->hipGetErrorString(e));
+        const hipError_t e2 = A->hipGraphInstantiate(&s->slot[i].exec, g, nullptr, nullptr, 0);
+        (void)A->hipGraphDestroy(g);
+        if (e2 != hipSuccess)
+            return mcs::fail(MCS_E_HIP, "graph instantiate: %s", A->hipGetErrorString(e2));
+    }
+    return MCS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mcs_stream_create(mcs_plan *plan, int depth, int use_graphs, mcs_stream **out)
+{
+    mcs::clear_error();
+    if (!plan || !out) return mcs::fail(MCS_E_INVALID, "NULL plan/out");
+    *out = nullptr;
+    if (depth < 1 || depth > kMaxDepth)
+        return mcs::fail(MCS_E_INVALID, "depth %d (1..%d)", depth, kMaxDepth);
+    mcs_flat_desc fd;
+    int rc = mcs_plan_describe(plan, &fd);
+    if (rc) return rc;
+    if (fd.out_w <= 0 || fd.out_h <= 0) return mcs::fail(MCS_E_SHAPE, "empty mosaic");
+    const Api *A = mcs::rt::api();
+    if (!A) return MCS_E_HIP;
+    int dev = 0;
+    HIP_TRY(A->hipGetDevice(&dev));
+    mcs_stream *s = new (std::nothrow) mcs_stream();
+    if (!s) return mcs::fail(MCS_E_NOMEM, "stream");
+    s->plan = plan;
+    s->depth = depth;
+    s->graphs = use_graphs != 0;
+    s->channels = fd.channels;
+    s->n_cams = fd.n_cams;
+    for (int c = 0; c < fd.n_cams; c++) {
+        s->cam_w[c] = fd.cam_w[c];
+        s->cam_h[c] = fd.cam_h[c];
+        s->cam_off[c] = s->in_bytes;
+        s->in_bytes += ((size_t)fd.cam_w[c] * fd.cam_h[c] * fd.channels + 255) & ~(size_t)255;
+    }
+    s->out_w = fd.out_w;
+    s->out_h = fd.out_h;
+    s->out_bytes = (size_t)fd.out_w * fd.out_h * fd.channels;
+    rc = build(A, s);
+    if (rc) {
+        release(A, s);
+        delete s;
+        return rc;
+    }
+    s->device = dev;
+    *out = s;
+    return MCS_OK;
+}
+
+uint8_t *mcs_stream_input(mcs_stream *s, int slot, int cam)
+{
+    if (!s || slot < 0 || slot >= s->depth || cam < 0 || cam >= s->n_cams) return nullptr;
+    return s->slot[slot].h_in + s->cam_off[cam];
+}
+
+int mcs_stream_next_slot(const mcs_stream *s)
+{
+    if (!s) return mcs::fail(MCS_E_INVALID, "NULL stream");
+    return s->slot[s->next].busy ? mcs::fail(MCS_E_INVALID, "slot %d not yet collected (call "
+                                             "mcs_stream_wait)", s->next)
+                                 : s->next;
+}
+
+int mcs_stream_submit(mcs_stream *s, const uint8_t *const *cams, int *slot_out)
+{
+    mcs::clear_error();
+    if (!s) return mcs::fail(MCS_E_INVALID, "NULL stream");
+    const Api *A = mcs::rt::api();
+    if (!A) return MCS_E_HIP;
+    const int i = s->next;
+    mcs_stream::Slot &sl = s->slot[i];
+    if (sl.busy)
+        return mcs::fail(MCS_E_INVALID, "slot %d not yet collected (call mcs_stream_wait)", i);
+    mcs::DeviceGuard g(A, s->device);
+    if (cams)   // else: the caller filled mcs_stream_input() buffers in place
+        for (int c = 0; c < s->n_cams; c++)
+            if (cams[c])
+                memcpy(sl.h_in + s->cam_off[c], cams[c],
+                       (size_t)s->cam_w[c] * s->cam_h[c] * s->channels);
+    HIP_TRY(A->hipMemcpyAsync(sl.d_in, sl.h_in, s->in_bytes, hipMemcpyHostToDevice, s->up));
+    HIP_TRY(A->hipEventRecord(sl.ev_in, s->up));
+    HIP_TRY(A->hipStreamWaitEvent(s->compute, sl.ev_in, 0));
+    if (s->graphs) {
+        HIP_TRY(A->hipGraphLaunch(sl.exec, s->compute));
+    } else {
+        const int rc = stitch_slot(s, i, s->compute);
+        if (rc) return rc;
+    }
+    HIP_TRY(A->hipEventRecord(sl.ev_k, s->compute));
+    HIP_TRY(A->hipStreamWaitEvent(s->down, sl.ev_k, 0));
+    HIP_TRY(A->hipMemcpyAsync(sl.h_out, sl.d_out, s->out_bytes, hipMemcpyDeviceToHost, s->down));
+    HIP_TRY(A->hipEventRecord(sl.ev_out, s->down));
+    sl.busy = true;
+    s->next = (i + 1) % s->depth;
+    if (slot_out) *slot_out = i;
+    return MCS_OK;
+}
+
+int mcs_stream_wait(mcs_stream *s, int slot, uint8_t *out)
+{
+    mcs::clear_error();
+    if (!s || slot < 0 || slot >= s->depth) return mcs::fail(MCS_E_INVALID, "stream/slot");
+    mcs_stream::Slot &sl = s->slot[slot];
+    if (!sl.busy) return mcs::fail(MCS_E_INVALID, "slot %d has no capture in flight", slot);
+    const Api *A = mcs::rt::api();
+    if (!A) return MCS_E_HIP;
+    mcs::DeviceGuard g(A, s->device);
+    HIP_TRY(A->hipEventSynchronize(sl.ev_out));
+    if (out) memcpy(out, sl.h_out, s->out_bytes);
+    sl.busy = false;
+    return MCS_OK;
+}
+
+int mcs_stream_destroy(mcs_stream *s)
+{
+    if (!s) return MCS_OK;
+    const Api *A = mcs::rt::api();
+    if (A) {
+        mcs::DeviceGuard g(A, s->device);
+        release(A, s);
+    }
+    delete s;
+    return MCS_OK;
+}
+
+}  // extern "C"
