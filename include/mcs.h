@@ -187,6 +187,19 @@ int mcs_match_hamming_knn2(const uint8_t *d_query, int n_query, const uint8_t *d
 int mcs_match_hamming_knn2_host(const uint8_t *query, int n_query, const uint8_t *train,
                                 int n_train, int32_t *idx2, int32_t *dist2, int device);
 
+/* ---- Features -----------------------------------------------------------
+ * ORB keypoints + 256-bit descriptors of one image (u8, channels 1 = gray or 3 = BGR, dense),
+ * the per-frame replacement of detectAndDescribe (StitcherClass.py:356-403, SIFT there):
+ * nlevels pyramid (scale_factor, INTER_LINEAR), FAST-9 (fast_threshold) + NMS, Harris ranking
+ * with OpenCV's per-level quota of nfeatures, intensity-centroid orientation, rBRIEF (OpenCV's
+ * 31x31 pattern).  Specified in csrc/mcs_orb_core.h.  Outputs (capacity nfeatures): kp_xy
+ * (level-0 pixels), kp_response, kp_angle (degrees), kp_level (may be NULL), desc (32 B each),
+ * *n_out.  Synchronous. */
+int mcs_orb_detect_host(const uint8_t *image, int w, int h, int channels, int nfeatures,
+                        int nlevels, float scale_factor, int fast_threshold, float *kp_xy,
+                        float *kp_response, float *kp_angle, int *kp_level, uint8_t *desc,
+                        int *n_out, int device);
+
 /* ---- Homography estimation ----------------------------------------------
  * RANSAC homography of n correspondences src_xy[i] -> dst_xy[i] (float x, y pairs), the role of
  * cv2.findHomography(ptsA, ptsB, cv2.RANSAC, reprojThresh) at StitcherClass.py:440-441.  `iters`

@@ -37,7 +37,7 @@ EXPORTS = (
     "mcs_plan_stats", "mcs_stitch_host_sized", "mcs_resize_linear_device",
     "mcs_match_hamming_knn2", "mcs_match_hamming_knn2_host", "mcs_plan_set_blend",
     "mcs_ransac_homography_host", "mcs_stream_create", "mcs_stream_input", "mcs_stream_next_slot",
-    "mcs_stream_submit", "mcs_stream_wait", "mcs_stream_destroy",
+    "mcs_stream_submit", "mcs_stream_wait", "mcs_stream_destroy", "mcs_orb_detect_host",
 )
 
 
@@ -182,6 +182,9 @@ def load() -> ctypes.CDLL:
         L.mcs_stream_wait.restype = I
         L.mcs_stream_destroy.argtypes = [P]
         L.mcs_stream_destroy.restype = I
+        L.mcs_orb_detect_host.argtypes = [P, I, I, I, I, I, ctypes.c_float, I, P, P, P, P, P,
+                                          ctypes.POINTER(I), I]
+        L.mcs_orb_detect_host.restype = I
         L.mcs_plan_set_blend.argtypes = [P, I]
         L.mcs_plan_set_blend.restype = I
         L.mcs_match_hamming_knn2.argtypes = [P, I, P, I, P, P, I, P]
@@ -416,3 +419,26 @@ class StreamPipeline:
             self.close()
         except Exception:
             pass
+
+
+def orb_detect(image, nfeatures: int = 2000, nlevels: int = 8, scale_factor: float = 1.2,
+               fast_threshold: int = 20, device: int = 0):
+    """ORB on the GPU (mcs_orb_detect_host): image u8 gray (h, w) or BGR (h, w, 3).  Returns a
+    dict of xy (n, 2) float32 level-0 pixels, response (n,) float32, angle (n,) degrees,
+    level (n,) int32, desc (n, 32) uint8."""
+    L = load()
+    img = np.ascontiguousarray(image, np.uint8)
+    ch = 1 if img.ndim == 2 else img.shape[2]
+    h, w = img.shape[:2]
+    xy = np.zeros((max(nfeatures, 1), 2), np.float32)
+    resp = np.zeros(max(nfeatures, 1), np.float32)
+    ang = np.zeros(max(nfeatures, 1), np.float32)
+    lvl = np.zeros(max(nfeatures, 1), np.int32)
+    desc = np.zeros((max(nfeatures, 1), 32), np.uint8)
+    n = ctypes.c_int(0)
+    check(L.mcs_orb_detect_host(img.ctypes.data, w, h, ch, nfeatures, nlevels,
+                                float(scale_factor), fast_threshold, xy.ctypes.data,
+                                resp.ctypes.data, ang.ctypes.data, lvl.ctypes.data,
+                                desc.ctypes.data, ctypes.byref(n), device))
+    k = n.value
+    return dict(xy=xy[:k], response=resp[:k], angle=ang[:k], level=lvl[:k], desc=desc[:k])

@@ -249,8 +249,8 @@ int prepare(const Api *A, mcs_plan *p, hipStream_t s)
     args.desc = p->d_desc;
     args.fallback = p->d_fallback;
     size_t sz = sizeof(args);
-    void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, (void *)&args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz,
-                   HIP_LAUNCH_PARAM_END};
+    void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, (void *)&args, HIP_LAUNCH_PARAM_BUFFER_SIZE,
+                   &sz, HIP_LAUNCH_PARAM_END};
     HIP_TRY(A->hipModuleLaunchKernel(k->prepare[p->fd.channels][p->fd.interp], p->gx, p->gy, 1,
                                      mcs::kWave, mcs::kWavesPerBlock, 1, 0, s, nullptr, cfg));
     int nf = 0;

@@ -1,6 +1,7 @@
 // mcs_features.cpp -- C ABI of the per-frame estimation path (include/mcs.h, "Matching"):
 // brute-force Hamming kNN-2 on the GPU.
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <mutex>
 
@@ -8,6 +9,7 @@
 
 #include "mcs_common.h"
 #include "mcs_fparams.h"
+#include "mcs_orb_core.h"
 #include "mcs_ransac_core.h"
 
 namespace {
@@ -19,13 +21,16 @@ struct FeatureKernels {
     bool loaded = false;
     hipFunction_t knn2 = nullptr, knn2_finalize = nullptr;
     hipFunction_t ransac_score = nullptr, ransac_mask = nullptr;
+    hipFunction_t orb_gray = nullptr, orb_blur_h = nullptr, orb_blur_v = nullptr;
+    hipFunction_t orb_fast = nullptr, orb_nms = nullptr, orb_describe = nullptr;
 };
 FeatureKernels g_fk[mcs::kMaxDevices];
 std::mutex g_fk_mu;
 
 int feature_kernels(const Api *A, int device, const FeatureKernels **out)
 {
-    if (device < 0 || device >= mcs::kMaxDevices) return mcs::fail(MCS_E_INVALID, "device %d", device);
+    if (device < 0 || device >= mcs::kMaxDevices)
+        return mcs::fail(MCS_E_INVALID, "device %d", device);
     std::lock_guard<std::mutex> lk(g_fk_mu);
     FeatureKernels &k = g_fk[device];
     if (!k.loaded) {
@@ -39,6 +44,14 @@ int feature_kernels(const Api *A, int device, const FeatureKernels **out)
         if (rc == MCS_OK)
             rc = mcs::module_function(A, device, mcs::kModFeatures, "mcs_ransac_mask",
                                       &k.ransac_mask);
+        const struct {
+            const char *name;
+            hipFunction_t *f;
+        } orb[] = {{"mcs_orb_gray", &k.orb_gray},     {"mcs_orb_blur_h", &k.orb_blur_h},
+                   {"mcs_orb_blur_v", &k.orb_blur_v}, {"mcs_orb_fast", &k.orb_fast},
+                   {"mcs_orb_nms", &k.orb_nms},       {"mcs_orb_describe", &k.orb_describe}};
+        for (const auto &o : orb)
+            if (rc == MCS_OK) rc = mcs::module_function(A, device, mcs::kModFeatures, o.name, o.f);
         if (rc) return rc;
         k.loaded = true;
     }
@@ -199,8 +212,10 @@ int mcs_ransac_homography_host(const float *src_xy, const float *dst_xy, int n, 
     double hb8[8];
     hipStream_t s = nullptr;
     hipError_t e = A->hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
-    if (e == hipSuccess) e = A->hipMemcpyAsync((void *)a.pts, pts.data(), pb, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) rc = launch(A, k->ransac_score, iters, 1, mcs::kRansacBlock, &a, sizeof(a), s);
+    if (e == hipSuccess)
+        e = A->hipMemcpyAsync((void *)a.pts, pts.data(), pb, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess)
+        rc = launch(A, k->ransac_score, iters, 1, mcs::kRansacBlock, &a, sizeof(a), s);
     if (e == hipSuccess && rc == MCS_OK)
         e = A->hipMemcpyAsync(scores.data(), a.scores, sb, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess && rc == MCS_OK) e = A->hipStreamSynchronize(s);
@@ -241,6 +256,188 @@ int mcs_ransac_homography_host(const float *src_xy, const float *dst_xy, int n, 
     *n_inliers = best_score;
     if (mask)
         for (int i = 0; i < n; i++) mask[i] = m8[i];
+    return MCS_OK;
+}
+
+int mcs_orb_detect_host(const uint8_t *image, int w, int h, int channels, int nfeatures,
+                        int nlevels, float scale_factor, int fast_threshold, float *kp_xy,
+                        float *kp_response, float *kp_angle, int *kp_level, uint8_t *desc,
+                        int *n_out, int device)
+{
+    mcs::clear_error();
+    if (!image || !kp_xy || !desc || !n_out) return mcs::fail(MCS_E_INVALID, "NULL buffer");
+    if (w <= 0 || h <= 0 || (channels != 1 && channels != 3) || nfeatures < 0 ||
+        nlevels < 1 || nlevels > mcs::kOrbMaxLevels || !(scale_factor > 1.0f) ||
+        fast_threshold < 0 || fast_threshold > 255)
+        return mcs::fail(MCS_E_INVALID, "w=%d h=%d channels=%d nfeatures=%d nlevels=%d "
+                         "scale=%g threshold=%d", w, h, channels, nfeatures, nlevels,
+                         (double)scale_factor, fast_threshold);
+    *n_out = 0;
+    const Api *A = mcs::rt::api();
+    if (!A) return MCS_E_HIP;
+    DeviceGuard g(A, device);
+    if (g.err != hipSuccess)
+        return mcs::fail(MCS_E_HIP, "hipSetDevice(%d): %s", device, A->hipGetErrorString(g.err));
+    const FeatureKernels *k = nullptr;
+    int rc = feature_kernels(A, device, &k);
+    if (rc) return rc;
+    // level sizes and quotas, as OpenCV's ORB computes them (float arithmetic)
+    int lw[mcs::kOrbMaxLevels], lh[mcs::kOrbMaxLevels], quota[mcs::kOrbMaxLevels];
+    float lscale[mcs::kOrbMaxLevels];
+    size_t off[mcs::kOrbMaxLevels + 1] = {0};
+    for (int l = 0; l < nlevels; l++) {
+        lscale[l] = (float)std::pow((double)scale_factor, (double)l);
+        lw[l] = (int)std::lrint((float)w / lscale[l]);
+        lh[l] = (int)std::lrint((float)h / lscale[l]);
+        if (lw[l] < 1 || lh[l] < 1) return mcs::fail(MCS_E_INVALID, "level %d is empty", l);
+        off[l + 1] = off[l] + (((size_t)lw[l] * lh[l] + 255) & ~(size_t)255);
+    }
+    {
+        const float factor = (float)(1.0 / scale_factor);
+        float per = nfeatures * (1 - factor) / (1 - (float)std::pow((double)factor,
+                                                                    (double)nlevels));
+        int sum = 0;
+        for (int l = 0; l < nlevels - 1; l++) {
+            quota[l] = (int)std::lrint(per);
+            sum += quota[l];
+            per *= factor;
+        }
+        quota[nlevels - 1] = std::max(nfeatures - sum, 0);
+    }
+    const size_t pix = off[nlevels];
+    size_t cap_total = 0, cap[mcs::kOrbMaxLevels], coff[mcs::kOrbMaxLevels + 1] = {0};
+    for (int l = 0; l < nlevels; l++) {
+        cap[l] = std::max((size_t)4096, (size_t)lw[l] * lh[l] / 8);
+        coff[l + 1] = coff[l] + cap[l];
+        cap_total += cap[l];
+    }
+    // one allocation: input, levels, blur (u16 pass + u8), scores, candidates, counts, keypoints,
+    // descriptors, orientations
+    const size_t in_bytes = (size_t)w * h * channels;
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+        const size_t at = o;
+        o += (bytes + 255) & ~(size_t)255;
+        return at;
+    };
+    const size_t o_in = take(in_bytes), o_lvl = take(pix), o_h16 = take(2 * pix);
+    const size_t o_blur = take(pix), o_score = take(pix);
+    const size_t o_cand = take(cap_total * sizeof(mcs::OrbCand));
+    const size_t o_cnt = take(mcs::kOrbMaxLevels * sizeof(int));
+    const size_t o_kp = take((size_t)std::max(nfeatures, 1) * 3 * sizeof(int));
+    const size_t o_desc = take((size_t)std::max(nfeatures, 1) * 32);
+    const size_t o_or = take((size_t)std::max(nfeatures, 1) * 2 * sizeof(double));
+    uint8_t *buf = nullptr;
+    HIP_TRY(A->hipMalloc((void **)&buf, o));
+    hipStream_t s = nullptr;
+    std::vector<int> counts(nlevels);
+    std::vector<mcs::OrbCand> cand(cap_total);
+    std::vector<int> kp;
+    std::vector<double> orient, resp;
+    hipError_t e = A->hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    uint8_t *lvl0 = buf + o_lvl;
+    if (e == hipSuccess)
+        e = A->hipMemcpyAsync(buf + o_in, image, in_bytes, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = A->hipMemsetAsync(buf + o_cnt, 0, mcs::kOrbMaxLevels * sizeof(int), s);
+    if (e == hipSuccess) {
+        if (channels == 3) {
+            mcs::KGrayArgs ga;
+            ga.bgr = buf + o_in;
+            ga.gray = lvl0;
+            ga.n = w * h;
+            ga.pad_ = 0;
+            rc = launch(A, k->orb_gray, (w * h + 255) / 256, 1, 256, &ga, sizeof(ga), s);
+        } else {
+            e = A->hipMemcpyAsync(lvl0, buf + o_in, in_bytes, hipMemcpyDeviceToDevice, s);
+        }
+    }
+    for (int l = 1; l < nlevels && e == hipSuccess && rc == MCS_OK; l++)
+        rc = mcs_resize_linear_device(buf + o_lvl + off[l - 1], lw[l - 1], lh[l - 1], lw[l - 1],
+                                      0, buf + o_lvl + off[l], lw[l], lh[l], lw[l], 0, 1, 1,
+                                      device, s);
+    for (int l = 0; l < nlevels && e == hipSuccess && rc == MCS_OK; l++) {
+        mcs::KOrbLevelArgs la;
+        la.img = buf + o_lvl + off[l];
+        la.hblur = reinterpret_cast<uint16_t *>(buf + o_h16) + off[l];
+        la.blur = buf + o_blur + off[l];
+        la.score = buf + o_score + off[l];
+        la.cand = reinterpret_cast<mcs::OrbCand *>(buf + o_cand) + coff[l];
+        la.ncand = reinterpret_cast<int *>(buf + o_cnt) + l;
+        la.w = lw[l];
+        la.h = lh[l];
+        la.threshold = fast_threshold;
+        la.cap = (int)cap[l];
+        const unsigned gx = (unsigned)(lw[l] + 255) / 256;
+        for (hipFunction_t f : {k->orb_blur_h, k->orb_blur_v, k->orb_fast, k->orb_nms})
+            if (rc == MCS_OK) rc = launch(A, f, gx, lh[l], 256, &la, sizeof(la), s);
+    }
+    if (e == hipSuccess && rc == MCS_OK)
+        e = A->hipMemcpyAsync(counts.data(), buf + o_cnt, nlevels * sizeof(int),
+                              hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess && rc == MCS_OK)
+        e = A->hipMemcpyAsync(cand.data(), buf + o_cand, cap_total * sizeof(mcs::OrbCand),
+                              hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess && rc == MCS_OK) e = A->hipStreamSynchronize(s);
+    int n = 0;
+    if (e == hipSuccess && rc == MCS_OK) {
+        // per level: rank by response (desc), then y, then x; keep the level's quota
+        for (int l = 0; l < nlevels; l++) {
+            const int c = std::min(counts[l], (int)cap[l]);
+            mcs::OrbCand *b = cand.data() + coff[l];
+            std::sort(b, b + c, [](const mcs::OrbCand &p, const mcs::OrbCand &q) {
+                if (p.response != q.response) return p.response > q.response;
+                return p.y != q.y ? p.y < q.y : p.x < q.x;
+            });
+            for (int i = 0; i < std::min(c, quota[l]); i++) {
+                kp.push_back(l);
+                kp.push_back(b[i].x);
+                kp.push_back(b[i].y);
+                resp.push_back(b[i].response);
+            }
+        }
+        n = (int)kp.size() / 3;
+        orient.resize(2 * (size_t)std::max(n, 1));
+        if (n > 0) {
+            e = A->hipMemcpyAsync(buf + o_kp, kp.data(), kp.size() * sizeof(int),
+                                  hipMemcpyHostToDevice, s);
+            mcs::KOrbDescArgs da;
+            for (int l = 0; l < mcs::kOrbMaxLevels; l++) {
+                const int ll = l < nlevels ? l : 0;
+                da.img[l] = buf + o_lvl + off[ll];
+                da.blur[l] = buf + o_blur + off[ll];
+                da.w[l] = lw[ll];
+            }
+            da.kp = reinterpret_cast<const int *>(buf + o_kp);
+            da.desc = buf + o_desc;
+            da.orient = reinterpret_cast<double *>(buf + o_or);
+            da.n = n;
+            da.pad_ = 0;
+            if (e == hipSuccess) rc = launch(A, k->orb_describe, n, 1, 64, &da, sizeof(da), s);
+            if (e == hipSuccess && rc == MCS_OK)
+                e = A->hipMemcpyAsync(desc, buf + o_desc, (size_t)n * 32, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess && rc == MCS_OK)
+                e = A->hipMemcpyAsync(orient.data(), buf + o_or, (size_t)n * 2 * sizeof(double),
+                                      hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess && rc == MCS_OK) e = A->hipStreamSynchronize(s);
+        }
+    }
+    if (s) (void)A->hipStreamDestroy(s);
+    (void)A->hipFree(buf);
+    if (e != hipSuccess) return mcs::fail(MCS_E_HIP, "orb: %s", A->hipGetErrorString(e));
+    if (rc) return rc;
+    for (int i = 0; i < n; i++) {
+        const int l = kp[3 * i];
+        kp_xy[2 * i] = (float)kp[3 * i + 1] * lscale[l];
+        kp_xy[2 * i + 1] = (float)kp[3 * i + 2] * lscale[l];
+        if (kp_level) kp_level[i] = l;
+        if (kp_response) kp_response[i] = (float)resp[i];
+        if (kp_angle) {
+            double a = std::atan2(orient[2 * i + 1], orient[2 * i]) * (180.0 / M_PI);
+            if (a < 0) a += 360.0;
+            kp_angle[i] = (float)a;
+        }
+    }
+    *n_out = n;
     return MCS_OK;
 }
 

@@ -19,6 +19,7 @@
 
 #include "mcs_fparams.h"
 #include "mcs_ransac_core.h"
+#include "mcs_orb_core.h"
 
 namespace mcs {
 
@@ -137,4 +138,134 @@ extern "C" __global__ __launch_bounds__(256) void mcs_ransac_mask(const mcs::KRa
     const double *h = a.hyps + (int64_t)a.best * 8;
     const double *p = a.pts + 4 * (int64_t)i;
     a.mask[i] = rs_inlier(h, p[0], p[1], p[2], p[3], a.t2) ? 1 : 0;
+}
+
+// ---- ORB (NS-3) ----------------------------------------------------------------------------
+// BGR -> gray with OpenCV's fixed point: (1868 B + 9617 G + 4899 R + 8192) >> 14.
+extern "C" __global__ __launch_bounds__(256) void mcs_orb_gray(const mcs::KGrayArgs a)
+{
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.n) return;
+    const uint8_t *p = a.bgr + 3 * (int64_t)i;
+    a.gray[i] = (uint8_t)((1868 * p[0] + 9617 * p[1] + 4899 * p[2] + 8192) >> 14);
+}
+
+__device__ __forceinline__ int orb_refl(int i, int n)
+{
+    return i < 0 ? -i : (i >= n ? 2 * n - 2 - i : i);
+}
+
+// grid (ceil(w / 256), h): horizontal 7-tap pass (u16, exact).
+extern "C" __global__ __launch_bounds__(256) void mcs_orb_blur_h(const mcs::KOrbLevelArgs a)
+{
+    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
+    if (x >= a.w) return;
+    const uint8_t *r = a.img + (int64_t)y * a.w;
+    int s = 0;
+#pragma unroll
+    for (int i = 0; i < 7; i++) s += mcs::kOrbBlur[i] * r[orb_refl(x + i - 3, a.w)];
+    a.hblur[(int64_t)y * a.w + x] = (uint16_t)s;
+}
+
+// grid (ceil(w / 256), h): vertical pass, one rounding.
+extern "C" __global__ __launch_bounds__(256) void mcs_orb_blur_v(const mcs::KOrbLevelArgs a)
+{
+    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
+    if (x >= a.w) return;
+    int s = 0;
+#pragma unroll
+    for (int j = 0; j < 7; j++)
+        s += mcs::kOrbBlur[j] * (int)a.hblur[(int64_t)orb_refl(y + j - 3, a.h) * a.w + x];
+    a.blur[(int64_t)y * a.w + x] = (uint8_t)((s + 32768) >> 16);
+}
+
+// grid (ceil(w / 256), h): FAST scores of corners (score > threshold) where the NMS of a
+// keypoint candidate can look (one pixel around the keypoint region), 0 elsewhere.
+extern "C" __global__ __launch_bounds__(256) void mcs_orb_fast(const mcs::KOrbLevelArgs a)
+{
+    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
+    if (x >= a.w) return;
+    const int lo = mcs::kOrbEdge - 1;
+    uint8_t v = 0;
+    if (x >= lo && y >= lo && x < a.w - lo && y < a.h - lo) {
+        const int sc = mcs::orb_fast_score(a.img + (int64_t)y * a.w + x, a.w);
+        v = sc > a.threshold ? (uint8_t)sc : 0;
+    }
+    a.score[(int64_t)y * a.w + x] = v;
+}
+
+// grid (ceil(w / 256), h): 3x3 non-maximum suppression + Harris response; survivors appended.
+extern "C" __global__ __launch_bounds__(256) void mcs_orb_nms(const mcs::KOrbLevelArgs a)
+{
+    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
+    const int e = mcs::kOrbEdge;
+    if (x < e || y < e || x >= a.w - e || y >= a.h - e) return;
+    const uint8_t *s = a.score + (int64_t)y * a.w + x;
+    const int c = s[0];
+    if (c == 0) return;
+    bool keep = true;
+#pragma unroll
+    for (int dy = -1; dy <= 1; dy++)
+#pragma unroll
+        for (int dx = -1; dx <= 1; dx++)
+            if (dx || dy) keep = keep && c > s[dy * a.w + dx];
+    if (!keep) return;
+    const double r = mcs::orb_harris(a.img + (int64_t)y * a.w + x, a.w);
+    const int i = atomicAdd(a.ncand, 1);
+    if (i < a.cap) {
+        a.cand[i].x = x;
+        a.cand[i].y = y;
+        a.cand[i].response = r;
+    }
+}
+
+// grid (n), block 64: one wave per keypoint -- orientation moments (lane v sums row v of the
+// disk, wave reduction), then 4 rBRIEF pairs per lane packed into the 32 descriptor bytes.
+extern "C" __global__ __launch_bounds__(64) void mcs_orb_describe(const mcs::KOrbDescArgs a)
+{
+    using namespace mcs;
+    const int k = blockIdx.x, lane = threadIdx.x;
+    const int lvl = a.kp[3 * k], x = a.kp[3 * k + 1], y = a.kp[3 * k + 2];
+    const int w = a.w[lvl];
+    const uint8_t *p = a.img[lvl] + (int64_t)y * w + x;
+    long long m10 = 0, m01 = 0;
+    if (lane <= kOrbHalfPatch) {
+        const int v = lane;
+        if (v == 0) {
+            for (int u = -kOrbHalfPatch; u <= kOrbHalfPatch; u++) m10 += u * (int)p[u];
+        } else {
+            long long vs = 0;
+            const int d = kOrbUmax[v];
+            for (int u = -d; u <= d; u++) {
+                const int q = p[u + v * w], r = p[u - v * w];
+                vs += q - r;
+                m10 += (long long)u * (q + r);
+            }
+            m01 = v * vs;
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        m10 += __shfl_down(m10, off, 64);
+        m01 += __shfl_down(m01, off, 64);
+    }
+    m10 = __shfl(m10, 0, 64);
+    m01 = __shfl(m01, 0, 64);
+    const double fx = (double)m10, fy = (double)m01;
+    const double r = sqrt(fx * fx + fy * fy);
+    const double cs = r > 0.0 ? fx / r : 1.0, sn = r > 0.0 ? fy / r : 0.0;
+    const uint8_t *b = a.blur[lvl] + (int64_t)y * w + x;
+    uint32_t bits = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const signed char *t = kOrbPattern[4 * lane + j];
+        const int v1 = b[orb_rot_off(t[0], t[1], cs, sn, w)];
+        const int v2 = b[orb_rot_off(t[2], t[3], cs, sn, w)];
+        bits |= (uint32_t)(v1 < v2) << j;
+    }
+    const uint32_t hi = __shfl_down(bits, 1, 64);
+    if ((lane & 1) == 0) a.desc[32 * (int64_t)k + (lane >> 1)] = (uint8_t)(bits | (hi << 4));
+    if (lane == 0) {
+        a.orient[2 * k] = cs;
+        a.orient[2 * k + 1] = sn;
+    }
 }

@@ -33,4 +33,32 @@ struct KRansacArgs {
     uint32_t seed;
 };
 
+// ORB (mcs_orb_core.h).
+struct OrbCand {
+    int x, y;
+    double response;
+};
+struct KOrbLevelArgs {
+    const uint8_t *img;    // level image (w x h, dense)
+    uint16_t *hblur;       // horizontal blur pass
+    uint8_t *blur;         // blurred level
+    uint8_t *score;        // FAST scores of corners (0 elsewhere)
+    OrbCand *cand;         // NMS survivors with their Harris response
+    int *ncand;
+    int w, h, threshold, cap;
+};
+struct KOrbDescArgs {
+    const uint8_t *img[12], *blur[12];
+    int w[12];
+    const int *kp;         // n x 3: level, x, y
+    uint8_t *desc;         // n x 32
+    double *orient;        // n x 2: cos, sin
+    int n, pad_;
+};
+struct KGrayArgs {
+    const uint8_t *bgr;
+    uint8_t *gray;
+    int n, pad_;
+};
+
 }  // namespace mcs

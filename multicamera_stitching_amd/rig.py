@@ -136,6 +136,18 @@ def world_frames(C, width, height, channels=3, seed=0):
     return frames
 
 
+def corner_texture(h, w, seed=0, n_rects=None):
+    """Feature-rich u8 gray test image: random axis-aligned rectangles of random gray levels over
+    a mid-gray background (corners for FAST/ORB), clipped to [1, 255]."""
+    rng = np.random.default_rng(seed)
+    img = np.full((h, w), 128, np.int32)
+    for _ in range(n_rects or max(8, h * w // 900)):
+        x0, y0 = rng.integers(0, w), rng.integers(0, h)
+        rw, rh = rng.integers(4, max(5, w // 8)), rng.integers(4, max(5, h // 8))
+        img[y0:y0 + rh, x0:x0 + rw] = rng.integers(0, 256)
+    return np.clip(img, 1, 255).astype(np.uint8)
+
+
 def labels(n_cams):
     return ["CAM{}".format(i + 1) for i in range(n_cams)]
 

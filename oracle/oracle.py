@@ -75,6 +75,9 @@ def lib():
         L.orc_ransac_homography.argtypes = [P, ctypes.c_int, ctypes.c_double, ctypes.c_int,
                                             ctypes.c_uint32, P, P, P]
         L.orc_ransac_homography.restype = ctypes.c_int
+        L.orc_orb_detect.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_float, ctypes.c_int, P, P, P, P, P, P]
+        L.orc_orb_detect.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -264,3 +267,34 @@ def ransac_homography(src, dst, thresh, iters=2000, seed=0):
     best = lib().orc_ransac_homography(_p(pts), n, float(thresh), iters, seed & 0xffffffff,
                                        _p(scores), _p(mask), _p(H))
     return (None if best < 0 else H.reshape(3, 3)), mask, best, scores
+
+
+def orb_pattern() -> np.ndarray:
+    """The 256 x 4 rBRIEF pattern (OpenCV bit_pattern_31_) -- data, read from the generated
+    header the GPU code compiles (csrc/mcs_orb_pattern.h, tools/gen_orb_pattern.py)."""
+    import re
+    hdr = os.path.join(os.path.dirname(_HERE), "multicamera_stitching_amd", "csrc",
+                       "mcs_orb_pattern.h")
+    body = open(hdr).read().split("kOrbPattern[256][4] = {", 1)[1]
+    vals = [int(v) for v in re.findall(r"-?\d+", body.split("};", 1)[0])]
+    pat = np.array(vals, np.int32).reshape(256, 4)
+    assert pat[0].tolist() == [8, -3, 9, 5]
+    return pat
+
+
+def orb_detect(gray, nfeatures=2000, nlevels=8, scale_factor=1.2, threshold=20):
+    """ORB per csrc/mcs_orb_core.h (orc_orb.c): dict of xy (n, 2) float32, response (n,)
+    float64, level (n,), cs_sn (n, 2) orientation (cos, sin), desc (n, 32) uint8."""
+    g = np.ascontiguousarray(gray, np.uint8)
+    h, w = g.shape
+    pat = np.ascontiguousarray(orb_pattern())
+    xy = np.zeros((nfeatures, 2), np.float32)
+    resp = np.zeros(nfeatures, np.float64)
+    lvl = np.zeros(nfeatures, np.int32)
+    cs = np.zeros((nfeatures, 2), np.float64)
+    desc = np.zeros((nfeatures, 32), np.uint8)
+    n = lib().orc_orb_detect(_p(g), w, h, nfeatures, nlevels, scale_factor, threshold, _p(pat),
+                             _p(xy), _p(resp), _p(lvl), _p(cs), _p(desc))
+    if n < 0:
+        raise ValueError("orc_orb_detect failed")
+    return dict(xy=xy[:n], response=resp[:n], level=lvl[:n], cs_sn=cs[:n], desc=desc[:n])
