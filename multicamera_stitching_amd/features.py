@@ -4,15 +4,23 @@ Reference (StitcherClass.py:356-448): OpenCV SIFT keypoints + float descriptors,
 kNN-2, Lowe ratio (strict <), more than 4 matches, findHomography(RANSAC, reprojThresh).  This
 runs once per calibration (a keypress, video_mapping_node.py:187-188), not per frame.
 
-Backends, in order: OpenCV contrib SIFT when cv2 is importable (the reference's own algorithm,
-CPU); otherwise none -- calibrate_stitcher then logs an error and returns, exactly like the
-reference without opencv-contrib (:87-93), unless the caller passes precomputed homographies.
+Backends (MCS_FEATURES = auto | sift | orb): "sift" is OpenCV contrib SIFT when cv2 is
+importable (the reference's own algorithm, CPU, float L2 matching); "orb" is the GPU path of
+SURVEY.md 8 NS-3..5 -- ORB (mcs_orb_detect_host), brute-force Hamming kNN-2
+(mcs_match_hamming_knn2_host), the same ratio test, RANSAC (mcs_ransac_homography_host).  "auto"
+prefers SIFT (reference behaviour) and falls back to ORB when a GPU is present.  With neither,
+calibrate_stitcher logs an error and returns, exactly like the reference without opencv-contrib
+(:87-93), unless the caller passes precomputed homographies.
 """
 from __future__ import annotations
+
+import os
 
 import numpy as np
 
 from ._debugger import DEBUG_LEVEL_0
+
+ORB_NFEATURES = int(os.environ.get("MCS_ORB_NFEATURES", "2000"))
 
 
 def _cv2():
@@ -23,7 +31,7 @@ def _cv2():
         return None
 
 
-def available() -> bool:
+def _sift_available() -> bool:
     cv2 = _cv2()
     if cv2 is None:
         return False
@@ -36,9 +44,36 @@ def available() -> bool:
         return False
 
 
+def _orb_available() -> bool:
+    try:
+        from . import _capi
+        return _capi.device_count() > 0
+    except Exception:
+        return False
+
+
+def backend():
+    """"sift", "orb" or None (MCS_FEATURES selects; "auto" = SIFT, else ORB on the GPU)."""
+    want = os.environ.get("MCS_FEATURES", "auto").lower()
+    if want in ("auto", "sift") and _sift_available():
+        return "sift"
+    if want in ("auto", "orb") and _orb_available():
+        return "orb"
+    return None
+
+
+def available() -> bool:
+    return backend() is not None
+
+
 def detect_and_describe(owner, image):
+    b = backend()
+    if b == "orb":
+        from . import _capi
+        r = _capi.orb_detect(np.ascontiguousarray(image), nfeatures=ORB_NFEATURES)
+        return r["xy"], r["desc"]
     cv2 = _cv2()
-    if cv2 is None or not available():
+    if cv2 is None or b is None:
         owner.debugger(DEBUG_LEVEL_0, "OpenCV is not a contrib version, check for the module "
                        "xfeatures2d", log_type="err")
         return None, None
@@ -55,6 +90,16 @@ def detect_and_describe(owner, image):
 
 
 def match_keypoints(owner, kpsA, kpsB, featuresA, featuresB, ratio=0.75, reprojThresh=4.0):
+    if np.asarray(featuresA).dtype == np.uint8:     # binary (ORB) descriptors: the GPU path
+        from . import _capi
+        idx, dist = _capi.match_hamming_knn2(featuresA, featuresB)
+        matches = ratio_matches(idx, dist, ratio)
+        H = status = None
+        if len(matches) > 4:
+            ptsA = np.float32([kpsA[i] for (_, i) in matches])
+            ptsB = np.float32([kpsB[i] for (i, _) in matches])
+            H, status = _capi.ransac_homography(ptsA, ptsB, reprojThresh)
+        return H, matches, status
     cv2 = _cv2()
     raw = cv2.DescriptorMatcher_create("BruteForce").knnMatch(featuresA, featuresB, 2)
     matches = [(m[0].trainIdx, m[0].queryIdx) for m in raw

@@ -56,3 +56,30 @@ def test_gpu_estimation_chain_recovers_motion():
     g = np.c_[np.random.default_rng(0).uniform(200, 600, (20, 2)), np.ones(20)]
     p, q = g @ H.T, g @ Ht.T
     assert np.abs(p[:, :2] / p[:, 2:] - q[:, :2] / q[:, 2:]).max() < 2.0
+
+
+def test_dropin_calibrates_with_gpu_orb_backend(monkeypatch):
+    """No OpenCV: Stitcher.calibrate_stitcher estimates each stage's homography with the GPU
+    ORB -> Hamming -> ratio -> RANSAC path (the reference's detectAndDescribe/matchKeypoints
+    roles), then stitches the captures."""
+    from multicamera_stitching_amd import features
+    from multicamera_stitching_amd.StitcherClass import Stitcher
+    monkeypatch.setenv("MCS_FEATURES", "orb")
+    assert features.backend() == "orb"
+    world = rig.corner_texture(600, 1500, seed=7)
+    w = 640
+    cams = [np.ascontiguousarray(world[50:530, x:x + w]) for x in (0, 420, 840)]
+    images = dict(zip(["CAM1", "CAM2", "CAM3"], cams))
+    st = Stitcher(images)
+    st.calibrate_stitcher(images, save=False)
+    assert all(sb.cachedAH is not None for sb in st.stitchers)
+    out = st.stitch(images)
+    assert out.shape[0] >= 480 and out.shape[1] >= 1400
+    # the mosaic reproduces the world strip (paste of camera 1 over exact warps of the others)
+    y0 = st.stitchers[1].Bpts[0][1] if st.stitchers[1].Bpts else 0
+    ref = world[50:530, :out.shape[1]].astype(np.int16)
+    crop = out[y0:y0 + 480, :ref.shape[1]].astype(np.int16)
+    if crop.ndim == 3:
+        crop = crop[..., 0]
+    err = np.abs(crop[:, 700:1300] - ref[:, 700:1300])
+    assert np.median(err) <= 2
