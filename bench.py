@@ -42,13 +42,19 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--frames", type=int, default=64,
                     help="rig captures per launch (per GPU); SURVEY.md 8d: >= 64 per launch")
-    ap.add_argument("--cams", type=int, default=4)
+    ap.add_argument("--rig", choices=["chain", "cylinder"], default="chain",
+                    help="chain: BASELINE configs[1] (homography chain, the reference's path); "
+                         "cylinder: SURVEY.md 8 C4 (8 cameras at 45 degree yaw, f = 1100, "
+                         "cylindrical 360 panorama)")
+    ap.add_argument("--focal", type=float, default=1100.0, help="cylinder rig focal length (px)")
+    ap.add_argument("--cams", type=int, default=None, help="default 4 (chain) / 8 (cylinder)")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--channels", type=int, default=3)
     ap.add_argument("--interp", choices=["linear", "nearest"], default="linear")
     ap.add_argument("--super-mode", action="store_true")
-    ap.add_argument("--blend", choices=["multiband", "feather", "none"], default="multiband",
+    ap.add_argument("--blend", choices=["multiband", "feather", "seam", "none"],
+                    default="multiband",
                     help="multiband = BASELINE configs[1]; none = the reference's paste")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--gather", action="store_true",
@@ -77,14 +83,33 @@ def main():
     from multicamera_stitching_amd.StitcherClass import _stage_desc
 
     interp = _capi.MCS_INTER_LINEAR if args.interp == "linear" else _capi.MCS_INTER_NEAREST
-    st, images, _ = rig.calibrated_stitcher(args.cams, args.width, args.height, args.channels,
-                                            super_mode=args.super_mode, seed=0)
-    cams = [images[label] for label in st.img_labels]
-    descs = [_stage_desc(sb) for sb in st.stitchers]
-    plan = _capi.Plan(descs, args.width, args.height, args.channels, interp,
-                      device=torch.cuda.current_device())
+    cyl = args.rig == "cylinder"
+    if args.cams is None:
+        args.cams = 8 if cyl else 4
+    if cyl and args.blend == "none":
+        raise SystemExit("bench: a cylindrical rig has no paste order (use --blend seam)")
+    st = geo = None
+    if cyl:
+        rig_cams, cams, geo = rig.cylinder_rig(args.cams, args.width, args.height, args.focal,
+                                               args.channels, seed=0, jitter_deg=0.5)
+
+        def make_plan():
+            return _capi.Plan.cylindrical(rig_cams, geo["out_w"], geo["out_h"], geo["f_cyl"],
+                                          geo["u0"], geo["v0"], args.channels, interp,
+                                          device=torch.cuda.current_device())
+    else:
+        st, images, _ = rig.calibrated_stitcher(args.cams, args.width, args.height,
+                                                args.channels, super_mode=args.super_mode,
+                                                seed=0)
+        cams = [images[label] for label in st.img_labels]
+        descs = [_stage_desc(sb) for sb in st.stitchers]
+
+        def make_plan():
+            return _capi.Plan(descs, args.width, args.height, args.channels, interp,
+                              device=torch.cuda.current_device())
+    plan = make_plan()
     blend = {"none": _capi.MCS_BLEND_NONE, "feather": _capi.MCS_BLEND_FEATHER,
-             "multiband": _capi.MCS_BLEND_MULTIBAND}[args.blend]
+             "multiband": _capi.MCS_BLEND_MULTIBAND, "seam": _capi.MCS_BLEND_SEAM}[args.blend]
     plan.set_blend(blend)
     C = args.channels
     F = args.frames
@@ -145,11 +170,13 @@ def main():
     value = world * mpix_per_launch * args.steps / elapsed
     frame0 = d_out[0, :, :out_w * C].reshape(out_h, out_w, C).cpu().numpy() if rank == 0 else None
 
-    # the same launch with the reference's paste (no blend pass): the blend's share of the time
+    # the same launch with the reference's paste (cylinder: the hard seam) and no blend pass:
+    # the blend's share of the time
     paste_ms = None
-    if blend != _capi.MCS_BLEND_NONE:
-        ref = _capi.Plan(descs, args.width, args.height, args.channels, interp,
-                         device=torch.cuda.current_device())
+    if blend not in (_capi.MCS_BLEND_NONE, _capi.MCS_BLEND_SEAM):
+        ref = make_plan()
+        if cyl:
+            ref.set_blend(_capi.MCS_BLEND_SEAM)
         ref.prepare(stream.cuda_stream)
 
         def step_ref():
@@ -177,6 +204,8 @@ def main():
     traffic = None
     workload = (f"{args.cams}x{args.width}x{args.height}x{C}-{args.interp}-"
                 f"super{int(args.super_mode)}-F{F}-{args.blend}")
+    if cyl:
+        workload = f"cyl-f{args.focal:g}-" + workload
     try:
         pm = json.load(open(args.pmc_json))
         if pm.get("workload") == workload:
@@ -189,9 +218,11 @@ def main():
         cpu = None
         max_abs = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu, max_abs = cpu_baseline(st, cams, frame0, args, interp, out_w, out_h, plan, blend)
+            cpu, max_abs = cpu_baseline(st, cams, frame0, args, interp, out_w, out_h, plan, blend,
+                                        (rig_cams, geo) if cyl else None)
         result = {
-            "metric": "stitched MPix/sec (4-cam 1080p rig)",
+            "metric": ("stitched MPix/sec (8-cam 360 cylindrical rig)" if cyl else
+                       "stitched MPix/sec (4-cam 1080p rig)"),
             "value": round(value, 3),
             "unit": "MPix/s",
             "n_gpus": world,
@@ -204,12 +235,7 @@ def main():
             "dtype": "u8",
             "data": "synthetic",
             "config": {
-                "workload": ("C2 rig: %d x %dx%d BGR cameras, precomputed homographies, "
-                             "%s warpPerspective + %s" % (
-                                 args.cams, args.width, args.height, args.interp,
-                                 {"multiband": "3-level multi-band blend (SURVEY.md 8 NS-1)",
-                     "feather": "linear feather blend (SURVEY.md 8 NS-2)",
-                     "none": "overwrite paste (the reference's StitcherClass semantics)"}[args.blend])),
+                "workload": describe_workload(args, cyl),
                 "blend": args.blend,
                 "mosaic": [out_h, out_w, C],
                 "frames_per_step": F,
@@ -229,7 +255,8 @@ def main():
                 "bound": "hbm",
                 "kernel": "mcs_stream_c%d%s (one launch)" % (
                     C, {"multiband": " + mcs_multiband_c%d_i1" % C,
-                        "feather": " + mcs_feather_c%d_i1" % C, "none": ""}[args.blend]),
+                        "feather": " + mcs_feather_c%d_i1" % C, "none": "",
+                        "seam": ""}[args.blend]),
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -247,7 +274,20 @@ def main():
     return result
 
 
-def cpu_baseline(st, cams, frame0, args, interp, out_w, out_h, plan, blend):
+def describe_workload(args, cyl):
+    what = {"multiband": "3-level multi-band blend (SURVEY.md 8 NS-1)",
+            "feather": "linear feather blend (SURVEY.md 8 NS-2)",
+            "seam": "distance seam, no blend",
+            "none": "overwrite paste (the reference's StitcherClass semantics)"}[args.blend]
+    if cyl:
+        return (f"C4 rig: {args.cams} x {args.width}x{args.height} BGR cameras at "
+                f"{360.0 / args.cams:g} degree yaw steps, f = {args.focal:g}, cylindrical warp "
+                f"({args.interp}) + {what}")
+    return (f"C2 rig: {args.cams} x {args.width}x{args.height} BGR cameras, precomputed "
+            f"homographies, {args.interp} warpPerspective + {what}")
+
+
+def cpu_baseline(st, cams, frame0, args, interp, out_w, out_h, plan, blend, cyl=None):
     """The same workload on host cores (oracle/, C restatement), bounded sample.  Paste: the
     reference-structured cascade (per-stage warp into full canvases + paste, StitcherClass.py);
     blend modes: the flattened restatement of the blend (orc_blend.c)."""
@@ -262,12 +302,20 @@ def cpu_baseline(st, cams, frame0, args, interp, out_w, out_h, plan, blend):
         def run():
             return oracle.cascade_stitch(stages, cams, interp)
         what = "cascaded per-stage warpPerspective+paste"
+    elif cyl is not None:
+        rig_cams, g = cyl
+
+        def run():
+            return oracle.blend_stitch_cyl(rig_cams, g["out_w"], g["out_h"], g["f_cyl"], g["u0"],
+                                           g["v0"], cams, blend, interp)
+        what = ({1: "feather", 2: "3-level multi-band", 3: "seam"}[blend] +
+                " cylindrical panorama (orc_blend.c)")
     else:
         flat = plan.describe()
 
         def run():
             return oracle.blend_stitch(flat, cams, blend, interp)
-        what = {1: "feather", 2: "3-level multi-band"}[blend] + " blend (orc_blend.c)"
+        what = {1: "feather", 2: "3-level multi-band", 3: "seam"}[blend] + " blend (orc_blend.c)"
     want = run()
     max_abs = int(np.abs(want.astype(np.int16) - frame0.astype(np.int16)).max())
     n = 0

@@ -45,8 +45,8 @@ enum { MCS_INTER_NEAREST = 0, MCS_INTER_LINEAR = 1 };
  * reference implementation; specified in oracle/orc_blend.c): every pixel belongs to the
  * covering camera farthest from its own image edge; FEATHER averages the covering cameras
  * weighted by that edge distance, MULTIBAND blends a 3-level Laplacian pyramid across those
- * ownership seams. */
-enum { MCS_BLEND_NONE = 0, MCS_BLEND_FEATHER = 1, MCS_BLEND_MULTIBAND = 2 };
+ * ownership seams, SEAM copies the owner's sample (the seam without blending). */
+enum { MCS_BLEND_NONE = 0, MCS_BLEND_FEATHER = 1, MCS_BLEND_MULTIBAND = 2, MCS_BLEND_SEAM = 3 };
 
 #define MCS_MAX_STAGES 15
 #define MCS_MAX_CAMS (MCS_MAX_STAGES + 1)
@@ -101,6 +101,25 @@ const char *mcs_hip_runtime(void);
  * Host-side only: no device memory is touched until the first stitch call. */
 int mcs_plan_create(const mcs_stage_desc *stages, int n_stages, int cam0_w, int cam0_h,
                     int channels, int interp, int device, mcs_plan **out);
+/* A camera of a rotation-only rig projected onto a cylinder (SURVEY.md section 8 NS-6 / C4:
+ * 8 cameras at 45 degree yaw steps around one centre, f = 1100).  R: rig -> camera rotation,
+ * row-major (a rig ray d maps to R d in camera coordinates, z forward, y down); f, cx, cy:
+ * pinhole intrinsics in pixels; w, h: frame size.  Undistorted frames (see mcs_undistort_*). */
+typedef struct mcs_cyl_camera {
+    double R[9];
+    double f, cx, cy;
+    int w, h;
+} mcs_cyl_camera;
+
+/* Plan of a cylindrical panorama: output pixel (u, v) is the rig ray (sin t, h, cos t) with
+ * t = (u - u0) / f_cyl, h = (v - v0) / f_cyl; every camera is warped through it and the cameras
+ * meet at the blend seam (largest edge distance, ties to the lower camera index), blended by the
+ * plan's blend mode: MCS_BLEND_MULTIBAND by default, FEATHER or SEAM (MCS_BLEND_NONE is
+ * refused: there is no paste order).  The same fixed-point bilinear / nearest sampling as the
+ * homography plans; the per-column sin/cos and per-row h are computed once on the host. */
+int mcs_plan_create_cylindrical(const mcs_cyl_camera *cams, int n_cams, int out_w, int out_h,
+                                double f_cyl, double u0, double v0, int channels, int interp,
+                                int device, mcs_plan **out);
 int mcs_plan_destroy(mcs_plan *plan);
 int mcs_plan_out_shape(const mcs_plan *plan, int *w, int *h, int *channels);
 int mcs_plan_describe(const mcs_plan *plan, mcs_flat_desc *out);
@@ -119,7 +138,8 @@ int mcs_plan_stats(const mcs_plan *plan, int64_t *stats, int n);
 /* Blend mode of the plan (MCS_BLEND_*; default NONE = the reference's paste).  Changing it drops
  * the prepared tables (rebuilt by mcs_plan_prepare or the next stitch).  FEATHER / MULTIBAND
  * replace the reference's paste with the blends of SURVEY.md 8 NS-2 / NS-1; MULTIBAND supports
- * up to 4 cameras meeting within 16 px (else MCS_E_UNSUPPORTED at prepare). */
+ * up to 4 cameras meeting within 16 px (else MCS_E_UNSUPPORTED at prepare).  Cylindrical plans
+ * refuse NONE. */
 int mcs_plan_set_blend(mcs_plan *plan, int mode);
 
 /* Stitcher.stitch on host arrays (drop-in path, :114-136): cams[i] is the i-th camera in

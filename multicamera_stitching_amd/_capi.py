@@ -25,6 +25,7 @@ MCS_INTER_LINEAR = 1
 MCS_BLEND_NONE = 0
 MCS_BLEND_FEATHER = 1
 MCS_BLEND_MULTIBAND = 2
+MCS_BLEND_SEAM = 3
 MCS_MAX_STAGES = 15
 MCS_MAX_CAMS = MCS_MAX_STAGES + 1
 ABI_VERSION = 1
@@ -38,6 +39,7 @@ EXPORTS = (
     "mcs_match_hamming_knn2", "mcs_match_hamming_knn2_host", "mcs_plan_set_blend",
     "mcs_ransac_homography_host", "mcs_stream_create", "mcs_stream_input", "mcs_stream_next_slot",
     "mcs_stream_submit", "mcs_stream_wait", "mcs_stream_destroy", "mcs_orb_detect_host",
+    "mcs_plan_create_cylindrical",
 )
 
 
@@ -186,6 +188,10 @@ def load() -> ctypes.CDLL:
                                           ctypes.POINTER(I), I]
         L.mcs_orb_detect_host.restype = I
         L.mcs_plan_set_blend.argtypes = [P, I]
+        L.mcs_plan_create_cylindrical.argtypes = [ctypes.POINTER(CylCamera), I, I, I,
+                                                  ctypes.c_double, ctypes.c_double,
+                                                  ctypes.c_double, I, I, I, ctypes.POINTER(P)]
+        L.mcs_plan_create_cylindrical.restype = I
         L.mcs_plan_set_blend.restype = I
         L.mcs_match_hamming_knn2.argtypes = [P, I, P, I, P, P, I, P]
         L.mcs_match_hamming_knn2.restype = I
@@ -224,18 +230,34 @@ def device_count() -> int:
     return n.value if rc == MCS_OK else 0
 
 
+class CylCamera(ctypes.Structure):
+    """include/mcs.h mcs_cyl_camera: rig -> camera rotation R (row-major), f, cx, cy, w, h."""
+    _fields_ = [
+        ("R", ctypes.c_double * 9),
+        ("f", ctypes.c_double),
+        ("cx", ctypes.c_double),
+        ("cy", ctypes.c_double),
+        ("w", ctypes.c_int),
+        ("h", ctypes.c_int),
+    ]
+
+
 class Plan:
-    """Owning handle of an mcs_plan (flattened geometry of one calibrated chain)."""
+    """Owning handle of an mcs_plan (flattened geometry of one calibrated chain, or of a
+    cylindrical rig: Plan.cylindrical)."""
 
     def __init__(self, stages, cam0_w: int, cam0_h: int, channels: int,
-                 interp: int = MCS_INTER_LINEAR, device: int = 0):
+                 interp: int = MCS_INTER_LINEAR, device: int = 0, _handle=None):
         L = load()
-        arr = (StageDesc * max(1, len(stages)))()
-        for i, s in enumerate(stages):
-            arr[i] = s
-        h = ctypes.c_void_p()
-        check(L.mcs_plan_create(arr, len(stages), int(cam0_w), int(cam0_h), int(channels),
-                                int(interp), int(device), ctypes.byref(h)))
+        if _handle is None:
+            arr = (StageDesc * max(1, len(stages)))()
+            for i, s in enumerate(stages):
+                arr[i] = s
+            h = ctypes.c_void_p()
+            check(L.mcs_plan_create(arr, len(stages), int(cam0_w), int(cam0_h), int(channels),
+                                    int(interp), int(device), ctypes.byref(h)))
+        else:
+            h = _handle
         self._h = h
         self._lib = L
         w, hh, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
@@ -248,6 +270,25 @@ class Plan:
         self.flat = fd
         self.n_cams = fd.n_cams
         self.cam_shapes = [(fd.cam_h[i], fd.cam_w[i]) for i in range(fd.n_cams)]
+
+    @classmethod
+    def cylindrical(cls, cams, out_w: int, out_h: int, f_cyl: float, u0: float, v0: float,
+                    channels: int, interp: int = MCS_INTER_LINEAR, device: int = 0):
+        """mcs_plan_create_cylindrical: cams = [dict(R=3x3, f=, cx=, cy=, w=, h=)]; the plan
+        blends with MCS_BLEND_MULTIBAND until set_blend changes it."""
+        L = load()
+        arr = (CylCamera * max(1, len(cams)))()
+        for i, c in enumerate(cams):
+            arr[i].R = (ctypes.c_double * 9)(*[float(v) for v in
+                                               np.asarray(c["R"], np.float64).reshape(9)])
+            arr[i].f, arr[i].cx, arr[i].cy = float(c["f"]), float(c["cx"]), float(c["cy"])
+            arr[i].w, arr[i].h = int(c["w"]), int(c["h"])
+        h = ctypes.c_void_p()
+        check(L.mcs_plan_create_cylindrical(arr, len(cams), int(out_w), int(out_h),
+                                            ctypes.c_double(f_cyl), ctypes.c_double(u0),
+                                            ctypes.c_double(v0), int(channels), int(interp),
+                                            int(device), ctypes.byref(h)))
+        return cls(None, 0, 0, channels, interp, device, _handle=h)
 
     @property
     def handle(self):
@@ -324,7 +365,8 @@ class Plan:
                 "blend_tiles": arr[6]}
 
     def set_blend(self, mode: int):
-        """MCS_BLEND_NONE (reference paste), MCS_BLEND_FEATHER or MCS_BLEND_MULTIBAND."""
+        """MCS_BLEND_NONE (reference paste), MCS_BLEND_FEATHER, MCS_BLEND_MULTIBAND or
+        MCS_BLEND_SEAM (owner only)."""
         check(self._lib.mcs_plan_set_blend(self._h, int(mode)))
         return self
 

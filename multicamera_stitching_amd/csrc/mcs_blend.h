@@ -34,7 +34,7 @@ __device__ __forceinline__ void slot_xy(const KParams &P, int s, int x, int y, i
     w = S.src_w;
     h = S.src_h;
     int X, Y;
-    map_exact<INTERP>(S, x + S.offx, y + S.offy, X, Y);
+    stage_map<INTERP>(P, S, x, y, X, Y);
     if (INTERP == MCS_INTER_NEAREST) {
         x32 = sat_i16(X) * 32;
         y32 = sat_i16(Y) * 32;

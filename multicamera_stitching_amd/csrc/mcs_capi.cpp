@@ -3,10 +3,12 @@
 // Replaces, for a calibrated chain, the per-frame work of Stitcher.stitch
 // (PostScripts/Stitcher/StitcherClass.py:114-136).  No exception crosses this boundary: every
 // entry point returns an MCS_* status and leaves a message in mcs_last_error().
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
 #include <new>
+#include <vector>
 
 #include "hip_rt.h"
 #include "mcs_common.h"
@@ -38,6 +40,10 @@ struct mcs_plan {
     uint8_t *d_owner = nullptr;
     uint32_t *d_binfo = nullptr;
     int *d_blist = nullptr;
+    // cylindrical plans: per-column (sin, cos) and per-row h, host copy and device table
+    bool cyl = false;
+    std::vector<double> cyl_tab;
+    double *d_cyl = nullptr;
 };
 
 #define MCS_VERSION_STRING "mcs 0.1.0 (gfx950 code object, HIP module launch)"
@@ -220,6 +226,18 @@ void release_tables(const Api *A, mcs_plan *p)
     p->n_fallback = p->n_blend = 0;
 }
 
+// Cylindrical plans: the per-column / per-row table on the plan's device (once).
+int ensure_cyl(const Api *A, mcs_plan *p, hipStream_t s)
+{
+    if (!p->cyl || p->d_cyl) return MCS_OK;
+    const size_t bytes = p->cyl_tab.size() * sizeof(double);
+    HIP_TRY(A->hipMalloc((void **)&p->d_cyl, bytes));
+    HIP_TRY(A->hipMemcpyAsync(p->d_cyl, p->cyl_tab.data(), bytes, hipMemcpyHostToDevice, s));
+    HIP_TRY(A->hipStreamSynchronize(s));
+    p->kp.cyl_tab = p->d_cyl;
+    return MCS_OK;
+}
+
 // Prepared tables of a plan: one prepare launch, then the fallback-tile count is read back.
 // Allocates and synchronises: call before graph capture (the stitch entry points call it lazily).
 int prepare(const Api *A, mcs_plan *p, hipStream_t s)
@@ -235,7 +253,9 @@ int prepare(const Api *A, mcs_plan *p, hipStream_t s)
         p->prepared = true;
         return MCS_OK;
     }
-    if (p->blend != MCS_BLEND_NONE) {
+    rc = ensure_cyl(A, p, s);
+    if (rc) return rc;
+    if (p->blend == MCS_BLEND_FEATHER || p->blend == MCS_BLEND_MULTIBAND) {
         rc = prepare_blend(A, p, k, s);
         if (rc) return rc;
     }
@@ -387,6 +407,7 @@ int launch_stitch(const Api *A, mcs_plan *p, const mcs::KParams &kp, int n_frame
     for (int j = 0; j < p->fd.n_stages; j++)
         uniform = uniform && kp.cam_fstride[p->fd.st[j].cam] == kp.cam_fstride[0];
     mcs::KParams P = kp;
+    P.cyl_tab = p->kp.cyl_tab;   // set by prepare on a cylindrical plan's first use
     if (uniform) return launch_pair(A, p, k, P, n_frames, s);
     for (int f = 0; f < n_frames; f++) {
         for (int i = 0; i < p->fd.n_cams; i++)
@@ -448,6 +469,75 @@ int mcs_plan_create(const mcs_stage_desc *stages, int n_stages, int cam0_w, int 
     return MCS_OK;
 }
 
+int mcs_plan_create_cylindrical(const mcs_cyl_camera *cams, int n_cams, int out_w, int out_h,
+                                double f_cyl, double u0, double v0, int channels, int interp,
+                                int device, mcs_plan **out)
+{
+    mcs::clear_error();
+    if (!cams || !out) return mcs::fail(MCS_E_INVALID, "NULL cams/out");
+    *out = nullptr;
+    if (device < 0 || device >= kMaxDevices) return mcs::fail(MCS_E_INVALID, "device=%d", device);
+    if (n_cams < 1 || n_cams > MCS_MAX_STAGES)
+        return mcs::fail(MCS_E_INVALID, "n_cams %d (1..%d)", n_cams, MCS_MAX_STAGES);
+    if (channels < 1 || channels > 4) return mcs::fail(MCS_E_INVALID, "channels %d", channels);
+    if (interp != MCS_INTER_NEAREST && interp != MCS_INTER_LINEAR)
+        return mcs::fail(MCS_E_INVALID, "interp %d", interp);
+    if (out_w < 1 || out_h < 1 || (int64_t)out_w * out_h * channels > ((int64_t)1 << 31))
+        return mcs::fail(MCS_E_SHAPE, "panorama %dx%d", out_w, out_h);
+    if (!(f_cyl > 0.0) || !std::isfinite(u0) || !std::isfinite(v0))
+        return mcs::fail(MCS_E_INVALID, "f_cyl / u0 / v0");
+    for (int c = 0; c < n_cams; c++) {
+        const mcs_cyl_camera &k = cams[c];
+        if (k.w < 1 || k.h < 1 || k.w > 32767 || k.h > 32767)
+            return mcs::fail(MCS_E_SHAPE, "camera %d: %dx%d", c, k.w, k.h);
+        bool fin = std::isfinite(k.f) && k.f > 0.0 && std::isfinite(k.cx) && std::isfinite(k.cy);
+        for (double r : k.R) fin = fin && std::isfinite(r);
+        if (!fin) return mcs::fail(MCS_E_INVALID, "camera %d: R / f / cx / cy", c);
+    }
+    mcs_plan *p = new (std::nothrow) mcs_plan();
+    if (!p) return mcs::fail(MCS_E_NOMEM, "plan allocation");
+    mcs_flat_desc &fd = p->fd;
+    memset(&fd, 0, sizeof(fd));
+    fd.n_stages = n_cams;
+    fd.out_w = out_w;
+    fd.out_h = out_h;
+    fd.channels = channels;
+    fd.interp = interp;
+    fd.n_cams = n_cams;
+    for (int c = 0; c < n_cams; c++) {
+        fd.cam_w[c] = cams[c].w;
+        fd.cam_h[c] = cams[c].h;
+        mcs_flat_stage &st = fd.st[c];
+        memcpy(st.minv, cams[c].R, sizeof(st.minv));   // the rotation (describe: R, not H^-1)
+        st.rect[2] = out_w;
+        st.rect[3] = out_h;
+        st.bw0 = 1;
+        st.cam = c;
+    }
+    mcs::fill_kparams(fd, &p->kp);
+    p->kp.cam0_w = p->kp.cam0_h = 0;   // no integer-placed camera: every camera is a stage
+    for (int c = 0; c < n_cams; c++) {
+        mcs::KStage &k = p->kp.st[c];
+        k.kind = mcs::kStageCylinder;
+        k.f = cams[c].f;
+        k.cx = cams[c].cx;
+        k.cy = cams[c].cy;
+    }
+    p->cyl = true;
+    p->cyl_tab.resize(2 * (size_t)out_w + out_h);
+    for (int u = 0; u < out_w; u++) {
+        const double t = ((double)u - u0) / f_cyl;
+        p->cyl_tab[2 * u] = std::sin(t);
+        p->cyl_tab[2 * u + 1] = std::cos(t);
+    }
+    for (int v = 0; v < out_h; v++) p->cyl_tab[2 * (size_t)out_w + v] = ((double)v - v0) / f_cyl;
+    p->blend = MCS_BLEND_MULTIBAND;
+    p->kp.blend = MCS_BLEND_MULTIBAND;
+    p->device = device;
+    *out = p;
+    return MCS_OK;
+}
+
 int mcs_plan_destroy(mcs_plan *p)
 {
     if (!p) return MCS_OK;
@@ -469,6 +559,7 @@ int mcs_plan_destroy(mcs_plan *p)
             if (p->d_owner) (void)A->hipFree(p->d_owner);
             if (p->d_binfo) (void)A->hipFree(p->d_binfo);
             if (p->d_blist) (void)A->hipFree(p->d_blist);
+            if (p->d_cyl) (void)A->hipFree(p->d_cyl);
             if (p->side) (void)A->hipStreamSynchronize(p->side);
             if (p->stream) (void)A->hipStreamDestroy(p->stream);
             if (p->side) (void)A->hipStreamDestroy(p->side);
@@ -649,8 +740,12 @@ int mcs_plan_set_blend(mcs_plan *p, int mode)
 {
     mcs::clear_error();
     if (!p) return mcs::fail(MCS_E_INVALID, "NULL plan");
-    if (mode != MCS_BLEND_NONE && mode != MCS_BLEND_FEATHER && mode != MCS_BLEND_MULTIBAND)
+    if (mode != MCS_BLEND_NONE && mode != MCS_BLEND_FEATHER && mode != MCS_BLEND_MULTIBAND &&
+        mode != MCS_BLEND_SEAM)
         return mcs::fail(MCS_E_INVALID, "blend mode %d", mode);
+    if (p->cyl && mode == MCS_BLEND_NONE)
+        return mcs::fail(MCS_E_INVALID, "a cylindrical plan has no paste order: blend mode "
+                         "NONE is not defined for it (use SEAM, FEATHER or MULTIBAND)");
     if (mode == p->blend) return MCS_OK;
     if (p->prepared) {
         const Api *A = mcs::rt::api();
@@ -689,6 +784,8 @@ int mcs_plan_footprint(mcs_plan *p, int64_t *touched_px, int n_cams)
     if (rc) return rc;
     const Kernels *k = nullptr;
     rc = kernels(A, p->device, &k);
+    if (rc) return rc;
+    rc = ensure_cyl(A, p, p->stream);
     if (rc) return rc;
     const int n = p->fd.n_cams;
     uint8_t *masks[MCS_MAX_CAMS] = {};

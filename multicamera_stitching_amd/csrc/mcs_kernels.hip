@@ -51,6 +51,33 @@ __device__ __forceinline__ void map_exact(const KStage &S, int X, int Y, int &xo
     yo = cv_round_clamped((Y0 + S.m[3] * dx1) * W);
 }
 
+// Source coordinate of output pixel (x, y) under stage S, in map_exact's units.  Cylinder
+// stages (mcs_plan_create_cylindrical): ray (sin t, h, cos t) of the panorama column/row, rotated
+// into the camera (d = R ray, explicit summation order), projected x = f dx / dz + cx; rays
+// behind the camera map far outside every frame.
+template <int INTERP>
+__device__ __forceinline__ void stage_map(const KParams &P, const KStage &S, int x, int y,
+                                          int &xo, int &yo)
+{
+    if (S.kind == kStageHomography) {
+        map_exact<INTERP>(S, x + S.offx, y + S.offy, xo, yo);
+        return;
+    }
+    const double sn = P.cyl_tab[2 * x], cs = P.cyl_tab[2 * x + 1];
+    const double hv = P.cyl_tab[2 * P.out_w + y];
+    const double dx = (S.m[0] * sn + S.m[1] * hv) + S.m[2] * cs;
+    const double dy = (S.m[3] * sn + S.m[4] * hv) + S.m[5] * cs;
+    const double dz = (S.m[6] * sn + S.m[7] * hv) + S.m[8] * cs;
+    if (!(dz > 0.0)) {
+        xo = yo = INTERP == MCS_INTER_LINEAR ? -(1 << 25) : -(1 << 20);
+        return;
+    }
+    const double sx = (S.f * dx) / dz + S.cx, sy = (S.f * dy) / dz + S.cy;
+    const double k = INTERP == MCS_INTER_LINEAR ? 32.0 : 1.0;
+    xo = cv_round_clamped(sx * k);
+    yo = cv_round_clamped(sy * k);
+}
+
 // 8 bytes starting at byte offset o of a frame of `fbytes` bytes (only the first NB are used).
 // Unaligned dwordx2 in the common case; an in-bounds dword path at the very end of a frame.
 template <int NB>
@@ -268,7 +295,7 @@ __device__ __forceinline__ Geo describe_geo(const KParams &P, int x, int y)
         g.cam = S.cam;
         sw = S.src_w;
         sh = S.src_h;
-        map_exact<INTERP>(S, x + S.offx, y + S.offy, X, Y);
+        stage_map<INTERP>(P, S, x, y, X, Y);
         if (INTERP == MCS_INTER_NEAREST) {   // remapNearest: a copy of (X, Y) or the border value
             X = sat_i16(X);
             Y = sat_i16(Y);
@@ -779,7 +806,7 @@ __device__ __forceinline__ void footprint_mark(const KParams &P, uint8_t *const 
     }
     const KStage &S = P.st[s];
     int X, Y;
-    map_exact<INTERP>(S, x + S.offx, y + S.offy, X, Y);
+    stage_map<INTERP>(P, S, x, y, X, Y);
     if (INTERP == MCS_INTER_NEAREST) {
         mark(S.cam, sat_i16(X), sat_i16(Y), S.src_w, S.src_h);
     } else {

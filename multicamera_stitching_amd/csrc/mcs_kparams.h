@@ -18,8 +18,12 @@ struct KStage {
     int bw_shift;             // log2(bw0) when bw0 is a power of two, else -1
     int cam;                  // camera sampled by this stage
     int src_w, src_h;         // its size
-    int pad_;
+    int kind;                 // kStageHomography (m = inverted H) or kStageCylinder (m = R)
+    double f, cx, cy;         // kStageCylinder: pinhole intrinsics of the camera
 };
+
+constexpr int kStageHomography = 0;
+constexpr int kStageCylinder = 1;
 
 struct KParams {
     int n_stages;
@@ -27,6 +31,9 @@ struct KParams {
     int cam0_offx, cam0_offy;
     int cam0_w, cam0_h;
     int blend;                     // MCS_BLEND_*: which camera owns a pixel (paste or blend rule)
+    // Cylinder plans: (sin theta, cos theta) per output column, then h per output row (computed
+    // once on the host, so that device and oracle share every transcendental value bit for bit)
+    const double *cyl_tab;
     const uint8_t *cams[MCS_MAX_CAMS];
     int64_t cam_fstride[MCS_MAX_CAMS];
     uint8_t *out;

@@ -163,3 +163,62 @@ def calibrated_stitcher(n_cams=4, width=1920, height=1080, channels=3, super_mod
     st.calibrate_stitcher(images, save=False,
                           homographies=homography_provider(C, lambda: st.stitchers))
     return st, images, C
+
+
+def _rot(axis, a):
+    c, s = np.cos(a), np.sin(a)
+    if axis == "x":
+        return np.array([[1, 0, 0], [0, c, -s], [0, s, c]])
+    if axis == "y":
+        return np.array([[c, 0, s], [0, 1, 0], [-s, 0, c]])
+    return np.array([[c, -s, 0], [s, c, 0], [0, 0, 1]])
+
+
+def cylinder_rig(n_cams=8, width=1920, height=1080, f=1100.0, channels=3, seed=0,
+                 jitter_deg=0.0, gain=0.06):
+    """Rotation-only 360 degree rig (8 cameras at 45 degree yaw steps,
+    f = 1100 px) and its frames rendered from ONE cylindrical world texture (float bilinear,
+    numpy; per-camera gain in [1 - gain, 1 + gain] so that seams show).  Camera k looks along
+    yaw 2 pi k / n (plus pitch/roll/yaw jitter); R maps rig rays to camera rays (x right,
+    y down, z forward).  Returns (cams, frames, geometry) with cams as
+    mcs_plan_create_cylindrical takes them and geometry = dict(out_w, out_h, f_cyl, u0, v0)
+    (full circle at the cameras' focal length, panorama centre on camera 0)."""
+    rng = np.random.default_rng(seed)
+    f_cyl = float(f)
+    out_w = int(round(2 * np.pi * f_cyl))
+    out_h = int(height)
+    u0, v0 = out_w / 2.0, (out_h - 1) / 2.0
+    cams = []
+    for k in range(n_cams):
+        j = np.deg2rad(rng.uniform(-jitter_deg, jitter_deg, size=3)) if jitter_deg else (0, 0, 0)
+        yaw = 2 * np.pi * k / n_cams + j[0]
+        # camera -> rig: yaw about y, then pitch about x, then roll about z (camera frame)
+        C = _rot("y", yaw) @ _rot("x", j[1]) @ _rot("z", j[2])
+        cams.append(dict(R=np.ascontiguousarray(C.T), f=float(f), cx=(width - 1) / 2.0,
+                         cy=(height - 1) / 2.0, w=int(width), h=int(height)))
+    pad = 48
+    world = texture(out_h + 2 * pad, out_w + 2 * pad, channels, seed=seed).astype(np.float64)
+    if world.ndim == 2:
+        world = world[..., None]
+    v, u = np.mgrid[0:height, 0:width].astype(np.float64)
+    frames = []
+    for c in cams:
+        rx, ry = (u - c["cx"]) / c["f"], (v - c["cy"]) / c["f"]
+        Rt = c["R"].T   # camera -> rig
+        dx = Rt[0, 0] * rx + Rt[0, 1] * ry + Rt[0, 2]
+        dy = Rt[1, 0] * rx + Rt[1, 1] * ry + Rt[1, 2]
+        dz = Rt[2, 0] * rx + Rt[2, 1] * ry + Rt[2, 2]
+        th = np.arctan2(dx, dz)
+        hh = dy / np.hypot(dx, dz)
+        X = np.mod(th * f_cyl + u0, out_w) + pad
+        Y = np.clip(hh * f_cyl + v0 + pad, 0, world.shape[0] - 1.001)
+        xi = np.clip(np.floor(X).astype(np.int64), 0, world.shape[1] - 2)
+        yi = np.floor(Y).astype(np.int64)
+        fx = np.clip(X - xi, 0, 1)[..., None]
+        fy = np.clip(Y - yi, 0, 1)[..., None]
+        img = (world[yi, xi] * (1 - fx) * (1 - fy) + world[yi, xi + 1] * fx * (1 - fy) +
+               world[yi + 1, xi] * (1 - fx) * fy + world[yi + 1, xi + 1] * fx * fy)
+        img = img * rng.uniform(1 - gain, 1 + gain)
+        img = np.clip(np.rint(img), 1, 255).astype(np.uint8)
+        frames.append(img if channels > 1 else img[..., 0])
+    return cams, frames, dict(out_w=out_w, out_h=out_h, f_cyl=f_cyl, u0=u0, v0=v0)

@@ -78,7 +78,15 @@ int orc_invert3x3(const double *m, double *out)
 static short g_bilin[INTER_TAB_SIZE * INTER_TAB_SIZE][4];
 static int g_bilin_ready = 0;
 
+/* Built once at load (a constructor): the fix-up below reads the next, not yet written entry,
+ * so concurrent lazy builds from OpenMP threads would race on the shared scratch table. */
+static void bilinear_tab_build(void) __attribute__((constructor));
 static void bilinear_tab(void)
+{
+    if (!g_bilin_ready) bilinear_tab_build();
+}
+
+static void bilinear_tab_build(void)
 {
     if (g_bilin_ready) return;
     /* flat table like OpenCV's BilinearTab_i: entry e occupies [4e, 4e+4) */
@@ -480,4 +488,31 @@ void orc_set_num_threads(int n)
 #else
     (void)n;
 #endif
+}
+
+/* Cylinder slot map (orc_blend.c, cylindrical plans): the rig ray
+ * (sn, hv, cs) of a panorama column/row rotated into the camera by R (explicit summation order),
+ * projected x = f dx / dz + cx; rays with dz <= 0 land far outside every frame.  Same fixed-point
+ * conventions as orc__stage_xy. */
+void orc__cyl_xy(const double *R, double f, double cx, double cy, double sn, double cs, double hv,
+                 int interp, int *x32, int *y32)
+{
+    const double dx = (R[0] * sn + R[1] * hv) + R[2] * cs;
+    const double dy = (R[3] * sn + R[4] * hv) + R[5] * cs;
+    const double dz = (R[6] * sn + R[7] * hv) + R[8] * cs;
+    int X, Y;
+    if (!(dz > 0.0)) {
+        X = Y = interp == ORC_INTER_NEAREST ? -(1 << 20) : -(1 << 25);
+    } else {
+        const double k = interp == ORC_INTER_NEAREST ? 1.0 : (double)INTER_TAB_SIZE;
+        X = sat_i32_round(((f * dx) / dz + cx) * k);
+        Y = sat_i32_round(((f * dy) / dz + cy) * k);
+    }
+    if (interp == ORC_INTER_NEAREST) {
+        *x32 = sat_i16(X) * 32;
+        *y32 = sat_i16(Y) * 32;
+    } else {
+        *x32 = sat_i16(X >> INTER_BITS) * 32 + (X & (INTER_TAB_SIZE - 1));
+        *y32 = sat_i16(Y >> INTER_BITS) * 32 + (Y & (INTER_TAB_SIZE - 1));
+    }
 }

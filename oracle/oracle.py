@@ -72,6 +72,11 @@ def lib():
                                        ctypes.c_int, ctypes.c_int, P, ctypes.c_int, ctypes.c_int,
                                        P]
         L.orc_blend_stitch.restype = ctypes.c_int
+        L.orc_blend_stitch_cyl.argtypes = [ctypes.c_int, P, P, P, P, ctypes.c_double,
+                                           ctypes.c_double, ctypes.c_double, P, P, P,
+                                           ctypes.c_int, ctypes.c_int, ctypes.c_int, P,
+                                           ctypes.c_int, ctypes.c_int, P]
+        L.orc_blend_stitch_cyl.restype = ctypes.c_int
         L.orc_ransac_homography.argtypes = [P, ctypes.c_int, ctypes.c_double, ctypes.c_int,
                                             ctypes.c_uint32, P, P, P]
         L.orc_ransac_homography.restype = ctypes.c_int
@@ -228,6 +233,7 @@ def flat_stitch(flat: dict, cams, interp: int = INTER_LINEAR) -> np.ndarray:
 
 BLEND_FEATHER = 1
 BLEND_MULTIBAND = 2
+BLEND_SEAM = 3
 
 
 def blend_stitch(flat: dict, cams, mode: int, interp: int = INTER_LINEAR, want_owner=False):
@@ -251,6 +257,31 @@ def blend_stitch(flat: dict, cams, mode: int, interp: int = INTER_LINEAR, want_o
                                 _p(ch), cn, interp, mode, _p(out), ow, oh, _p(owner))
     if rc != 0:
         raise ValueError("orc_blend_stitch failed")
+    return (out, owner) if want_owner else out
+
+
+def blend_stitch_cyl(rig: list, out_w: int, out_h: int, f_cyl: float, u0: float, v0: float,
+                     cams, mode: int, interp: int = INTER_LINEAR, want_owner=False):
+    """Cylindrical panorama (orc_blend.c orc_blend_stitch_cyl): rig = [dict(R, f, cx, cy)] per
+    camera (as mcs_plan_create_cylindrical), cams = the frames; owner values = camera index."""
+    n = len(rig)
+    R = np.ascontiguousarray(np.concatenate([np.asarray(c["R"], np.float64).reshape(9)
+                                             for c in rig]))
+    f = np.array([c["f"] for c in rig], np.float64)
+    cx = np.array([c["cx"] for c in rig], np.float64)
+    cy = np.array([c["cy"] for c in rig], np.float64)
+    cams = [np.ascontiguousarray(c, dtype=np.uint8) for c in cams]
+    cn = 1 if cams[0].ndim == 2 else cams[0].shape[2]
+    out = np.zeros((out_h, out_w, cn) if cams[0].ndim == 3 else (out_h, out_w), np.uint8)
+    owner = np.zeros((out_h, out_w), np.uint8)
+    ptrs = (ctypes.c_void_p * n)(*[c.ctypes.data for c in cams])
+    cw = np.array([c.shape[1] for c in cams], np.int32)
+    ch = np.array([c.shape[0] for c in cams], np.int32)
+    rc = lib().orc_blend_stitch_cyl(n, _p(R), _p(f), _p(cx), _p(cy), float(f_cyl), float(u0),
+                                    float(v0), ptrs, _p(cw), _p(ch), cn, interp, mode, _p(out),
+                                    int(out_w), int(out_h), _p(owner))
+    if rc != 0:
+        raise ValueError("orc_blend_stitch_cyl failed")
     return (out, owner) if want_owner else out
 
 

@@ -32,6 +32,10 @@
  *   collapse R1 = B1 + up(B2), R0 = B0 + up(R1), up in double: acc += (uy * ux) * R over the
  *            taps in the order listed (rows outer), then acc / 64;
  *   out = clamp(floor(R0 + 0.5), 0, 255) where an owner exists, else 0.
+ * SEAM: out = I_owner (the seam without blending), 0 where no slot covers p.
+ * Cylindrical rigs (orc_blend_stitch_cyl, NS-6): slot s = camera s, positions from
+ *   orc__cyl_xy over the panorama's per-column (sin t, cos t) and per-row h, t = (u - u0) / fc,
+ *   h = (v - v0) / fc (libm sin/cos, once per column); the rest as above.
  *   refl = reflect-101 at each level's own size (BORDER_DEFAULT); sizes n_{l+1} = (n_l + 1) / 2.
  */
 #include <math.h>
@@ -41,10 +45,13 @@
 
 #define ORC_BLEND_FEATHER 1
 #define ORC_BLEND_MULTIBAND 2
+#define ORC_BLEND_SEAM 3
 
 void orc__stage_xy(const double *M, int bw0, int interp, int X, int Y, int *x32, int *y32);
 void orc__sample_replicate(const uint8_t *src, int sw, int sh, int cn, int x32, int y32,
                            uint8_t *d);
+void orc__cyl_xy(const double *R, double f, double cx, double cy, double sn, double cs, double hv,
+                 int interp, int *x32, int *y32);
 
 static inline int refl(int i, int n)
 {
@@ -56,20 +63,29 @@ static inline int refl(int i, int n)
     return i;
 }
 
+/* Slot geometry: the homography chain of a plan, or a cylindrical rig. */
 typedef struct {
-    int n_slots;
-    int cam[16];
-} slots_t;
+    int kind;                      /* 0: homography chain, 1: cylinder */
+    int n_stages;
+    const int *off_x, *off_y, *bw0;
+    const double *minv;
+    const double *R, *f, *cx, *cy; /* cylinder: per camera */
+    const double *tab;             /* cylinder: (sin, cos) per column, then h per row */
+    int ow;
+} geo_t;
 
-static void slot_xy(int s, int n_stages, const int *off_x, const int *off_y, const double *minv,
-                    const int *bw0, int interp, int x, int y, int *x32, int *y32)
+static void slot_xy(const geo_t *g, int s, int interp, int x, int y, int *x32, int *y32)
 {
-    if (s == 0) {
-        *x32 = (x + off_x[n_stages]) * 32;
-        *y32 = (y + off_y[n_stages]) * 32;
+    if (g->kind == 1) {
+        orc__cyl_xy(g->R + 9 * s, g->f[s], g->cx[s], g->cy[s], g->tab[2 * x], g->tab[2 * x + 1],
+                    g->tab[2 * g->ow + y], interp, x32, y32);
+    } else if (s == 0) {
+        *x32 = (x + g->off_x[g->n_stages]) * 32;
+        *y32 = (y + g->off_y[g->n_stages]) * 32;
     } else {
         int j = s - 1;
-        orc__stage_xy(minv + 9 * j, bw0[j], interp, x + off_x[j], y + off_y[j], x32, y32);
+        orc__stage_xy(g->minv + 9 * j, g->bw0[j], interp, x + g->off_x[j], y + g->off_y[j], x32,
+                      y32);
     }
 }
 
@@ -128,16 +144,10 @@ static inline double expand_d(const double *r, int gw, int gh, int cn, int y, in
     return acc / 64.0;
 }
 
-int orc_blend_stitch(int n_stages, const int *off_x, const int *off_y, const double *minv,
-                     const int *bw0, const int *stage_cam, const uint8_t *const *cams,
-                     const int *cw, const int *ch, int cn, int interp, int mode, uint8_t *out,
-                     int ow, int oh, uint8_t *owner_out)
+static int blend_core(const geo_t *geo, int S, const int *scam, const uint8_t *const *cams,
+                      const int *cw, const int *ch, int cn, int interp, int mode, uint8_t *out,
+                      int ow, int oh, uint8_t *owner_out)
 {
-    if (n_stages < 0 || n_stages > 15 || ow <= 0 || oh <= 0) return -1;
-    const int S = n_stages + 1;
-    int scam[16];
-    scam[0] = 0;
-    for (int j = 0; j < n_stages; j++) scam[j + 1] = stage_cam[j];
     const long npx = (long)ow * oh;
     uint8_t *owner = (uint8_t *)malloc((size_t)npx);
     uint8_t *g0 = (uint8_t *)malloc((size_t)npx * cn * S);
@@ -151,7 +161,7 @@ int orc_blend_stitch(int n_stages, const int *off_x, const int *off_y, const dou
         for (int s = 0; s < S; s++) {
             const int c = scam[s], w = cw[c], h = ch[c];
             int x32, y32;
-            slot_xy(s, n_stages, off_x, off_y, minv, bw0, interp, x, y, &x32, &y32);
+            slot_xy(geo, s, interp, x, y, &x32, &y32);
             orc__sample_replicate(cams[c], w, h, cn, x32, y32, g0 + ((long)s * npx + p) * cn);
             int d = -1;
             if (x32 >= 0 && y32 >= 0 && x32 <= 32 * (w - 1) && y32 <= 32 * (h - 1)) {
@@ -168,7 +178,12 @@ int orc_blend_stitch(int n_stages, const int *off_x, const int *off_y, const dou
     if (owner_out) memcpy(owner_out, owner, (size_t)npx);
 
     int rc = 0;
-    if (mode == ORC_BLEND_FEATHER) {
+    if (mode == ORC_BLEND_SEAM) {
+        for (long p = 0; p < npx; p++) {
+            if (owner[p] == 255) memset(out + p * cn, 0, (size_t)cn);
+            else memcpy(out + p * cn, g0 + ((long)owner[p] * npx + p) * cn, (size_t)cn);
+        }
+    } else if (mode == ORC_BLEND_FEATHER) {
 #pragma omp parallel for schedule(static)
         for (long p = 0; p < npx; p++) {
             uint8_t *d = out + p * cn;
@@ -263,5 +278,58 @@ int orc_blend_stitch(int n_stages, const int *off_x, const int *off_y, const dou
         rc = -1;
     }
     free(owner); free(g0); free(dist);
+    return rc;
+}
+
+int orc_blend_stitch(int n_stages, const int *off_x, const int *off_y, const double *minv,
+                     const int *bw0, const int *stage_cam, const uint8_t *const *cams,
+                     const int *cw, const int *ch, int cn, int interp, int mode, uint8_t *out,
+                     int ow, int oh, uint8_t *owner_out)
+{
+    if (n_stages < 0 || n_stages > 15 || ow <= 0 || oh <= 0) return -1;
+    int scam[16];
+    scam[0] = 0;
+    for (int j = 0; j < n_stages; j++) scam[j + 1] = stage_cam[j];
+    geo_t g;
+    memset(&g, 0, sizeof(g));
+    g.n_stages = n_stages;
+    g.off_x = off_x;
+    g.off_y = off_y;
+    g.bw0 = bw0;
+    g.minv = minv;
+    return blend_core(&g, n_stages + 1, scam, cams, cw, ch, cn, interp, mode, out, ow, oh,
+                      owner_out);
+}
+
+/* Cylindrical rig (include/mcs.h mcs_plan_create_cylindrical): slot s = camera s; panorama
+ * pixel (u, v) is the ray (sin t, h, cos t), t = (u - u0) / fc, h = (v - v0) / fc. */
+int orc_blend_stitch_cyl(int n_cams, const double *R, const double *f, const double *cx,
+                         const double *cy, double fc, double u0, double v0,
+                         const uint8_t *const *cams, const int *cw, const int *ch, int cn,
+                         int interp, int mode, uint8_t *out, int ow, int oh, uint8_t *owner_out)
+{
+    if (n_cams < 1 || n_cams > 15 || ow <= 0 || oh <= 0) return -1;
+    double *tab = (double *)malloc(sizeof(double) * (2 * (size_t)ow + (size_t)oh));
+    if (!tab) return -1;
+    for (int u = 0; u < ow; u++) {
+        const double t = ((double)u - u0) / fc;
+        tab[2 * u] = sin(t);
+        tab[2 * u + 1] = cos(t);
+    }
+    for (int v = 0; v < oh; v++) tab[2 * ow + v] = ((double)v - v0) / fc;
+    int scam[16];
+    for (int c = 0; c < n_cams; c++) scam[c] = c;
+    geo_t g;
+    memset(&g, 0, sizeof(g));
+    g.kind = 1;
+    g.R = R;
+    g.f = f;
+    g.cx = cx;
+    g.cy = cy;
+    g.tab = tab;
+    g.ow = ow;
+    const int rc = blend_core(&g, n_cams, scam, cams, cw, ch, cn, interp, mode, out, ow, oh,
+                              owner_out);
+    free(tab);
     return rc;
 }
