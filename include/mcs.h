@@ -142,6 +142,24 @@ int mcs_plan_stats(const mcs_plan *plan, int64_t *stats, int n);
  * refuse NONE. */
 int mcs_plan_set_blend(mcs_plan *plan, int mode);
 
+/* Seams.  MCS_SEAM_DISTANCE: the owner is the covering camera farthest from
+ * its image edge (the default).  MCS_SEAM_GRAPHCUT: pairwise minimum cuts through the overlaps
+ * (cost: colour difference of the two cameras, OpenCV GraphCutSeamFinder COST_COLOR style) on
+ * the 2^scale_log2-subsampled panorama of this capture (cams: host frames at calibrated sizes),
+ * then every pixel takes its grid point's camera when that camera covers it.  Once per plan
+ * (calibration time: device sampling + host max-flow); drops the prepared tables.  The exact
+ * rules: oracle/orc_seam.c.  scale_log2: 0..4. */
+enum { MCS_SEAM_DISTANCE = 0, MCS_SEAM_GRAPHCUT = 1 };
+int mcs_plan_find_seams(mcs_plan *plan, const uint8_t *const *cams, int method, int scale_log2);
+/* The current seam labels (camera per grid point, 255 = none): *w, *h = grid size (0 when the
+ * plan uses distance seams); out (w*h bytes) may be NULL to query the size. */
+int mcs_plan_seam_labels(const mcs_plan *plan, uint8_t *out, int *w, int *h);
+/* The host half of mcs_plan_find_seams on caller-supplied inputs (no device): labels (in: the
+ * distance owners' cameras, 255 = none; out: the cut), cover (bit c: camera c covers the point),
+ * samples [camera][point][channels].  grid gw x gh, up to 16 cameras. */
+int mcs_seam_graphcut_host(int n_cams, int gw, int gh, uint8_t *labels, const uint16_t *cover,
+                           const uint8_t *samples, int channels);
+
 /* Stitcher.stitch on host arrays (drop-in path, :114-136): cams[i] is the i-th camera in
  * sorted-label order, dense HxWxC u8 of the calibrated size; out is a dense out_h x out_w x C
  * buffer.  Synchronous: H2D -> kernel -> D2H on the plan's stream. */

@@ -26,6 +26,8 @@ MCS_BLEND_NONE = 0
 MCS_BLEND_FEATHER = 1
 MCS_BLEND_MULTIBAND = 2
 MCS_BLEND_SEAM = 3
+MCS_SEAM_DISTANCE = 0
+MCS_SEAM_GRAPHCUT = 1
 MCS_MAX_STAGES = 15
 MCS_MAX_CAMS = MCS_MAX_STAGES + 1
 ABI_VERSION = 1
@@ -39,7 +41,8 @@ EXPORTS = (
     "mcs_match_hamming_knn2", "mcs_match_hamming_knn2_host", "mcs_plan_set_blend",
     "mcs_ransac_homography_host", "mcs_stream_create", "mcs_stream_input", "mcs_stream_next_slot",
     "mcs_stream_submit", "mcs_stream_wait", "mcs_stream_destroy", "mcs_orb_detect_host",
-    "mcs_plan_create_cylindrical",
+    "mcs_plan_create_cylindrical", "mcs_plan_find_seams", "mcs_plan_seam_labels",
+    "mcs_seam_graphcut_host",
 )
 
 
@@ -192,6 +195,12 @@ def load() -> ctypes.CDLL:
                                                   ctypes.c_double, ctypes.c_double,
                                                   ctypes.c_double, I, I, I, ctypes.POINTER(P)]
         L.mcs_plan_create_cylindrical.restype = I
+        L.mcs_plan_find_seams.argtypes = [P, P, I, I]
+        L.mcs_plan_find_seams.restype = I
+        L.mcs_plan_seam_labels.argtypes = [P, P, ctypes.POINTER(I), ctypes.POINTER(I)]
+        L.mcs_plan_seam_labels.restype = I
+        L.mcs_seam_graphcut_host.argtypes = [I, I, I, P, P, P, I]
+        L.mcs_seam_graphcut_host.restype = I
         L.mcs_plan_set_blend.restype = I
         L.mcs_match_hamming_knn2.argtypes = [P, I, P, I, P, P, I, P]
         L.mcs_match_hamming_knn2.restype = I
@@ -343,6 +352,27 @@ class Plan:
             check(self._lib.mcs_stitch_host_sized(self._h, ptrs, ws, hs, outp))
         return out
 
+    def find_seams(self, cams=None, method: int = MCS_SEAM_GRAPHCUT, scale_log2: int = 2):
+        """mcs_plan_find_seams: graph-cut seams from one capture (host frames, calibrated
+        sizes), or back to distance seams (method=MCS_SEAM_DISTANCE)."""
+        if cams is None:
+            check(self._lib.mcs_plan_find_seams(self._h, None, int(method), int(scale_log2)))
+            return
+        cams = [np.ascontiguousarray(c, dtype=np.uint8) for c in cams]
+        ptrs = (ctypes.c_void_p * len(cams))(*[c.ctypes.data for c in cams])
+        check(self._lib.mcs_plan_find_seams(self._h, ptrs, int(method), int(scale_log2)))
+
+    def seam_labels(self):
+        """The graph-cut seam grid (camera per point, 255 = none), or None."""
+        w, h = ctypes.c_int(), ctypes.c_int()
+        check(self._lib.mcs_plan_seam_labels(self._h, None, ctypes.byref(w), ctypes.byref(h)))
+        if w.value == 0:
+            return None
+        out = np.empty((h.value, w.value), np.uint8)
+        check(self._lib.mcs_plan_seam_labels(self._h, out.ctypes.data_as(ctypes.c_void_p),
+                                             ctypes.byref(w), ctypes.byref(h)))
+        return out
+
     def stitch_device(self, cam_ptrs, cam_frame_strides, out_ptr: int, out_pitch: int,
                       out_frame_stride: int, n_frames: int, stream: int = 0):
         """Device-resident batch (raw device pointers, e.g. torch tensor data_ptr())."""
@@ -484,3 +514,19 @@ def orb_detect(image, nfeatures: int = 2000, nlevels: int = 8, scale_factor: flo
                                 desc.ctypes.data, ctypes.byref(n), device))
     k = n.value
     return dict(xy=xy[:k], response=resp[:k], angle=ang[:k], level=lvl[:k], desc=desc[:k])
+
+
+def seam_graphcut_host(labels, cover, samples):
+    """mcs_seam_graphcut_host: labels (gh, gw) u8 (distance owners' cameras), cover (gh, gw)
+    u16 camera masks, samples (n_cams, gh, gw, C) u8 -> the cut labels (new array)."""
+    L = load()
+    lab = np.ascontiguousarray(labels, np.uint8).copy()
+    cov = np.ascontiguousarray(cover, np.uint16)
+    smp = np.ascontiguousarray(samples, np.uint8)
+    n, gh, gw = smp.shape[0], lab.shape[0], lab.shape[1]
+    C = 1 if smp.ndim == 3 else smp.shape[3]
+    check(L.mcs_seam_graphcut_host(n, gw, gh, lab.ctypes.data_as(ctypes.c_void_p),
+                                   cov.ctypes.data_as(ctypes.c_void_p),
+                                   smp.ctypes.data_as(ctypes.c_void_p), C))
+    return lab
+

@@ -58,12 +58,18 @@ template <int INTERP>
 __device__ __forceinline__ int blend_owner(const KParams &P, int x, int y, uint32_t *pos_mask)
 {
     int best = kBlendNone, bestd = -1, bestcam = 0;
+    // graph-cut seams: the label's camera owns the pixel when it covers it
+    const int hcam = P.seam_hint ? (int)P.seam_hint[(int64_t)(y >> P.seam_shift) * P.seam_w +
+                                                    (x >> P.seam_shift)]
+                                 : (int)kBlendNone;
+    int hslot = -1;
     uint32_t pm = 0;
     for (int s = 0; s <= P.n_stages; s++) {
         int x32, y32, cam, w, h;
         slot_xy<INTERP>(P, s, x, y, x32, y32, cam, w, h);
         const int d = slot_dist(x32, y32, w, h);
         if (d > 0) pm |= 1u << s;
+        if (d >= 0 && cam == hcam) hslot = s;
         if (d >= 0 && (d > bestd || (d == bestd && cam < bestcam))) {
             best = s;
             bestd = d;
@@ -71,7 +77,7 @@ __device__ __forceinline__ int blend_owner(const KParams &P, int x, int y, uint3
         }
     }
     if (pos_mask) *pos_mask = pm;
-    return best;
+    return hslot >= 0 ? hslot : best;
 }
 
 // Bilinear sample at (x32, y32) with the taps clamped into the image (BORDER_REPLICATE), the
@@ -115,6 +121,39 @@ __device__ __forceinline__ int refl(int i, int n)
         if (i >= n) i = 2 * n - 2 - i;
     }
     return i;
+}
+
+// ---- seam finder inputs (mcs_plan_find_seams) ------------------------------------------------
+// One thread per point of the 2^k grid (P.seam_hint must be NULL: the distance owner).
+template <int CN, int INTERP>
+__device__ __forceinline__ void seam_sample(const KSeamArgs &a)
+{
+    const KParams &P = a.P;
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= a.gw * a.gh) return;
+    const int x = (q % a.gw) << a.k, y = (q / a.gw) << a.k;
+    const int64_t np = (int64_t)a.gw * a.gh;
+    const int o = blend_owner<INTERP>(P, x, y, nullptr);
+    uint32_t cov = 0;
+    for (int s = 0; s <= P.n_stages; s++) {
+        int x32, y32, cam, w, h;
+        slot_xy<INTERP>(P, s, x, y, x32, y32, cam, w, h);
+        if (slot_dist(x32, y32, w, h) < 0) continue;
+        cov |= 1u << cam;
+        const uint8_t *fb = P.cams[cam];
+        const uint32_t v = sample_replicate<CN>(fb, w, h, x32, y32);
+        uint8_t *d = a.samples + ((int64_t)cam * np + q) * CN;
+#pragma unroll
+        for (int k = 0; k < CN; k++) d[k] = (uint8_t)(v >> (8 * k));
+    }
+    a.cov[q] = (uint16_t)cov;
+    int ocam = kBlendNone;
+    if (o != kBlendNone) {
+        int c, w, h;
+        slot_info(P, o, c, w, h);
+        ocam = c;
+    }
+    a.label[q] = (uint8_t)ocam;
 }
 
 // ---- prepare (once per plan) -----------------------------------------------------------------

@@ -44,6 +44,10 @@ struct mcs_plan {
     bool cyl = false;
     std::vector<double> cyl_tab;
     double *d_cyl = nullptr;
+    // graph-cut seam labels (mcs_plan_find_seams): host copy and device grid
+    std::vector<uint8_t> seam_lab;
+    int seam_w = 0, seam_h = 0, seam_k = 0;
+    uint8_t *d_seam = nullptr;
 };
 
 #define MCS_VERSION_STRING "mcs 0.1.0 (gfx950 code object, HIP module launch)"
@@ -63,6 +67,7 @@ struct Kernels {
     hipFunction_t resize[5] = {};         // [channels]
     hipFunction_t blend_owner[2] = {};    // [interp]
     hipFunction_t blend_classify = nullptr;
+    hipFunction_t seam_sample[5][2] = {};  // [channels][interp]
     hipFunction_t feather[5][2] = {};     // [channels][interp]
     hipFunction_t multiband[5][2][2] = {};   // [channels][interp][<= 2 owners : <= 4]
 };
@@ -95,6 +100,8 @@ int kernels(const Api *A, int device, const Kernels **out)
                 if (rc == MCS_OK) rc = fn(name, &k.multiband[c][i][0]);
                 snprintf(name, sizeof(name), "mcs_multiband_c%d_i%d_s4", c, i);
                 if (rc == MCS_OK) rc = fn(name, &k.multiband[c][i][1]);
+                snprintf(name, sizeof(name), "mcs_seam_sample_c%d_i%d", c, i);
+                if (rc == MCS_OK) rc = fn(name, &k.seam_sample[c][i]);
                 for (int o = 0; o < 2 && rc == MCS_OK; o++) {
                     snprintf(name, sizeof(name), "mcs_direct_c%d_i%d_o%d", c, i, o ? 32 : 64);
                     rc = fn(name, &k.direct[c][i][o]);
@@ -560,6 +567,7 @@ int mcs_plan_destroy(mcs_plan *p)
             if (p->d_binfo) (void)A->hipFree(p->d_binfo);
             if (p->d_blist) (void)A->hipFree(p->d_blist);
             if (p->d_cyl) (void)A->hipFree(p->d_cyl);
+            if (p->d_seam) (void)A->hipFree(p->d_seam);
             if (p->side) (void)A->hipStreamSynchronize(p->side);
             if (p->stream) (void)A->hipStreamDestroy(p->stream);
             if (p->side) (void)A->hipStreamDestroy(p->side);
@@ -755,6 +763,112 @@ int mcs_plan_set_blend(mcs_plan *p, int mode)
     }
     p->blend = mode;
     p->kp.blend = mode;
+    return MCS_OK;
+}
+
+int mcs_plan_find_seams(mcs_plan *p, const uint8_t *const *cams, int method, int scale_log2)
+{
+    mcs::clear_error();
+    if (!p) return mcs::fail(MCS_E_INVALID, "NULL plan");
+    if (method != MCS_SEAM_DISTANCE && method != MCS_SEAM_GRAPHCUT)
+        return mcs::fail(MCS_E_INVALID, "seam method %d", method);
+    if (method == MCS_SEAM_GRAPHCUT && (!cams || scale_log2 < 0 || scale_log2 > 4))
+        return mcs::fail(MCS_E_INVALID, "graph-cut seams need cams and scale_log2 in 0..4");
+    const Api *A = mcs::rt::api();
+    if (!A) return MCS_E_HIP;
+    DeviceGuard g(A, p->device);
+    if (g.err != hipSuccess)
+        return mcs::fail(MCS_E_HIP, "hipSetDevice(%d): %s", p->device, A->hipGetErrorString(g.err));
+    release_tables(A, p);
+    if (p->d_seam) (void)A->hipFree(p->d_seam);
+    p->d_seam = nullptr;
+    p->kp.seam_hint = nullptr;
+    p->seam_lab.clear();
+    p->seam_w = p->seam_h = p->seam_k = 0;
+    if (method == MCS_SEAM_DISTANCE || p->fd.out_w <= 0 || p->fd.out_h <= 0) return MCS_OK;
+    int rc = ensure_stream(A, p);
+    if (rc == MCS_OK) rc = ensure_host_buffers(A, p);
+    if (rc == MCS_OK) rc = ensure_cyl(A, p, p->stream);
+    const Kernels *k = nullptr;
+    if (rc == MCS_OK) rc = kernels(A, p->device, &k);
+    if (rc) return rc;
+    const int C = p->fd.channels, n = p->fd.n_cams;
+    for (int i = 0; i < n; i++) {
+        if (!cams[i]) return mcs::fail(MCS_E_INVALID, "NULL cams[%d]", i);
+        HIP_TRY(A->hipMemcpyAsync(p->d_cams[i], cams[i],
+                                  (size_t)p->fd.cam_w[i] * p->fd.cam_h[i] * C,
+                                  hipMemcpyHostToDevice, p->stream));
+    }
+    const int kk = scale_log2;
+    const int gw = (p->fd.out_w + (1 << kk) - 1) >> kk, gh = (p->fd.out_h + (1 << kk) - 1) >> kk;
+    const size_t np = (size_t)gw * gh;
+    mcs::KSeamArgs a;
+    memset(&a, 0, sizeof(a));
+    a.P = p->kp;
+    for (int i = 0; i < n; i++) {
+        a.P.cams[i] = p->d_cams[i];
+        a.P.cam_fstride[i] = 0;
+    }
+    a.gw = gw;
+    a.gh = gh;
+    a.k = kk;
+    std::vector<uint8_t> lab(np), smp(np * C * n);
+    std::vector<uint16_t> cov(np);
+    hipError_t e = A->hipMalloc((void **)&a.label, np);
+    if (e == hipSuccess) e = A->hipMalloc((void **)&a.cov, np * sizeof(uint16_t));
+    if (e == hipSuccess) e = A->hipMalloc((void **)&a.samples, np * C * n);
+    if (e == hipSuccess) e = A->hipMemsetAsync(a.samples, 0, np * C * n, p->stream);
+    if (e == hipSuccess) {
+        rc = launch_args(A, k->seam_sample[C][p->fd.interp], (unsigned)((np + 255) / 256), 1,
+                         256, 1, &a, sizeof(a), p->stream);
+        if (rc) e = hipErrorLaunchFailure;
+    }
+    if (e == hipSuccess)
+        e = A->hipMemcpyAsync(lab.data(), a.label, np, hipMemcpyDeviceToHost, p->stream);
+    if (e == hipSuccess)
+        e = A->hipMemcpyAsync(cov.data(), a.cov, np * 2, hipMemcpyDeviceToHost, p->stream);
+    if (e == hipSuccess)
+        e = A->hipMemcpyAsync(smp.data(), a.samples, np * C * n, hipMemcpyDeviceToHost,
+                              p->stream);
+    if (e == hipSuccess) e = A->hipStreamSynchronize(p->stream);
+    for (void *q : {(void *)a.label, (void *)a.cov, (void *)a.samples})
+        if (q) (void)A->hipFree(q);
+    if (rc) return rc;
+    if (e != hipSuccess)
+        return mcs::fail(MCS_E_HIP, "seam sampling: %s", A->hipGetErrorString(e));
+    rc = mcs::seam_graphcut(n, gw, gh, lab.data(), cov.data(), smp.data(), C);
+    if (rc) return rc;
+    HIP_TRY(A->hipMalloc((void **)&p->d_seam, np));
+    HIP_TRY(A->hipMemcpyAsync(p->d_seam, lab.data(), np, hipMemcpyHostToDevice, p->stream));
+    HIP_TRY(A->hipStreamSynchronize(p->stream));
+    p->seam_lab.swap(lab);
+    p->seam_w = gw;
+    p->seam_h = gh;
+    p->seam_k = kk;
+    p->kp.seam_hint = p->d_seam;
+    p->kp.seam_w = gw;
+    p->kp.seam_shift = kk;
+    return MCS_OK;
+}
+
+int mcs_seam_graphcut_host(int n_cams, int gw, int gh, uint8_t *labels, const uint16_t *cover,
+                           const uint8_t *samples, int channels)
+{
+    mcs::clear_error();
+    if (!labels || !cover || !samples) return mcs::fail(MCS_E_INVALID, "NULL input");
+    if (n_cams < 1 || n_cams > 16 || gw < 1 || gh < 1 || channels < 1 || channels > 4 ||
+        (int64_t)gw * gh > (int64_t)1 << 28)
+        return mcs::fail(MCS_E_INVALID, "n_cams %d, grid %dx%d, channels %d", n_cams, gw, gh,
+                         channels);
+    return mcs::seam_graphcut(n_cams, gw, gh, labels, cover, samples, channels);
+}
+
+int mcs_plan_seam_labels(const mcs_plan *p, uint8_t *out, int *w, int *h)
+{
+    if (!p) return mcs::fail(MCS_E_INVALID, "NULL plan");
+    if (w) *w = p->seam_w;
+    if (h) *h = p->seam_h;
+    if (out && !p->seam_lab.empty()) memcpy(out, p->seam_lab.data(), p->seam_lab.size());
     return MCS_OK;
 }
 

@@ -929,6 +929,20 @@ MCS_ENTRIES(4)
     }
 MCS_BLEND_PREP_ENTRY(0)
 MCS_BLEND_PREP_ENTRY(1)
+#define MCS_SEAM_ENTRY(CN, IN)                                                                 \
+    extern "C" __global__ __launch_bounds__(256) void mcs_seam_sample_c##CN##_i##IN(           \
+        const mcs::KSeamArgs a)                                                                \
+    {                                                                                          \
+        mcs::seam_sample<CN, IN>(a);                                                           \
+    }
+MCS_SEAM_ENTRY(1, 0)
+MCS_SEAM_ENTRY(1, 1)
+MCS_SEAM_ENTRY(2, 0)
+MCS_SEAM_ENTRY(2, 1)
+MCS_SEAM_ENTRY(3, 0)
+MCS_SEAM_ENTRY(3, 1)
+MCS_SEAM_ENTRY(4, 0)
+MCS_SEAM_ENTRY(4, 1)
 extern "C" __global__ __launch_bounds__(256) void mcs_blend_classify(const mcs::KBlendPrepArgs a)
 {
     mcs::blend_classify(a.P, a.mode, a.owner, a.info, a.list, a.overflow);

@@ -34,6 +34,10 @@ struct KParams {
     // Cylinder plans: (sin theta, cos theta) per output column, then h per output row (computed
     // once on the host, so that device and oracle share every transcendental value bit for bit)
     const double *cyl_tab;
+    // Graph-cut seam labels (mcs_plan_find_seams): camera per point of the 2^seam_shift grid,
+    // 255 = none; NULL = distance seams only
+    const uint8_t *seam_hint;
+    int seam_w, seam_shift;
     const uint8_t *cams[MCS_MAX_CAMS];
     int64_t cam_fstride[MCS_MAX_CAMS];
     uint8_t *out;
@@ -156,5 +160,16 @@ constexpr int kMaxRing = 6;
 // 3 blocks per CU for 3-4 channels (52 KiB each of the CU's 160 KiB), 4 for 1-2 channels.
 constexpr int lds_stream_bytes(int cn) { return cn >= 3 ? 53248 : 40960; }
 constexpr int lds_ring_bytes(int cn) { return lds_stream_bytes(cn) - (int)sizeof(TileHdr); }
+
+
+// Seam-finder inputs (mcs_plan_find_seams): per point of the 2^k grid the distance owner's
+// camera, the covering cameras and every covering camera's sample (samples[cam][point][CN]).
+struct KSeamArgs {
+    KParams P;
+    uint8_t *label;
+    uint16_t *cov;
+    uint8_t *samples;
+    int gw, gh, k, pad_;
+};
 
 }  // namespace mcs

@@ -70,12 +70,12 @@ def lib():
         L.orc_hamming_knn2.restype = None
         L.orc_blend_stitch.argtypes = [ctypes.c_int, P, P, P, P, P, P, P, P, ctypes.c_int,
                                        ctypes.c_int, ctypes.c_int, P, ctypes.c_int, ctypes.c_int,
-                                       P]
+                                       P, ctypes.c_int, P]
         L.orc_blend_stitch.restype = ctypes.c_int
         L.orc_blend_stitch_cyl.argtypes = [ctypes.c_int, P, P, P, P, ctypes.c_double,
                                            ctypes.c_double, ctypes.c_double, P, P, P,
                                            ctypes.c_int, ctypes.c_int, ctypes.c_int, P,
-                                           ctypes.c_int, ctypes.c_int, P]
+                                           ctypes.c_int, ctypes.c_int, P, ctypes.c_int, P]
         L.orc_blend_stitch_cyl.restype = ctypes.c_int
         L.orc_ransac_homography.argtypes = [P, ctypes.c_int, ctypes.c_double, ctypes.c_int,
                                             ctypes.c_uint32, P, P, P]
@@ -83,6 +83,9 @@ def lib():
         L.orc_orb_detect.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_float, ctypes.c_int, P, P, P, P, P, P]
         L.orc_orb_detect.restype = ctypes.c_int
+        L.orc_seam_graphcut.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P,
+                                        ctypes.c_int]
+        L.orc_seam_graphcut.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -236,9 +239,18 @@ BLEND_MULTIBAND = 2
 BLEND_SEAM = 3
 
 
-def blend_stitch(flat: dict, cams, mode: int, interp: int = INTER_LINEAR, want_owner=False):
-    """Blended mosaic of the plan's geometry (orc_blend.c: FEATHER = 1, MULTIBAND = 2).
-    flat: mcs_plan_describe dict; cams: all cameras in sorted-label order, calibrated sizes."""
+def _seam_buf(ow, oh, seam_k):
+    if seam_k is None or seam_k < 0:
+        return -1, np.zeros(1, np.uint8)
+    k = int(seam_k)
+    return k, np.zeros((((oh + (1 << k) - 1) >> k), ((ow + (1 << k) - 1) >> k)), np.uint8)
+
+
+def blend_stitch(flat: dict, cams, mode: int, interp: int = INTER_LINEAR, want_owner=False,
+                 seam_k=None, want_seams=False):
+    """Blended mosaic of the plan's geometry (orc_blend.c: FEATHER = 1, MULTIBAND = 2,
+    SEAM = 3).  flat: mcs_plan_describe dict; cams: all cameras in sorted-label order,
+    calibrated sizes.  seam_k: graph-cut seams on the 2^k grid (orc_seam.c), None = distance."""
     n = int(flat["n_stages"])
     offx = np.ascontiguousarray(flat["off_x"], np.int32)
     offy = np.ascontiguousarray(flat["off_y"], np.int32)
@@ -253,15 +265,22 @@ def blend_stitch(flat: dict, cams, mode: int, interp: int = INTER_LINEAR, want_o
     ptrs = (ctypes.c_void_p * len(cams))(*[c.ctypes.data for c in cams])
     cw = np.array([c.shape[1] for c in cams], np.int32)
     ch = np.array([c.shape[0] for c in cams], np.int32)
+    k, lab = _seam_buf(ow, oh, seam_k)
     rc = lib().orc_blend_stitch(n, _p(offx), _p(offy), _p(minv), _p(bw0), _p(scam), ptrs, _p(cw),
-                                _p(ch), cn, interp, mode, _p(out), ow, oh, _p(owner))
+                                _p(ch), cn, interp, mode, _p(out), ow, oh, _p(owner), k, _p(lab))
     if rc != 0:
         raise ValueError("orc_blend_stitch failed")
-    return (out, owner) if want_owner else out
+    return _ret(out, owner, lab, want_owner, want_seams)
+
+
+def _ret(out, owner, lab, want_owner, want_seams):
+    r = (out,) + ((owner,) if want_owner else ()) + ((lab,) if want_seams else ())
+    return r if len(r) > 1 else out
 
 
 def blend_stitch_cyl(rig: list, out_w: int, out_h: int, f_cyl: float, u0: float, v0: float,
-                     cams, mode: int, interp: int = INTER_LINEAR, want_owner=False):
+                     cams, mode: int, interp: int = INTER_LINEAR, want_owner=False, seam_k=None,
+                     want_seams=False):
     """Cylindrical panorama (orc_blend.c orc_blend_stitch_cyl): rig = [dict(R, f, cx, cy)] per
     camera (as mcs_plan_create_cylindrical), cams = the frames; owner values = camera index."""
     n = len(rig)
@@ -277,12 +296,25 @@ def blend_stitch_cyl(rig: list, out_w: int, out_h: int, f_cyl: float, u0: float,
     ptrs = (ctypes.c_void_p * n)(*[c.ctypes.data for c in cams])
     cw = np.array([c.shape[1] for c in cams], np.int32)
     ch = np.array([c.shape[0] for c in cams], np.int32)
+    k, lab = _seam_buf(out_w, out_h, seam_k)
     rc = lib().orc_blend_stitch_cyl(n, _p(R), _p(f), _p(cx), _p(cy), float(f_cyl), float(u0),
                                     float(v0), ptrs, _p(cw), _p(ch), cn, interp, mode, _p(out),
-                                    int(out_w), int(out_h), _p(owner))
+                                    int(out_w), int(out_h), _p(owner), k, _p(lab))
     if rc != 0:
         raise ValueError("orc_blend_stitch_cyl failed")
-    return (out, owner) if want_owner else out
+    return _ret(out, owner, lab, want_owner, want_seams)
+
+
+def seam_graphcut(labels, cover, samples):
+    """orc_seam.c on caller inputs (see _capi.seam_graphcut_host): returns the cut labels."""
+    lab = np.ascontiguousarray(labels, np.uint8).copy()
+    cov = np.ascontiguousarray(cover, np.uint16)
+    smp = np.ascontiguousarray(samples, np.uint8)
+    n, gh, gw = smp.shape[0], lab.shape[0], lab.shape[1]
+    C = 1 if smp.ndim == 3 else smp.shape[3]
+    if lib().orc_seam_graphcut(n, gw, gh, _p(lab), _p(cov), _p(smp), C) != 0:
+        raise ValueError("orc_seam_graphcut failed")
+    return lab
 
 
 def ransac_homography(src, dst, thresh, iters=2000, seed=0):

@@ -33,6 +33,8 @@
  *            taps in the order listed (rows outer), then acc / 64;
  *   out = clamp(floor(R0 + 0.5), 0, 255) where an owner exists, else 0.
  * SEAM: out = I_owner (the seam without blending), 0 where no slot covers p.
+ * Graph-cut seams (seam_k >= 0, orc_seam.c): the owner is the seam label's camera when it
+ *   covers p (d >= 0), else the distance owner above.
  * Cylindrical rigs (orc_blend_stitch_cyl, NS-6): slot s = camera s, positions from
  *   orc__cyl_xy over the panorama's per-column (sin t, cos t) and per-row h, t = (u - u0) / fc,
  *   h = (v - v0) / fc (libm sin/cos, once per column); the rest as above.
@@ -144,11 +146,56 @@ static inline double expand_d(const double *r, int gw, int gh, int cn, int y, in
     return acc / 64.0;
 }
 
+int orc_seam_graphcut(int n_cams, int gw, int gh, uint8_t *lab, const uint16_t *cov,
+                      const uint8_t *smp, int cn);
+
+/* Graph-cut seam labels (orc_seam.c) on the 2^k seam grid: inputs from the slot geometry. */
+static int seam_labels(const geo_t *geo, int S, const int *scam, const uint8_t *const *cams,
+                       const int *cw, const int *ch, int cn, int interp, int ow, int oh, int k,
+                       uint8_t *lab)
+{
+    const int gw = (ow + (1 << k) - 1) >> k, gh = (oh + (1 << k) - 1) >> k;
+    const long np = (long)gw * gh;
+    int n_cams = 0;
+    for (int s = 0; s < S; s++)
+        if (scam[s] + 1 > n_cams) n_cams = scam[s] + 1;
+    uint16_t *cov = (uint16_t *)calloc((size_t)np, sizeof(uint16_t));
+    uint8_t *smp = (uint8_t *)calloc((size_t)np * cn * n_cams, 1);
+    if (!cov || !smp) { free(cov); free(smp); return -1; }
+#pragma omp parallel for schedule(static)
+    for (long q = 0; q < np; q++) {
+        const int x = (int)(q % gw) << k, y = (int)(q / gw) << k;
+        int best = -1, bestd = -1;
+        for (int s = 0; s < S; s++) {
+            const int c = scam[s], w = cw[c], h = ch[c];
+            int x32, y32;
+            slot_xy(geo, s, interp, x, y, &x32, &y32);
+            if (!(x32 >= 0 && y32 >= 0 && x32 <= 32 * (w - 1) && y32 <= 32 * (h - 1))) continue;
+            int d = x32;
+            if (y32 < d) d = y32;
+            if (32 * (w - 1) - x32 < d) d = 32 * (w - 1) - x32;
+            if (32 * (h - 1) - y32 < d) d = 32 * (h - 1) - y32;
+            if (d > bestd || (d == bestd && c < scam[best])) best = s, bestd = d;
+            cov[q] |= (uint16_t)(1u << c);
+            orc__sample_replicate(cams[c], w, h, cn, x32, y32, smp + ((long)c * np + q) * cn);
+        }
+        lab[q] = (uint8_t)(best < 0 ? 255 : scam[best]);
+    }
+    const int rc = orc_seam_graphcut(n_cams, gw, gh, lab, cov, smp, cn);
+    free(cov);
+    free(smp);
+    return rc;
+}
+
 static int blend_core(const geo_t *geo, int S, const int *scam, const uint8_t *const *cams,
                       const int *cw, const int *ch, int cn, int interp, int mode, uint8_t *out,
-                      int ow, int oh, uint8_t *owner_out)
+                      int ow, int oh, uint8_t *owner_out, int seam_k, uint8_t *seam_lab)
 {
     const long npx = (long)ow * oh;
+    const int gw = seam_k >= 0 ? (ow + (1 << seam_k) - 1) >> seam_k : 0;
+    if (seam_k >= 0 &&
+        seam_labels(geo, S, scam, cams, cw, ch, cn, interp, ow, oh, seam_k, seam_lab) != 0)
+        return -1;
     uint8_t *owner = (uint8_t *)malloc((size_t)npx);
     uint8_t *g0 = (uint8_t *)malloc((size_t)npx * cn * S);
     int32_t *dist = (int32_t *)malloc(sizeof(int32_t) * (size_t)npx * S);
@@ -172,6 +219,11 @@ static int blend_core(const geo_t *geo, int S, const int *scam, const uint8_t *c
                 if (d > bestd || (d == bestd && c < scam[best])) best = s, bestd = d;
             }
             dist[(long)s * npx + p] = d;
+        }
+        if (seam_k >= 0) {   /* the seam label's camera, when it covers the pixel */
+            const int hc = seam_lab[(long)(y >> seam_k) * gw + (x >> seam_k)];
+            for (int s = 0; s < S && hc != 255; s++)
+                if (scam[s] == hc && dist[(long)s * npx + p] >= 0) best = s;
         }
         owner[p] = (uint8_t)(best < 0 ? 255 : best);
     }
@@ -284,7 +336,7 @@ static int blend_core(const geo_t *geo, int S, const int *scam, const uint8_t *c
 int orc_blend_stitch(int n_stages, const int *off_x, const int *off_y, const double *minv,
                      const int *bw0, const int *stage_cam, const uint8_t *const *cams,
                      const int *cw, const int *ch, int cn, int interp, int mode, uint8_t *out,
-                     int ow, int oh, uint8_t *owner_out)
+                     int ow, int oh, uint8_t *owner_out, int seam_k, uint8_t *seam_lab)
 {
     if (n_stages < 0 || n_stages > 15 || ow <= 0 || oh <= 0) return -1;
     int scam[16];
@@ -298,7 +350,7 @@ int orc_blend_stitch(int n_stages, const int *off_x, const int *off_y, const dou
     g.bw0 = bw0;
     g.minv = minv;
     return blend_core(&g, n_stages + 1, scam, cams, cw, ch, cn, interp, mode, out, ow, oh,
-                      owner_out);
+                      owner_out, seam_k, seam_lab);
 }
 
 /* Cylindrical rig (include/mcs.h mcs_plan_create_cylindrical): slot s = camera s; panorama
@@ -306,7 +358,8 @@ int orc_blend_stitch(int n_stages, const int *off_x, const int *off_y, const dou
 int orc_blend_stitch_cyl(int n_cams, const double *R, const double *f, const double *cx,
                          const double *cy, double fc, double u0, double v0,
                          const uint8_t *const *cams, const int *cw, const int *ch, int cn,
-                         int interp, int mode, uint8_t *out, int ow, int oh, uint8_t *owner_out)
+                         int interp, int mode, uint8_t *out, int ow, int oh, uint8_t *owner_out,
+                         int seam_k, uint8_t *seam_lab)
 {
     if (n_cams < 1 || n_cams > 15 || ow <= 0 || oh <= 0) return -1;
     double *tab = (double *)malloc(sizeof(double) * (2 * (size_t)ow + (size_t)oh));
@@ -329,7 +382,7 @@ int orc_blend_stitch_cyl(int n_cams, const double *R, const double *f, const dou
     g.tab = tab;
     g.ow = ow;
     const int rc = blend_core(&g, n_cams, scam, cams, cw, ch, cn, interp, mode, out, ow, oh,
-                              owner_out);
+                              owner_out, seam_k, seam_lab);
     free(tab);
     return rc;
 }
