@@ -120,6 +120,24 @@ typedef struct mcs_cyl_camera {
 int mcs_plan_create_cylindrical(const mcs_cyl_camera *cams, int n_cams, int out_w, int out_h,
                                 double f_cyl, double u0, double v0, int channels, int interp,
                                 int device, mcs_plan **out);
+/* cv2.warpPerspective(src, M, (dst_w, dst_h)) as a plan (flags INTER_LINEAR / INTER_NEAREST,
+ * BORDER_CONSTANT 0): the extrinsic bird's-eye view of the reference's display path
+ * (MediaPlayer/view.py:387-388, PostScripts/Calibration_Utils/Extrinsic.py:99).  One camera of
+ * src_w x src_h; stitch calls take one camera pointer.  Blend mode NONE only. */
+int mcs_plan_create_warp(const double *M, int src_w, int src_h, int dst_w, int dst_h,
+                         int channels, int interp, int device, mcs_plan **out);
+/* cv2.undistort(src, K, dist) as a plan (OpenCV 3.4 stripes + initUndistortRectifyMap + remap
+ * INTER_LINEAR, BORDER_CONSTANT): the per-frame undistortion before stitching
+ * (video_mapping_node.py:157-158, MediaPlayer/view.py:380-381, Intrinsic.py:234-235).  K: 3x3
+ * row-major; dist: 0, 4, 5, 8, 12 or 14 coefficients (tilt tau_x = tau_y = 0).  The map is
+ * computed once on the host; per frame it is the plan's remap.  Blend mode NONE only. */
+int mcs_plan_create_undistort(const double *K, const double *dist, int n_dist, int w, int h,
+                              int channels, int device, mcs_plan **out);
+/* The undistortion map of mcs_plan_create_undistort on the host (no device): map[2 p], map[2 p+1]
+ * = cv::initUndistortRectifyMap's CV_16SC2 + CV_16UC1 pair of output pixel p as one fixed-point
+ * value per axis, (short)(i >> 5) * 32 + (i & 31) with i = cvRound(32 u). */
+int mcs_undistort_map_host(const double *K, const double *dist, int n_dist, int w, int h,
+                           int32_t *map);
 int mcs_plan_destroy(mcs_plan *plan);
 int mcs_plan_out_shape(const mcs_plan *plan, int *w, int *h, int *channels);
 int mcs_plan_describe(const mcs_plan *plan, mcs_flat_desc *out);

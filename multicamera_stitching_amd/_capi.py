@@ -42,7 +42,8 @@ EXPORTS = (
     "mcs_ransac_homography_host", "mcs_stream_create", "mcs_stream_input", "mcs_stream_next_slot",
     "mcs_stream_submit", "mcs_stream_wait", "mcs_stream_destroy", "mcs_orb_detect_host",
     "mcs_plan_create_cylindrical", "mcs_plan_find_seams", "mcs_plan_seam_labels",
-    "mcs_seam_graphcut_host",
+    "mcs_seam_graphcut_host", "mcs_plan_create_warp", "mcs_plan_create_undistort",
+    "mcs_undistort_map_host",
 )
 
 
@@ -201,6 +202,12 @@ def load() -> ctypes.CDLL:
         L.mcs_plan_seam_labels.restype = I
         L.mcs_seam_graphcut_host.argtypes = [I, I, I, P, P, P, I]
         L.mcs_seam_graphcut_host.restype = I
+        L.mcs_plan_create_warp.argtypes = [P, I, I, I, I, I, I, I, ctypes.POINTER(P)]
+        L.mcs_plan_create_warp.restype = I
+        L.mcs_plan_create_undistort.argtypes = [P, P, I, I, I, I, I, ctypes.POINTER(P)]
+        L.mcs_plan_create_undistort.restype = I
+        L.mcs_undistort_map_host.argtypes = [P, P, I, I, I, P]
+        L.mcs_undistort_map_host.restype = I
         L.mcs_plan_set_blend.restype = I
         L.mcs_match_hamming_knn2.argtypes = [P, I, P, I, P, P, I, P]
         L.mcs_match_hamming_knn2.restype = I
@@ -298,6 +305,32 @@ class Plan:
                                             ctypes.c_double(v0), int(channels), int(interp),
                                             int(device), ctypes.byref(h)))
         return cls(None, 0, 0, channels, interp, device, _handle=h)
+
+    @classmethod
+    def warp(cls, M, src_w: int, src_h: int, dst_w: int, dst_h: int, channels: int,
+             interp: int = MCS_INTER_LINEAR, device: int = 0):
+        """mcs_plan_create_warp: cv2.warpPerspective(src, M, (dst_w, dst_h)) as a plan."""
+        L = load()
+        m = np.ascontiguousarray(np.asarray(M, np.float64).reshape(9))
+        h = ctypes.c_void_p()
+        check(L.mcs_plan_create_warp(m.ctypes.data_as(ctypes.c_void_p), int(src_w), int(src_h),
+                                     int(dst_w), int(dst_h), int(channels), int(interp),
+                                     int(device), ctypes.byref(h)))
+        return cls(None, 0, 0, channels, interp, device, _handle=h)
+
+    @classmethod
+    def undistort(cls, K, dist, w: int, h: int, channels: int, device: int = 0):
+        """mcs_plan_create_undistort: cv2.undistort(src, K, dist) as a plan."""
+        L = load()
+        k = np.ascontiguousarray(np.asarray(K, np.float64).reshape(9))
+        d = np.ascontiguousarray(np.asarray(dist if dist is not None else [], np.float64)
+                                 .reshape(-1))
+        hd = ctypes.c_void_p()
+        check(L.mcs_plan_create_undistort(k.ctypes.data_as(ctypes.c_void_p),
+                                          d.ctypes.data_as(ctypes.c_void_p) if d.size else None,
+                                          int(d.size), int(w), int(h), int(channels),
+                                          int(device), ctypes.byref(hd)))
+        return cls(None, 0, 0, channels, MCS_INTER_LINEAR, device, _handle=hd)
 
     @property
     def handle(self):
@@ -529,4 +562,17 @@ def seam_graphcut_host(labels, cover, samples):
                                    cov.ctypes.data_as(ctypes.c_void_p),
                                    smp.ctypes.data_as(ctypes.c_void_p), C))
     return lab
+
+
+def undistort_map_host(K, dist, w: int, h: int) -> np.ndarray:
+    """mcs_undistort_map_host: (h, w, 2) int32 fixed-point map (x, y in 1/32 px)."""
+    L = load()
+    k = np.ascontiguousarray(np.asarray(K, np.float64).reshape(9))
+    d = np.ascontiguousarray(np.asarray(dist if dist is not None else [], np.float64).reshape(-1))
+    out = np.empty((h, w, 2), np.int32)
+    check(L.mcs_undistort_map_host(k.ctypes.data_as(ctypes.c_void_p),
+                                   d.ctypes.data_as(ctypes.c_void_p) if d.size else None,
+                                   int(d.size), int(w), int(h),
+                                   out.ctypes.data_as(ctypes.c_void_p)))
+    return out
 

@@ -48,6 +48,10 @@ struct mcs_plan {
     std::vector<uint8_t> seam_lab;
     int seam_w = 0, seam_h = 0, seam_k = 0;
     uint8_t *d_seam = nullptr;
+    // single-camera remap plans (warp / undistort): blend modes refused; table plans' map
+    bool single = false;
+    std::vector<int32_t> map_tab;
+    int32_t *d_map = nullptr;
 };
 
 #define MCS_VERSION_STRING "mcs 0.1.0 (gfx950 code object, HIP module launch)"
@@ -236,6 +240,13 @@ void release_tables(const Api *A, mcs_plan *p)
 // Cylindrical plans: the per-column / per-row table on the plan's device (once).
 int ensure_cyl(const Api *A, mcs_plan *p, hipStream_t s)
 {
+    if (!p->map_tab.empty() && !p->d_map) {
+        const size_t bytes = p->map_tab.size() * sizeof(int32_t);
+        HIP_TRY(A->hipMalloc((void **)&p->d_map, bytes));
+        HIP_TRY(A->hipMemcpyAsync(p->d_map, p->map_tab.data(), bytes, hipMemcpyHostToDevice, s));
+        HIP_TRY(A->hipStreamSynchronize(s));
+        p->kp.map_tab = p->d_map;
+    }
     if (!p->cyl || p->d_cyl) return MCS_OK;
     const size_t bytes = p->cyl_tab.size() * sizeof(double);
     HIP_TRY(A->hipMalloc((void **)&p->d_cyl, bytes));
@@ -415,6 +426,7 @@ int launch_stitch(const Api *A, mcs_plan *p, const mcs::KParams &kp, int n_frame
         uniform = uniform && kp.cam_fstride[p->fd.st[j].cam] == kp.cam_fstride[0];
     mcs::KParams P = kp;
     P.cyl_tab = p->kp.cyl_tab;   // set by prepare on a cylindrical plan's first use
+    P.map_tab = p->kp.map_tab;   // (table plans)
     if (uniform) return launch_pair(A, p, k, P, n_frames, s);
     for (int f = 0; f < n_frames; f++) {
         for (int i = 0; i < p->fd.n_cams; i++)
@@ -545,6 +557,102 @@ int mcs_plan_create_cylindrical(const mcs_cyl_camera *cams, int n_cams, int out_
     return MCS_OK;
 }
 
+namespace {
+
+// Single-camera plan: stage 0 samples camera 0 everywhere (empty paste rect, paste rule).
+mcs_plan *single_plan(int src_w, int src_h, int dst_w, int dst_h, int channels, int interp,
+                      int device, const double *minv, int kind)
+{
+    mcs_plan *p = new (std::nothrow) mcs_plan();
+    if (!p) return nullptr;
+    mcs_flat_desc &fd = p->fd;
+    memset(&fd, 0, sizeof(fd));
+    fd.n_stages = 1;
+    fd.out_w = dst_w;
+    fd.out_h = dst_h;
+    fd.channels = channels;
+    fd.interp = interp;
+    fd.n_cams = 1;
+    fd.cam_w[0] = src_w;
+    fd.cam_h[0] = src_h;
+    if (minv) memcpy(fd.st[0].minv, minv, sizeof(fd.st[0].minv));
+    fd.st[0].bw0 = mcs::block_width(dst_w, dst_h);
+    fd.st[0].cam = 0;
+    mcs::fill_kparams(fd, &p->kp);
+    p->kp.cam0_w = p->kp.cam0_h = 0;
+    p->kp.st[0].kind = kind;
+    p->single = true;
+    p->device = device;
+    return p;
+}
+
+int check_single_args(int src_w, int src_h, int dst_w, int dst_h, int channels, int device)
+{
+    if (device < 0 || device >= kMaxDevices) return mcs::fail(MCS_E_INVALID, "device=%d", device);
+    if (channels < 1 || channels > 4) return mcs::fail(MCS_E_INVALID, "channels %d", channels);
+    if (src_w < 1 || src_h < 1 || src_w > 32767 || src_h > 32767)
+        return mcs::fail(MCS_E_SHAPE, "source %dx%d", src_w, src_h);
+    if (dst_w < 1 || dst_h < 1 || (int64_t)dst_w * dst_h * channels > ((int64_t)1 << 31))
+        return mcs::fail(MCS_E_SHAPE, "destination %dx%d", dst_w, dst_h);
+    return MCS_OK;
+}
+
+}  // namespace
+
+int mcs_plan_create_warp(const double *M, int src_w, int src_h, int dst_w, int dst_h,
+                         int channels, int interp, int device, mcs_plan **out)
+{
+    mcs::clear_error();
+    if (!M || !out) return mcs::fail(MCS_E_INVALID, "NULL M/out");
+    *out = nullptr;
+    int rc = check_single_args(src_w, src_h, dst_w, dst_h, channels, device);
+    if (rc) return rc;
+    if (interp != MCS_INTER_NEAREST && interp != MCS_INTER_LINEAR)
+        return mcs::fail(MCS_E_INVALID, "interp %d", interp);
+    for (int i = 0; i < 9; i++)
+        if (!std::isfinite(M[i])) return mcs::fail(MCS_E_INVALID, "M[%d] not finite", i);
+    double minv[9];
+    mcs::invert3x3_cv(M, minv);   // warpPerspective inverts M (no WARP_INVERSE_MAP)
+    mcs_plan *p = single_plan(src_w, src_h, dst_w, dst_h, channels, interp, device, minv,
+                              mcs::kStageHomography);
+    if (!p) return mcs::fail(MCS_E_NOMEM, "plan allocation");
+    *out = p;
+    return MCS_OK;
+}
+
+int mcs_plan_create_undistort(const double *K, const double *dist, int n_dist, int w, int h,
+                              int channels, int device, mcs_plan **out)
+{
+    mcs::clear_error();
+    if (!K || !out || (n_dist > 0 && !dist)) return mcs::fail(MCS_E_INVALID, "NULL K/dist/out");
+    *out = nullptr;
+    int rc = check_single_args(w, h, w, h, channels, device);
+    if (rc) return rc;
+    for (int i = 0; i < 9; i++)
+        if (!std::isfinite(K[i])) return mcs::fail(MCS_E_INVALID, "K[%d] not finite", i);
+    std::vector<int32_t> tab(2 * (size_t)w * h);
+    if (!mcs::undistort_map(K, dist, n_dist, w, h, tab.data()))
+        return mcs::fail(MCS_E_UNSUPPORTED, "distortion vector of %d coefficients (0, 4, 5, 8, "
+                         "12 or 14 with tau = 0)", n_dist);
+    mcs_plan *p = single_plan(w, h, w, h, channels, MCS_INTER_LINEAR, device, nullptr,
+                              mcs::kStageTable);
+    if (!p) return mcs::fail(MCS_E_NOMEM, "plan allocation");
+    p->map_tab.swap(tab);
+    *out = p;
+    return MCS_OK;
+}
+
+int mcs_undistort_map_host(const double *K, const double *dist, int n_dist, int w, int h,
+                           int32_t *map)
+{
+    mcs::clear_error();
+    if (!K || !map || (n_dist > 0 && !dist)) return mcs::fail(MCS_E_INVALID, "NULL K/dist/map");
+    if (w < 1 || h < 1 || w > 32767 || h > 32767) return mcs::fail(MCS_E_SHAPE, "%dx%d", w, h);
+    if (!mcs::undistort_map(K, dist, n_dist, w, h, map))
+        return mcs::fail(MCS_E_UNSUPPORTED, "distortion vector of %d coefficients", n_dist);
+    return MCS_OK;
+}
+
 int mcs_plan_destroy(mcs_plan *p)
 {
     if (!p) return MCS_OK;
@@ -568,6 +676,7 @@ int mcs_plan_destroy(mcs_plan *p)
             if (p->d_blist) (void)A->hipFree(p->d_blist);
             if (p->d_cyl) (void)A->hipFree(p->d_cyl);
             if (p->d_seam) (void)A->hipFree(p->d_seam);
+            if (p->d_map) (void)A->hipFree(p->d_map);
             if (p->side) (void)A->hipStreamSynchronize(p->side);
             if (p->stream) (void)A->hipStreamDestroy(p->stream);
             if (p->side) (void)A->hipStreamDestroy(p->side);
@@ -751,6 +860,9 @@ int mcs_plan_set_blend(mcs_plan *p, int mode)
     if (mode != MCS_BLEND_NONE && mode != MCS_BLEND_FEATHER && mode != MCS_BLEND_MULTIBAND &&
         mode != MCS_BLEND_SEAM)
         return mcs::fail(MCS_E_INVALID, "blend mode %d", mode);
+    if (p->single && mode != MCS_BLEND_NONE)
+        return mcs::fail(MCS_E_INVALID, "a single-camera remap plan (warp / undistort) has "
+                         "nothing to blend: blend mode NONE only");
     if (p->cyl && mode == MCS_BLEND_NONE)
         return mcs::fail(MCS_E_INVALID, "a cylindrical plan has no paste order: blend mode "
                          "NONE is not defined for it (use SEAM, FEATHER or MULTIBAND)");

@@ -26,6 +26,8 @@ void invert3x3_cv(const double *m, double *out);
 int build_flat(const mcs_stage_desc *stages, int n_stages, int cam0_w, int cam0_h, int channels,
                int interp, mcs_flat_desc *fd);
 void fill_kparams(const mcs_flat_desc &fd, KParams *kp);
+int block_width(int W, int H);
+bool undistort_map(const double *K, const double *dist, int n_dist, int w, int h, int32_t *tab);
 // Pairwise graph-cut seam labels over the seam grid (mcs_seam.cpp; spec: oracle/orc_seam.c).
 int seam_graphcut(int n_cams, int gw, int gh, uint8_t *lab, const uint16_t *cov,
                   const uint8_t *smp, int cn);

@@ -63,6 +63,12 @@ __device__ __forceinline__ void stage_map(const KParams &P, const KStage &S, int
         map_exact<INTERP>(S, x + S.offx, y + S.offy, xo, yo);
         return;
     }
+    if (S.kind == kStageTable) {
+        const int64_t p = 2 * ((int64_t)y * P.out_w + x);
+        xo = P.map_tab[p];
+        yo = P.map_tab[p + 1];
+        return;
+    }
     const double sn = P.cyl_tab[2 * x], cs = P.cyl_tab[2 * x + 1];
     const double hv = P.cyl_tab[2 * P.out_w + y];
     const double dx = (S.m[0] * sn + S.m[1] * hv) + S.m[2] * cs;

@@ -18,12 +18,14 @@ struct KStage {
     int bw_shift;             // log2(bw0) when bw0 is a power of two, else -1
     int cam;                  // camera sampled by this stage
     int src_w, src_h;         // its size
-    int kind;                 // kStageHomography (m = inverted H) or kStageCylinder (m = R)
+    int kind;                 // kStageHomography (m = inverted H), kStageCylinder (m = R),
+                              // kStageTable (map_tab)
     double f, cx, cy;         // kStageCylinder: pinhole intrinsics of the camera
 };
 
 constexpr int kStageHomography = 0;
 constexpr int kStageCylinder = 1;
+constexpr int kStageTable = 2;    // per-output-pixel map (KParams.map_tab), e.g. undistortion
 
 struct KParams {
     int n_stages;
@@ -38,6 +40,8 @@ struct KParams {
     // 255 = none; NULL = distance seams only
     const uint8_t *seam_hint;
     int seam_w, seam_shift;
+    // kStageTable plans: map value (bilinear fixed point) of every output pixel, x then y
+    const int32_t *map_tab;
     const uint8_t *cams[MCS_MAX_CAMS];
     int64_t cam_fstride[MCS_MAX_CAMS];
     uint8_t *out;

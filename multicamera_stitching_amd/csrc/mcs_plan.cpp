@@ -15,6 +15,8 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <algorithm>
+#include <cmath>
 #include <cstring>
 
 namespace mcs {
@@ -73,7 +75,7 @@ static void py_slice(long start, long stop, long n, long *s0, long *s1)
 }
 
 // WarpPerspectiveInvoker block geometry (BLOCK_SZ = 32): bh0 = min(16, H); bw0 = min(1024/bh0, W).
-static int block_width(int W, int H)
+int block_width(int W, int H)
 {
     int bh0 = H < 16 ? H : 16;
     if (bh0 < 1) bh0 = 1;
@@ -213,4 +215,55 @@ void fill_kparams(const mcs_flat_desc &fd, KParams *kp)
     }
 }
 
+// cv::undistort(src, K, dist) coordinate map (OpenCV 3.4 imgproc/src/undistort.cpp): stripes of
+// min(max(1, 4096 / w), h) rows, each with the new camera matrix's cy shifted by the stripe's
+// first row, initUndistortRectifyMap's scalar loop (iR = inv(A_r) by cv::invert DECOMP_LU; x, y,
+// w accumulated along the row by repeated addition; the rational + tangential + thin-prism model,
+// tilt identity) and its CV_16SC2 + CV_16UC1 packing.  tab[2 p] / tab[2 p + 1]: the map value of
+// output pixel p as (short)(iu >> 5) * 32 + (iu & 31), i.e. the bilinear fixed point the stitch
+// kernels sample with.  Returns false for distortion vectors the map does not cover.
+bool undistort_map(const double *K, const double *dist, int n_dist, int w, int h, int32_t *tab)
+{
+    double k[14] = {0};
+    if (!(n_dist == 0 || n_dist == 4 || n_dist == 5 || n_dist == 8 || n_dist == 12 ||
+          n_dist == 14))
+        return false;
+    for (int i = 0; i < n_dist; i++) k[i] = dist[i];
+    if (k[12] != 0.0 || k[13] != 0.0) return false;   // sensor tilt: not supported
+    const double k1 = k[0], k2 = k[1], p1 = k[2], p2 = k[3], k3 = k[4], k4 = k[5], k5 = k[6],
+                 k6 = k[7], s1 = k[8], s2 = k[9], s3 = k[10], s4 = k[11];
+    const double u0 = K[2], v0 = K[5], fx = K[0], fy = K[4];
+    const int stripe0 = std::min(std::max(1, (1 << 12) / std::max(w, 1)), h);
+    for (int y0 = 0; y0 < h; y0 += stripe0) {
+        const int rows = std::min(stripe0, h - y0);
+        double Ar[9];
+        memcpy(Ar, K, sizeof(Ar));
+        Ar[5] = v0 - y0;
+        double ir[9];
+        invert3x3_cv(Ar, ir);
+        for (int i = 0; i < rows; i++) {
+            int32_t *row = tab + 2 * (int64_t)(y0 + i) * w;
+            double _x = i * ir[1] + ir[2], _y = i * ir[4] + ir[5], _w = i * ir[7] + ir[8];
+            for (int j = 0; j < w; j++, _x += ir[0], _y += ir[3], _w += ir[6]) {
+                const double ww = 1. / _w, x = _x * ww, y = _y * ww;
+                const double x2 = x * x, y2 = y * y;
+                const double r2 = x2 + y2, _2xy = 2 * x * y;
+                const double kr = (1 + ((k3 * r2 + k2) * r2 + k1) * r2) /
+                                  (1 + ((k6 * r2 + k5) * r2 + k4) * r2);
+                const double xd = x * kr + p1 * _2xy + p2 * (r2 + 2 * x2) + s1 * r2 + s2 * r2 * r2;
+                const double yd = y * kr + p1 * (r2 + 2 * y2) + p2 * _2xy + s3 * r2 + s4 * r2 * r2;
+                // tilt = identity: vecTilt = (1 xd + 0 yd + 0, 0 xd + 1 yd + 0, 1), invProj = 1
+                const double tx = 1.0 * xd + 0.0 * yd + 0.0 * 1.0;
+                const double ty = 0.0 * xd + 1.0 * yd + 0.0 * 1.0;
+                const double u = fx * 1.0 * tx + u0, v = fy * 1.0 * ty + v0;
+                const int iu = (int)lrint(u * 32), iv = (int)lrint(v * 32);
+                row[2 * j] = (int32_t)(int16_t)(iu >> 5) * 32 + (iu & 31);
+                row[2 * j + 1] = (int32_t)(int16_t)(iv >> 5) * 32 + (iv & 31);
+            }
+        }
+    }
+    return true;
+}
+
 }  // namespace mcs
+

@@ -212,6 +212,14 @@ static inline void sample_px(const uint8_t *src, int sw, int sh, long sstep, int
     }
 }
 
+/* remapBilinear of one pixel from a CV_16SC2 (sx, sy) + CV_16UC1 (alpha) map entry. */
+void orc__remap_bilinear_px(const uint8_t *src, int sw, int sh, long sstep, int cn, int sx, int sy,
+                            int alpha, uint8_t *d)
+{
+    bilinear_tab();
+    sample_px(src, sw, sh, sstep, cn, ORC_INTER_LINEAR, sx, sy, alpha, d);
+}
+
 /* Block geometry of WarpPerspectiveInvoker (BLOCK_SZ = 32). */
 static void block_geom(int dw, int dh, int *bw0_out)
 {

@@ -86,6 +86,9 @@ def lib():
         L.orc_seam_graphcut.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P,
                                         ctypes.c_int]
         L.orc_seam_graphcut.restype = ctypes.c_int
+        L.orc_undistort.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P,
+                                    ctypes.c_int, P]
+        L.orc_undistort.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -134,6 +137,21 @@ def warp_perspective(src: np.ndarray, M, dsize, interp: int = INTER_LINEAR,
     m = np.ascontiguousarray(np.asarray(M, dtype=np.float64).reshape(9))
     lib().orc_warp_perspective(_p(src), sw, sh, sw * cn, cn, _p(dst), W, H, W * cn, _p(m),
                                interp, 1 if inverse_map else 0)
+    return dst
+
+
+def undistort(src: np.ndarray, K, dist=None) -> np.ndarray:
+    """cv2.undistort(src, K, dist) (orc_undistort.c, OpenCV 3.4 semantics)."""
+    src = np.ascontiguousarray(src, dtype=np.uint8)
+    cn = 1 if src.ndim == 2 else src.shape[2]
+    h, w = src.shape[:2]
+    A = np.ascontiguousarray(np.asarray(K, np.float64).reshape(9))
+    d = np.ascontiguousarray(np.zeros(0) if dist is None else
+                             np.asarray(dist, np.float64).reshape(-1))
+    dst = np.zeros_like(src)
+    if lib().orc_undistort(_p(src), w, h, cn, _p(A), _p(d) if d.size else None, int(d.size),
+                           _p(dst)) != 0:
+        raise ValueError("orc_undistort: unsupported distortion vector")
     return dst
 
 
