@@ -256,6 +256,19 @@ int mcs_orb_detect_host(const uint8_t *image, int w, int h, int channels, int nf
                         float *kp_response, float *kp_angle, int *kp_level, uint8_t *desc,
                         int *n_out, int device);
 
+/* BFMatcher(NORM_L2) ("BruteForce").knnMatch(query, train, k=2) for float descriptors (the
+ * reference's SIFT matcher, StitcherClass.py:423-424) on MFMA.  Descriptors that
+ * are all integers in [0, 255] (OpenCV SIFT's) are matched exactly (int8 MFMA, integer squared
+ * distances, float(sqrt) -- OpenCV's own float result for such data, ordered by (distance,
+ * index) as its batchDistance); other data on f32 MFMA (|a|^2 + |b|^2 - 2 a.b in float).
+ * *exact (optional) reports which.  idx2 / dist2: n_query x 2, -1 / -1.0f where fewer than two
+ * train descriptors exist.  dim 1..256.  Allocates scratch and synchronises (calibration-time). */
+int mcs_match_l2_knn2(const float *d_query, int n_query, const float *d_train, int n_train,
+                      int dim, int32_t *d_idx2, float *d_dist2, int *exact, int device,
+                      void *stream);
+int mcs_match_l2_knn2_host(const float *query, int n_query, const float *train, int n_train,
+                           int dim, int32_t *idx2, float *dist2, int *exact, int device);
+
 /* ---- Homography estimation ----------------------------------------------
  * RANSAC homography of n correspondences src_xy[i] -> dst_xy[i] (float x, y pairs), the role of
  * cv2.findHomography(ptsA, ptsB, cv2.RANSAC, reprojThresh) at StitcherClass.py:440-441.  `iters`

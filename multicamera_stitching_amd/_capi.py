@@ -43,7 +43,7 @@ EXPORTS = (
     "mcs_stream_submit", "mcs_stream_wait", "mcs_stream_destroy", "mcs_orb_detect_host",
     "mcs_plan_create_cylindrical", "mcs_plan_find_seams", "mcs_plan_seam_labels",
     "mcs_seam_graphcut_host", "mcs_plan_create_warp", "mcs_plan_create_undistort",
-    "mcs_undistort_map_host",
+    "mcs_undistort_map_host", "mcs_match_l2_knn2", "mcs_match_l2_knn2_host",
 )
 
 
@@ -208,6 +208,10 @@ def load() -> ctypes.CDLL:
         L.mcs_plan_create_undistort.restype = I
         L.mcs_undistort_map_host.argtypes = [P, P, I, I, I, P]
         L.mcs_undistort_map_host.restype = I
+        L.mcs_match_l2_knn2.argtypes = [P, I, P, I, I, P, P, P, I, P]
+        L.mcs_match_l2_knn2.restype = I
+        L.mcs_match_l2_knn2_host.argtypes = [P, I, P, I, I, P, P, P, I]
+        L.mcs_match_l2_knn2_host.restype = I
         L.mcs_plan_set_blend.restype = I
         L.mcs_match_hamming_knn2.argtypes = [P, I, P, I, P, P, I, P]
         L.mcs_match_hamming_knn2.restype = I
@@ -575,4 +579,24 @@ def undistort_map_host(K, dist, w: int, h: int) -> np.ndarray:
                                    int(d.size), int(w), int(h),
                                    out.ctypes.data_as(ctypes.c_void_p)))
     return out
+
+
+def match_l2_knn2(query, train, device: int = 0):
+    """mcs_match_l2_knn2_host: BFMatcher(NORM_L2).knnMatch(k=2) of float descriptors ->
+    (idx (nq, 2) int32, dist (nq, 2) float32, exact: bool)."""
+    L = load()
+    q = np.ascontiguousarray(query, np.float32)
+    t = np.ascontiguousarray(train, np.float32)
+    nq = q.shape[0]
+    nt = t.shape[0] if t.size else 0
+    dim = q.shape[1] if q.ndim == 2 else (t.shape[1] if t.ndim == 2 else 1)
+    idx = np.empty((nq, 2), np.int32)
+    dist = np.empty((nq, 2), np.float32)
+    ex = ctypes.c_int(0)
+    check(L.mcs_match_l2_knn2_host(q.ctypes.data_as(ctypes.c_void_p), nq,
+                                   t.ctypes.data_as(ctypes.c_void_p) if nt else None, nt, dim,
+                                   idx.ctypes.data_as(ctypes.c_void_p),
+                                   dist.ctypes.data_as(ctypes.c_void_p), ctypes.byref(ex),
+                                   int(device)))
+    return idx, dist, bool(ex.value)
 

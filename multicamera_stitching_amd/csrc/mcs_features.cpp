@@ -23,6 +23,7 @@ struct FeatureKernels {
     hipFunction_t ransac_score = nullptr, ransac_mask = nullptr;
     hipFunction_t orb_gray = nullptr, orb_blur_h = nullptr, orb_blur_v = nullptr;
     hipFunction_t orb_fast = nullptr, orb_nms = nullptr, orb_describe = nullptr;
+    hipFunction_t l2_prep = nullptr, l2_i8 = nullptr, l2_f32 = nullptr, l2_finalize = nullptr;
 };
 FeatureKernels g_fk[mcs::kMaxDevices];
 std::mutex g_fk_mu;
@@ -49,7 +50,9 @@ int feature_kernels(const Api *A, int device, const FeatureKernels **out)
             hipFunction_t *f;
         } orb[] = {{"mcs_orb_gray", &k.orb_gray},     {"mcs_orb_blur_h", &k.orb_blur_h},
                    {"mcs_orb_blur_v", &k.orb_blur_v}, {"mcs_orb_fast", &k.orb_fast},
-                   {"mcs_orb_nms", &k.orb_nms},       {"mcs_orb_describe", &k.orb_describe}};
+                   {"mcs_orb_nms", &k.orb_nms},       {"mcs_orb_describe", &k.orb_describe},
+                   {"mcs_l2_prep", &k.l2_prep},       {"mcs_l2_knn2_i8", &k.l2_i8},
+                   {"mcs_l2_knn2_f32", &k.l2_f32},    {"mcs_l2_knn2_finalize", &k.l2_finalize}};
         for (const auto &o : orb)
             if (rc == MCS_OK) rc = mcs::module_function(A, device, mcs::kModFeatures, o.name, o.f);
         if (rc) return rc;
@@ -92,6 +95,83 @@ int knn2(const Api *A, const FeatureKernels *k, const uint8_t *q, int nq, const 
     if (rc == MCS_OK)
         rc = launch(A, k->knn2_finalize, (2 * nq + 255) / 256, 1, 256, &a, sizeof(a), s);
     return rc;
+}
+
+// L2 kNN-2 on device buffers (float descriptors); scratch allocated here; synchronises.
+int l2_knn2(const Api *A, const FeatureKernels *k, const float *dq, int nq, const float *dt, int nt,
+            int dim, int32_t *idx2, float *dist2, int *exact, hipStream_t s)
+{
+    const int dimp = (dim + 63) / 64 * 64;
+    const size_t n = (size_t)nq + nt;
+    const size_t b8 = n * dimp, bi = n * 4, bk = (size_t)nq * 2 * 8;
+    uint8_t *buf = nullptr;
+    HIP_TRY(A->hipMalloc((void **)&buf, b8 + 5 * bi + bk + 256));
+    int8_t *d8 = reinterpret_cast<int8_t *>(buf);
+    uint8_t *p = buf + ((b8 + 15) & ~(size_t)15);
+    int32_t *norm_i = reinterpret_cast<int32_t *>(p);
+    int32_t *sum_i = norm_i + n;
+    float *norm_f = reinterpret_cast<float *>(sum_i + n);
+    uint32_t *flag = reinterpret_cast<uint32_t *>(norm_f + n);
+    unsigned long long *keys =
+        reinterpret_cast<unsigned long long *>(((uintptr_t)(flag + 4) + 15) & ~(uintptr_t)15);
+    int rc = MCS_OK;
+    hipError_t e = A->hipMemsetAsync(flag, 0, 4, s);
+    if (e == hipSuccess) e = A->hipMemsetAsync(keys, 0xff, bk, s);
+    for (int side = 0; side < 2 && e == hipSuccess && rc == MCS_OK; side++) {
+        mcs::KL2PrepArgs pa;
+        pa.desc = side ? dt : dq;
+        pa.n = side ? nt : nq;
+        const size_t o = side ? (size_t)nq : 0;
+        pa.i8 = d8 + o * dimp;
+        pa.norm_i = norm_i + o;
+        pa.sum_i = sum_i + o;
+        pa.norm_f = norm_f + o;
+        pa.flag = flag;
+        pa.dim = dim;
+        pa.dimp = dimp;
+        pa.pad_ = 0;
+        if (pa.n > 0) rc = launch(A, k->l2_prep, (pa.n + 3) / 4, 1, 256, &pa, sizeof(pa), s);
+    }
+    mcs::KL2Args a;
+    a.q8 = d8;
+    a.t8 = d8 + (size_t)nq * dimp;
+    a.qf = dq;
+    a.tf = dt;
+    a.qn = norm_i, a.tn = norm_i + nq, a.qs = sum_i, a.ts = sum_i + nq;
+    a.qnf = norm_f, a.tnf = norm_f + nq;
+    a.flag = flag;
+    a.keys = keys;
+    a.idx = idx2;
+    a.dist = dist2;
+    a.nq = nq, a.nt = nt, a.dim = dim, a.dimp = dimp, a.pad_ = 0;
+    const int qblocks = (nq + mcs::kL2QueriesPerBlock - 1) / mcs::kL2QueriesPerBlock;
+    int chunks = (2048 + qblocks - 1) / qblocks;
+    chunks = std::max(1, std::min(chunks, (nt + 255) / 256));
+    a.per_chunk = ((nt + chunks - 1) / chunks + 15) / 16 * 16;
+    chunks = nt > 0 ? (nt + a.per_chunk - 1) / a.per_chunk : 0;
+    if (e == hipSuccess && rc == MCS_OK && chunks > 0) {
+        rc = launch(A, k->l2_i8, qblocks, chunks, 256, &a, sizeof(a), s);
+        if (rc == MCS_OK) rc = launch(A, k->l2_f32, qblocks, chunks, 256, &a, sizeof(a), s);
+    }
+    if (e == hipSuccess && rc == MCS_OK)
+        rc = launch(A, k->l2_finalize, (2 * nq + 255) / 256, 1, 256, &a, sizeof(a), s);
+    uint32_t hflag = 0;
+    if (e == hipSuccess && rc == MCS_OK)
+        e = A->hipMemcpyAsync(&hflag, flag, 4, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = A->hipStreamSynchronize(s);
+    (void)A->hipFree(buf);
+    if (rc) return rc;
+    if (e != hipSuccess) return mcs::fail(MCS_E_HIP, "l2 knn2: %s", A->hipGetErrorString(e));
+    if (exact) *exact = hflag ? 0 : 1;
+    return MCS_OK;
+}
+
+int check_l2(int nq, int nt, int dim)
+{
+    if (nq < 0 || nt < 0 || nq > (1 << 26) || nt > (1 << 30) || dim < 1 || dim > mcs::kL2MaxDim)
+        return mcs::fail(MCS_E_INVALID, "n_query=%d n_train=%d dim=%d (1..%d)", nq, nt, dim,
+                         mcs::kL2MaxDim);
+    return MCS_OK;
 }
 
 int check_sizes(int nq, int nt)
@@ -164,6 +244,69 @@ int mcs_match_hamming_knn2_host(const uint8_t *query, int n_query, const uint8_t
     if (s) (void)A->hipStreamDestroy(s);
     (void)A->hipFree(buf);
     if (e != hipSuccess) return mcs::fail(MCS_E_HIP, "knn2 host path: %s", A->hipGetErrorString(e));
+    return rc;
+}
+
+int mcs_match_l2_knn2(const float *d_query, int n_query, const float *d_train, int n_train,
+                      int dim, int32_t *d_idx2, float *d_dist2, int *exact, int device,
+                      void *stream)
+{
+    mcs::clear_error();
+    int rc = check_l2(n_query, n_train, dim);
+    if (rc) return rc;
+    if (n_query == 0) return MCS_OK;
+    if (!d_query || (!d_train && n_train) || !d_idx2 || !d_dist2)
+        return mcs::fail(MCS_E_INVALID, "NULL buffer");
+    const Api *A = mcs::rt::api();
+    if (!A) return MCS_E_HIP;
+    DeviceGuard g(A, device);
+    if (g.err != hipSuccess)
+        return mcs::fail(MCS_E_HIP, "hipSetDevice(%d): %s", device, A->hipGetErrorString(g.err));
+    const FeatureKernels *k = nullptr;
+    rc = feature_kernels(A, device, &k);
+    if (rc) return rc;
+    return l2_knn2(A, k, d_query, n_query, d_train, n_train, dim, d_idx2, d_dist2, exact,
+                   (hipStream_t)stream);
+}
+
+int mcs_match_l2_knn2_host(const float *query, int n_query, const float *train, int n_train,
+                           int dim, int32_t *idx2, float *dist2, int *exact, int device)
+{
+    mcs::clear_error();
+    int rc = check_l2(n_query, n_train, dim);
+    if (rc) return rc;
+    if (n_query == 0) return MCS_OK;
+    if (!query || (!train && n_train) || !idx2 || !dist2)
+        return mcs::fail(MCS_E_INVALID, "NULL buffer");
+    const Api *A = mcs::rt::api();
+    if (!A) return MCS_E_HIP;
+    DeviceGuard g(A, device);
+    if (g.err != hipSuccess)
+        return mcs::fail(MCS_E_HIP, "hipSetDevice(%d): %s", device, A->hipGetErrorString(g.err));
+    const FeatureKernels *k = nullptr;
+    rc = feature_kernels(A, device, &k);
+    if (rc) return rc;
+    const size_t qb = (size_t)n_query * dim * 4, tb = (size_t)n_train * dim * 4;
+    const size_t ob = (size_t)n_query * 2 * 4;
+    uint8_t *buf = nullptr;
+    HIP_TRY(A->hipMalloc((void **)&buf, qb + tb + 2 * ob + 64));
+    float *dq = reinterpret_cast<float *>(buf);
+    float *dt = reinterpret_cast<float *>(buf + qb);
+    int32_t *di = reinterpret_cast<int32_t *>(buf + ((qb + tb + 15) & ~(size_t)15));
+    float *dd = reinterpret_cast<float *>(di + (size_t)n_query * 2);
+    hipStream_t s = nullptr;
+    hipError_t e = A->hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    if (e == hipSuccess) e = A->hipMemcpyAsync(dq, query, qb, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && tb) e = A->hipMemcpyAsync(dt, train, tb, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) rc = l2_knn2(A, k, dq, n_query, dt, n_train, dim, di, dd, exact, s);
+    if (e == hipSuccess && rc == MCS_OK)
+        e = A->hipMemcpyAsync(idx2, di, ob, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess && rc == MCS_OK)
+        e = A->hipMemcpyAsync(dist2, dd, ob, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess && s) e = A->hipStreamSynchronize(s);
+    if (s) (void)A->hipStreamDestroy(s);
+    (void)A->hipFree(buf);
+    if (e != hipSuccess) return mcs::fail(MCS_E_HIP, "l2 host path: %s", A->hipGetErrorString(e));
     return rc;
 }
 

@@ -82,6 +82,199 @@ extern "C" __global__ __launch_bounds__(256) void mcs_hamming_knn2_finalize(
     a.dist[i] = none ? -1 : (int32_t)(k >> kKnnKeyShift);
 }
 
+// ---- L2 kNN-2 --------------------------------------------------------------
+// Prep: one wave per descriptor (block 256 = 4 descriptors).
+extern "C" __global__ __launch_bounds__(256) void mcs_l2_prep(const mcs::KL2PrepArgs a)
+{
+    const int lane = threadIdx.x & 63, i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= a.n) return;
+    const float *d = a.desc + (int64_t)i * a.dim;
+    int8_t *o = a.i8 + (int64_t)i * a.dimp;
+    int ni = 0, si = 0;
+    float nf = 0.f;
+    bool ok = true;
+    for (int e = lane; e < a.dimp; e += 64) {
+        const float v = e < a.dim ? d[e] : 0.f;
+        const bool iv = v >= 0.f && v <= 255.f && v == __builtin_rintf(v);
+        ok = ok && iv;
+        const int x = iv ? (int)v : 0;
+        o[e] = (int8_t)(x - 128);
+        ni += x * x;
+        si += x - 128;
+        nf = __builtin_fmaf(v, v, nf);
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        ni += __shfl_xor(ni, off, 64);
+        si += __shfl_xor(si, off, 64);
+        nf += __shfl_xor(nf, off, 64);
+    }
+    const bool all = __all(ok);
+    if (lane == 0) {
+        a.norm_i[i] = ni;
+        a.sum_i[i] = si;
+        a.norm_f[i] = nf;
+        if (!all) atomicOr(a.flag, 1u);
+    }
+}
+
+namespace {
+
+__device__ __forceinline__ void top2_u64(unsigned long long &k0, unsigned long long &k1,
+                                         unsigned long long k)
+{
+    const unsigned long long lo = k < k0 ? k : k0, hi = k < k0 ? k0 : k;
+    k0 = lo;
+    k1 = hi < k1 ? hi : k1;
+}
+
+__device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long v, int m)
+{
+    const int lo = __shfl_xor((int)(uint32_t)v, m, 64), hi = __shfl_xor((int)(v >> 32), m, 64);
+    return ((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+
+// Key of squared distance d2 (>= 0) to train j: float distance bits, then the index.
+__device__ __forceinline__ unsigned long long l2_key(double d2, int j)
+{
+    const float f = (float)__builtin_sqrt(d2);
+    return ((unsigned long long)__float_as_uint(f) << 32) | (uint32_t)j;
+}
+
+// Lanes 16g .. 16g+15 hold partial top-2 lists of the same 4 queries: merge them, then lane 16g
+// merges into the global keys (3 atomics per query, as the Hamming matcher).
+__device__ __forceinline__ void l2_publish(const mcs::KL2Args &a, int q0, int lane,
+                                           unsigned long long (&k0)[4],
+                                           unsigned long long (&k1)[4])
+{
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+#pragma unroll
+        for (int m = 1; m < 16; m <<= 1) {
+            const unsigned long long b0 = shfl_xor_u64(k0[r], m), b1 = shfl_xor_u64(k1[r], m);
+            top2_u64(k0[r], k1[r], b0);
+            top2_u64(k0[r], k1[r], b1);
+        }
+    if ((lane & 15) != 0) return;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int q = q0 + (lane >> 4) * 4 + r;
+        if (q >= a.nq) continue;
+        const unsigned long long old = atomicMin(&a.keys[2 * q], k0[r]);
+        atomicMin(&a.keys[2 * q + 1], old > k0[r] ? old : k0[r]);
+        atomicMin(&a.keys[2 * q + 1], k1[r]);
+    }
+}
+
+typedef int l2_v4i __attribute__((ext_vector_type(4)));
+typedef float l2_v4f __attribute__((ext_vector_type(4)));
+
+}  // namespace
+
+// Exact path: grid (query blocks, train chunks), block 256.  Wave w: queries q0 .. q0+15 as the
+// MFMA A tile (lane l: query q0 + (l & 15), bytes 16 (l >> 4) .. +16 of each 64-byte k step),
+// trains in tiles of 16 as B (same lane map); C[g*4 + r][l & 15] = (a - 128).(b - 128).
+extern "C" __global__ __launch_bounds__(256) void mcs_l2_knn2_i8(const mcs::KL2Args a)
+{
+    using namespace mcs;
+    if (*a.flag) return;
+    const int lane = threadIdx.x & 63, g = lane >> 4;
+    const int q0 = blockIdx.x * kL2QueriesPerBlock + (threadIdx.x >> 6) * 16;
+    if (q0 >= a.nq) return;
+    const int steps = a.dimp / 64;
+    const int qa = min(q0 + (lane & 15), a.nq - 1);
+    l2_v4i A[kL2MaxDim / 64];
+#pragma unroll
+    for (int s = 0; s < kL2MaxDim / 64; s++)
+        A[s] = s < steps ? *reinterpret_cast<const l2_v4i *>(a.q8 + (int64_t)qa * a.dimp + s * 64 +
+                                                          g * 16)
+                         : l2_v4i{0, 0, 0, 0};
+    int qn[4], qs[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int q = min(q0 + g * 4 + r, a.nq - 1);
+        qn[r] = a.qn[q];
+        qs[r] = a.qs[q];
+    }
+    unsigned long long k0[4], k1[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) k0[r] = k1[r] = kL2KeyNone;
+    const int j0 = blockIdx.y * a.per_chunk, j1 = min(a.nt, j0 + a.per_chunk);
+    const int bias = 16384 * a.dimp;
+    for (int t0 = j0; t0 < j1; t0 += 16) {
+        const int j = t0 + (lane & 15), jr = min(j, a.nt - 1);
+        l2_v4i acc = {0, 0, 0, 0};
+#pragma unroll
+        for (int s = 0; s < kL2MaxDim / 64; s++) {
+            if (s >= steps) break;
+            const l2_v4i B =
+                *reinterpret_cast<const l2_v4i *>(a.t8 + (int64_t)jr * a.dimp + s * 64 + g * 16);
+            acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[s], B, acc, 0, 0, 0);
+        }
+        const int tn = a.tn[jr], ts = a.ts[jr];
+        if (j < j1) {
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int dot = acc[r] + 128 * (qs[r] + ts) + bias;
+                top2_u64(k0[r], k1[r], l2_key((double)(qn[r] + tn - 2 * dot), j));
+            }
+        }
+    }
+    l2_publish(a, q0, lane, k0, k1);
+}
+
+// f32 path: the same tiling with v_mfma_f32_16x16x4_f32; k chunks of 128, lane group g supplies
+// elements 32 g + s of the chunk at step s (the same map for A and B).
+extern "C" __global__ __launch_bounds__(256) void mcs_l2_knn2_f32(const mcs::KL2Args a)
+{
+    using namespace mcs;
+    if (!*a.flag) return;
+    const int lane = threadIdx.x & 63, g = lane >> 4;
+    const int q0 = blockIdx.x * kL2QueriesPerBlock + (threadIdx.x >> 6) * 16;
+    if (q0 >= a.nq) return;
+    const int qa = min(q0 + (lane & 15), a.nq - 1);
+    float qn[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) qn[r] = a.qnf[min(q0 + g * 4 + r, a.nq - 1)];
+    unsigned long long k0[4], k1[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) k0[r] = k1[r] = kL2KeyNone;
+    const int j0 = blockIdx.y * a.per_chunk, j1 = min(a.nt, j0 + a.per_chunk);
+    const float *qrow = a.qf + (int64_t)qa * a.dim;
+    for (int t0 = j0; t0 < j1; t0 += 16) {
+        const int j = t0 + (lane & 15), jr = min(j, a.nt - 1);
+        const float *trow = a.tf + (int64_t)jr * a.dim;
+        l2_v4f acc = {0.f, 0.f, 0.f, 0.f};
+        for (int c = 0; c < a.dim; c += 128) {
+#pragma unroll
+            for (int s = 0; s < 32; s++) {
+                const int e = c + 32 * g + s;
+                const float x = e < a.dim ? qrow[e] : 0.f, y = e < a.dim ? trow[e] : 0.f;
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x, y, acc, 0, 0, 0);
+            }
+        }
+        const float tn = a.tnf[jr];
+        if (j < j1) {
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const float d2 = qn[r] + tn - 2.f * acc[r];
+                top2_u64(k0[r], k1[r], l2_key(d2 > 0.f ? (double)d2 : 0.0, j));
+            }
+        }
+    }
+    l2_publish(a, q0, lane, k0, k1);
+}
+
+// keys -> (train index, distance); -1 / -1.0f where fewer than two train descriptors exist.
+extern "C" __global__ __launch_bounds__(256) void mcs_l2_knn2_finalize(const mcs::KL2Args a)
+{
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= 2 * a.nq) return;
+    const unsigned long long k = a.keys[i];
+    const bool none = k == mcs::kL2KeyNone;
+    a.idx[i] = none ? -1 : (int32_t)(uint32_t)k;
+    a.dist[i] = none ? -1.f : __uint_as_float((uint32_t)(k >> 32));
+}
+
 // ---- RANSAC homography (NS-5) ------------------------------------------------------------------
 // grid (iters), block kRansacBlock: thread 0 draws hypothesis k and solves its 4-point model,
 // then the block counts its inliers over all n correspondences (FP64, mcs_ransac_core.h).

@@ -20,6 +20,36 @@ struct KHammingArgs {
     int nq, nt, per_chunk, pad_;
 };
 
+// Brute-force L2 kNN-2 over float descriptors (BFMatcher(NORM_L2) / "BruteForce"
+// .knnMatch(k=2), the reference's SIFT matcher, StitcherClass.py:423-424).
+// Integer-valued descriptors in [0, 255] (OpenCV's SIFT output) take the exact path: int8 MFMA
+// on (d - 128), |a - b|^2 = |a|^2 + |b|^2 - 2 a.b in int32, distance = float(sqrt(double)) --
+// the same float OpenCV computes (its float sums are exact for such data); anything else takes
+// the f32-MFMA path (float |a|^2 + |b|^2 - 2 a.b).  Keys: float bits << 32 | train index.
+constexpr int kL2QueriesPerBlock = 64;   // 4 waves x one 16-query MFMA row tile
+constexpr int kL2MaxDim = 256;
+constexpr unsigned long long kL2KeyNone = ~0ull;
+struct KL2PrepArgs {
+    const float *desc;   // n x dim
+    int8_t *i8;          // n x dimp: d - 128 (padding: d = 0)
+    int32_t *norm_i;     // sum d^2 (exact path)
+    int32_t *sum_i;      // sum (d - 128)
+    float *norm_f;       // sum d^2 in float (f32 path)
+    uint32_t *flag;      // |= 1 when a value is not an integer in [0, 255]
+    int n, dim, dimp, pad_;
+};
+struct KL2Args {
+    const int8_t *q8, *t8;
+    const float *qf, *tf;
+    const int32_t *qn, *tn, *qs, *ts;
+    const float *qnf, *tnf;
+    const uint32_t *flag;
+    unsigned long long *keys;   // nq x 2
+    int32_t *idx;               // nq x 2 (finalised)
+    float *dist;                // nq x 2
+    int nq, nt, dim, dimp, per_chunk, pad_;
+};
+
 // RANSAC homography (mcs_ransac_core.h): one block per hypothesis scores it
 // over all correspondences; a second launch writes the best hypothesis' inlier mask.
 constexpr int kRansacBlock = 256;

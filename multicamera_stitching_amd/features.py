@@ -5,7 +5,8 @@ kNN-2, Lowe ratio (strict <), more than 4 matches, findHomography(RANSAC, reproj
 runs once per calibration (a keypress, video_mapping_node.py:187-188), not per frame.
 
 Backends (MCS_FEATURES = auto | sift | orb): "sift" is OpenCV contrib SIFT when cv2 is
-importable (the reference's own algorithm, CPU, float L2 matching); "orb" is the GPU path of
+importable (the reference's own algorithm; its float L2 kNN-2 runs on the GPU unless
+MCS_L2_MATCHER=cv2, exact for SIFT's integer-valued descriptors); "orb" is the GPU path of
 SURVEY.md 8 NS-3..5 -- ORB (mcs_orb_detect_host), brute-force Hamming kNN-2
 (mcs_match_hamming_knn2_host), the same ratio test, RANSAC (mcs_ransac_homography_host).  "auto"
 prefers SIFT (reference behaviour) and falls back to ORB when a GPU is present.  With neither,
@@ -101,9 +102,16 @@ def match_keypoints(owner, kpsA, kpsB, featuresA, featuresB, ratio=0.75, reprojT
             H, status = _capi.ransac_homography(ptsA, ptsB, reprojThresh)
         return H, matches, status
     cv2 = _cv2()
-    raw = cv2.DescriptorMatcher_create("BruteForce").knnMatch(featuresA, featuresB, 2)
-    matches = [(m[0].trainIdx, m[0].queryIdx) for m in raw
-               if len(m) == 2 and m[0].distance < m[1].distance * ratio]
+    if os.environ.get("MCS_L2_MATCHER", "gpu") == "gpu":
+        # BruteForce L2 kNN-2 on MFMA: SIFT's integer-valued descriptors are
+        # matched exactly as OpenCV's float arithmetic does (mcs_match_l2_knn2_host)
+        from . import _capi
+        idx, dist, _ = _capi.match_l2_knn2(featuresA, featuresB)
+        matches = ratio_matches(idx, dist, ratio)
+    else:
+        raw = cv2.DescriptorMatcher_create("BruteForce").knnMatch(featuresA, featuresB, 2)
+        matches = [(m[0].trainIdx, m[0].queryIdx) for m in raw
+                   if len(m) == 2 and m[0].distance < m[1].distance * ratio]
     H = status = None
     if len(matches) > 4:
         ptsA = np.float32([kpsA[i] for (_, i) in matches])

@@ -89,6 +89,8 @@ def lib():
         L.orc_undistort.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P,
                                     ctypes.c_int, P]
         L.orc_undistort.restype = ctypes.c_int
+        L.orc_l2_knn2.argtypes = [P, ctypes.c_int, P, ctypes.c_int, ctypes.c_int, P, P]
+        L.orc_l2_knn2.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -184,6 +186,18 @@ def hamming_knn2(query: np.ndarray, train: np.ndarray):
     dist = np.empty((q.shape[0], 2), np.int32)
     lib().orc_hamming_knn2(_p(q), q.shape[0], _p(t), t.shape[0], _p(idx), _p(dist))
     return idx, dist
+
+
+def l2_knn2(query, train):
+    """BFMatcher(NORM_L2).knnMatch(k=2) of float descriptors (orc_match.c): (idx, dist, exact)."""
+    q = np.ascontiguousarray(query, np.float32)
+    t = np.ascontiguousarray(train, np.float32)
+    dim = q.shape[1]
+    idx = np.empty((q.shape[0], 2), np.int32)
+    dist = np.empty((q.shape[0], 2), np.float32)
+    ex = lib().orc_l2_knn2(_p(q), q.shape[0], _p(t), t.shape[0] if t.size else 0, dim, _p(idx),
+                           _p(dist))
+    return idx, dist, bool(ex)
 
 
 def _stage_array(stages):

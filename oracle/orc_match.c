@@ -11,6 +11,7 @@
  * strictly larger -- so among equal distances the lower train index ranks first.
  * Parity against a real cv2 is unpinned (none in this image).
  */
+#include <math.h>
 #include <stdint.h>
 
 static inline int popcount32(uint32_t v) { return __builtin_popcount(v); }
@@ -41,4 +42,61 @@ void orc_hamming_knn2(const uint8_t *query, int nq, const uint8_t *train, int nt
             dist2[2 * q + k] = best_i[k] < 0 ? -1 : best_d[k];
         }
     }
+}
+
+/* BFMatcher(NORM_L2).knnMatch(query, train, k=2) for float descriptors (StitcherClass.py:423-424,
+ * SURVEY.md 8f-3).  OpenCV computes sqrt(sum (a - b)^2) in float; for descriptors that are
+ * integers in [0, 255] (SIFT's output) every partial sum is an integer below 2^24, so its result
+ * is exactly float(sqrt(d2)) of the integer d2 whatever its summation order -- restated here
+ * with int64 sums.  Other data: sum in double, distance float(sqrt) (a reference for tolerance
+ * checks, not OpenCV's rounding).  Order: distance, then train index (batchDistance insertion).
+ * Returns 1 when the exact integer form applied. */
+int orc_l2_knn2(const float *query, int nq, const float *train, int nt, int dim, int32_t *idx2,
+                float *dist2)
+{
+    int exact = 1;
+    for (long i = 0; i < (long)(nq + 0) * dim && exact; i++) {
+        const float v = query[i];
+        exact = v >= 0.f && v <= 255.f && v == (float)(int)v;
+    }
+    for (long i = 0; i < (long)nt * dim && exact; i++) {
+        const float v = train[i];
+        exact = v >= 0.f && v <= 255.f && v == (float)(int)v;
+    }
+#pragma omp parallel for schedule(static)
+    for (int q = 0; q < nq; q++) {
+        float bd[2] = {0, 0};
+        int bi[2] = {-1, -1};
+        for (int t = 0; t < nt; t++) {
+            double d2;
+            if (exact) {
+                int64_t s = 0;
+                for (int k = 0; k < dim; k++) {
+                    const int64_t d = (int64_t)query[(long)q * dim + k] -
+                                      (int64_t)train[(long)t * dim + k];
+                    s += d * d;
+                }
+                d2 = (double)s;
+            } else {
+                d2 = 0.0;
+                for (int k = 0; k < dim; k++) {
+                    const double d = (double)query[(long)q * dim + k] -
+                                     (double)train[(long)t * dim + k];
+                    d2 += d * d;
+                }
+            }
+            const float f = (float)sqrt(d2);
+            if (bi[0] < 0 || f < bd[0]) {
+                bd[1] = bd[0], bi[1] = bi[0];
+                bd[0] = f, bi[0] = t;
+            } else if (bi[1] < 0 || f < bd[1]) {
+                bd[1] = f, bi[1] = t;
+            }
+        }
+        for (int m = 0; m < 2; m++) {
+            idx2[2 * q + m] = bi[m];
+            dist2[2 * q + m] = bi[m] < 0 ? -1.f : bd[m];
+        }
+    }
+    return exact;
 }
