@@ -225,6 +225,13 @@ int mcs_stream_create(mcs_plan *plan, int depth, int use_graphs, mcs_stream **ou
 uint8_t *mcs_stream_input(mcs_stream *stream, int slot, int cam);
 int mcs_stream_next_slot(const mcs_stream *stream);
 int mcs_stream_submit(mcs_stream *stream, const uint8_t *const *cams, int *slot);
+/* mcs_stream_submit with a row pitch (bytes) per camera: camera c is cam_h rows of
+ * cam_w * channels bytes starting at cams[c], rows row_pitch[c] apart -- e.g. one frame of the
+ * reference's memmap bus, np.concatenate(images, axis=1) (video_mapping_node.py:140), with
+ * cams[c] = frame + c * cam_w * channels and row_pitch = the frame's row bytes.  NULL row_pitch
+ * = dense cameras. */
+int mcs_stream_submit_strided(mcs_stream *s, const uint8_t *const *cams,
+                              const int64_t *row_pitch, int *slot);
 int mcs_stream_wait(mcs_stream *stream, int slot, uint8_t *out);
 int mcs_stream_destroy(mcs_stream *stream);
 

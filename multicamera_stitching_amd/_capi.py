@@ -44,6 +44,7 @@ EXPORTS = (
     "mcs_plan_create_cylindrical", "mcs_plan_find_seams", "mcs_plan_seam_labels",
     "mcs_seam_graphcut_host", "mcs_plan_create_warp", "mcs_plan_create_undistort",
     "mcs_undistort_map_host", "mcs_match_l2_knn2", "mcs_match_l2_knn2_host",
+    "mcs_stream_submit_strided",
 )
 
 
@@ -184,6 +185,8 @@ def load() -> ctypes.CDLL:
         L.mcs_stream_next_slot.restype = I
         L.mcs_stream_submit.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(I)]
         L.mcs_stream_submit.restype = I
+        L.mcs_stream_submit_strided.argtypes = [P, ctypes.POINTER(P), P, ctypes.POINTER(I)]
+        L.mcs_stream_submit_strided.restype = I
         L.mcs_stream_wait.argtypes = [P, I, P]
         L.mcs_stream_wait.restype = I
         L.mcs_stream_destroy.argtypes = [P]
@@ -510,6 +513,31 @@ class StreamPipeline:
         ptrs = (ctypes.c_void_p * len(cams))(*[c.ctypes.data for c in cams])
         slot = ctypes.c_int(-1)
         check(self._lib.mcs_stream_submit(self._h, ptrs, ctypes.byref(slot)))
+        return slot.value
+
+    def submit_concat(self, frame) -> int:
+        """One frame of the reference's memmap bus layout: the cameras side by side on axis 1
+        (np.concatenate(images, axis=1), video_mapping_node.py:140), in the plan's camera
+        order; gathered into the pinned slot without an intermediate copy per camera."""
+        frame = np.asarray(frame)
+        if frame.dtype != np.uint8 or frame.strides[-1] != 1 or (
+                frame.ndim == 3 and frame.strides[1] != frame.shape[2]):
+            frame = np.ascontiguousarray(frame, dtype=np.uint8)
+        C = self.plan.channels
+        pitch = frame.strides[0]
+        ptrs, pitches, x = [], [], 0
+        for (h, w) in self.plan.cam_shapes:
+            if frame.shape[0] < h or frame.shape[1] < x + w:
+                raise ValueError(f"frame {frame.shape} too small for cameras {self.plan.cam_shapes}")
+            ptrs.append(frame.ctypes.data + x * C)
+            pitches.append(pitch)
+            x += w
+        if frame.shape[1] != x:
+            raise ValueError(f"frame width {frame.shape[1]} != sum of camera widths {x}")
+        pp = (ctypes.c_void_p * len(ptrs))(*ptrs)
+        rp = (ctypes.c_int64 * len(pitches))(*pitches)
+        slot = ctypes.c_int(-1)
+        check(self._lib.mcs_stream_submit_strided(self._h, pp, rp, ctypes.byref(slot)))
         return slot.value
 
     def wait(self, slot: int, out=None) -> np.ndarray:

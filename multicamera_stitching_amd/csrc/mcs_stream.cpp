@@ -166,8 +166,19 @@ int mcs_stream_next_slot(const mcs_stream *s)
 
 int mcs_stream_submit(mcs_stream *s, const uint8_t *const *cams, int *slot_out)
 {
+    return mcs_stream_submit_strided(s, cams, nullptr, slot_out);
+}
+
+int mcs_stream_submit_strided(mcs_stream *s, const uint8_t *const *cams,
+                              const int64_t *row_pitch, int *slot_out)
+{
     mcs::clear_error();
     if (!s) return mcs::fail(MCS_E_INVALID, "NULL stream");
+    if (cams && row_pitch)
+        for (int c = 0; c < s->n_cams; c++)
+            if (cams[c] && row_pitch[c] < (int64_t)s->cam_w[c] * s->channels)
+                return mcs::fail(MCS_E_INVALID, "camera %d: row pitch %lld < %d", c,
+                                 (long long)row_pitch[c], s->cam_w[c] * s->channels);
     const Api *A = mcs::rt::api();
     if (!A) return MCS_E_HIP;
     const int i = s->next;
@@ -176,10 +187,18 @@ int mcs_stream_submit(mcs_stream *s, const uint8_t *const *cams, int *slot_out)
         return mcs::fail(MCS_E_INVALID, "slot %d not yet collected (call mcs_stream_wait)", i);
     mcs::DeviceGuard g(A, s->device);
     if (cams)   // else: the caller filled mcs_stream_input() buffers in place
-        for (int c = 0; c < s->n_cams; c++)
-            if (cams[c])
-                memcpy(sl.h_in + s->cam_off[c], cams[c],
-                       (size_t)s->cam_w[c] * s->cam_h[c] * s->channels);
+        for (int c = 0; c < s->n_cams; c++) {
+            if (!cams[c]) continue;
+            const size_t row = (size_t)s->cam_w[c] * s->channels;
+            if (!row_pitch || row_pitch[c] == (int64_t)row) {
+                memcpy(sl.h_in + s->cam_off[c], cams[c], row * s->cam_h[c]);
+                continue;
+            }
+            // a camera inside a wider frame (e.g. the main_stream layout, cameras side by side
+            // on axis 1): gathered row by row into its dense staging slot
+            for (int y = 0; y < s->cam_h[c]; y++)
+                memcpy(sl.h_in + s->cam_off[c] + y * row, cams[c] + y * row_pitch[c], row);
+        }
     HIP_TRY(A->hipMemcpyAsync(sl.d_in, sl.h_in, s->in_bytes, hipMemcpyHostToDevice, s->up));
     HIP_TRY(A->hipEventRecord(sl.ev_in, s->up));
     HIP_TRY(A->hipStreamWaitEvent(s->compute, sl.ev_in, 0));
