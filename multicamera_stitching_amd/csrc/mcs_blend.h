@@ -264,64 +264,69 @@ __device__ __forceinline__ void feather_tile(const KBlendArgs &a)
     }
 }
 
-// Multi-band (3 levels): grid (listed tiles, ceil(frames / kMbFrames)), block kMbThreads2/4, the
-// source positions computed once per block and reused for its kMbFrames captures.  Level ranges
-// held per tile
-// (origin of the 32-px tile X0): level 0 [X0-16, X0+48), level 1 [X0/2-6, X0/2+20] (g1, m1),
-// level 2 [X0/4-2, X0/4+9] (g2, m2, B2), collapsed level 1 [X0/2-1, X0/2+16] (R1).  Entries at
-// coordinates outside the mosaic hold the reflected coordinate's value, so reflected lookups
-// (always inside the mosaic) land in range.
+// ---- multi-band (3 levels) -------------------------------------------------------------------
+// Per listed tile (a 32 x 32 output tile whose 64 x 64 neighbourhood holds two or more owners)
+// the pyramid needs, per owner slot: level 0 over [X0-14, X0+42] (57 of the 64 px), level 1
+// g1 over [X0/2-6, X0/2+20] (27), level 2 g2 over [X0/4-2, X0/4+9] (12), and the collapsed
+// level 1 R1 over [X0/2-1, X0/2+16] (18, "the R1 region").  Entries at coordinates outside the
+// mosaic hold the reflected coordinate's value, so reflected lookups land in range.  Three
+// kernels, all with small LDS footprints (many blocks per CU) and no FP64 map in the capture
+// loop:
+//   mcs_mb_prep_c*_i*   once per plan: per (tile, owner) the source window + folded bilinear
+//                       weights of every level-0 sample (mb_desc), and per tile the seam masks
+//                       m1 (R1 region), m2, and their sums over the owners (the denominators);
+//   mcs_mb_levels_c*    per (tile, owner, 4 captures): samples -> level 0 (LDS) -> separable
+//                       5-tap reduces -> g1 (R1 region, u16) and g2 to a scratch buffer;
+//   mcs_mb_blend_c*     per (tile, capture): B2, R1 = B1 + up(B2), R0 = L0_owner + up(R1) over
+//                       the tile's pixels; level 0 of the owner is the owner sample the stitch
+//                       kernel already wrote (equal to the replicate-border sample wherever the
+//                       owner covers the pixel, which it always does).
+// Long launches run in chunks of captures so the scratch stays a few tens of MB.
 constexpr int kMbR0 = kBlendTile + 2 * kBlendHalo;   // 64
 constexpr int kMbN1 = 27, kMbO1 = 6;                  // level 1: [X0/2 - 6, X0/2 + 20]
-constexpr int kMbN2 = 12, kMbO2 = 2;                  // level 2: [X0/4 - 2, X0/4 + 9]
-constexpr int kMbNR = 18, kMbOR = 1;                  // R1:      [X0/2 - 1, X0/2 + 16]
-constexpr int kMbFirst = 2, kMbUsed = 57;             // level-0 offsets the pyramid reads
+constexpr int kMbN2 = kMbN2Px, kMbO2 = 2;             // level 2: [X0/4 - 2, X0/4 + 9]
+constexpr int kMbNR = kMbNRPx, kMbOR = 1;             // R1:      [X0/2 - 1, X0/2 + 16]
+constexpr int kMbFirst = 2, kMbUsed = kMbUsedPx;      // level-0 offsets the pyramid reads
+constexpr int kMbU = kMbUsed * kMbUsed;               // level-0 samples per owner
+constexpr int kMbRS = kMbO1 - kMbOR;                  // R1 region origin in the level-1 array (5)
 
-__device__ __forceinline__ int exp_taps(int x, int n, int *idx, int *wt)
+// Expand taps of fine index x into a coarse level of size n (IN: no reflection needed).
+template <bool IN>
+__device__ __forceinline__ void exp_taps(int x, int n, int *idx, int *wt)
 {
     if ((x & 1) == 0) {
-        idx[0] = refl(x / 2 - 1, n), wt[0] = 1;
-        idx[1] = refl(x / 2, n), wt[1] = 6;
-        idx[2] = refl(x / 2 + 1, n), wt[2] = 1;
-        return 3;
+        idx[0] = IN ? x / 2 - 1 : refl(x / 2 - 1, n), wt[0] = 1;
+        idx[1] = IN ? x / 2 : refl(x / 2, n), wt[1] = 6;
+        idx[2] = IN ? x / 2 + 1 : refl(x / 2 + 1, n), wt[2] = 1;
+        return;
     }
-    idx[0] = refl((x - 1) / 2, n), wt[0] = 4;
-    idx[1] = refl((x + 1) / 2, n), wt[1] = 4;
+    idx[0] = IN ? (x - 1) / 2 : refl((x - 1) / 2, n), wt[0] = 4;
+    idx[1] = IN ? (x + 1) / 2 : refl((x + 1) / 2, n), wt[1] = 4;
     idx[2] = idx[1], wt[2] = 0;   // padding tap: adds an exact 0, keeps the trip count fixed
-    return 3;
 }
-
-// LDS of one multi-band block for up to S owner slots.  Level-0 arrays hold the 57 x 57 part of
-// the 64 x 64 neighbourhood the pyramid reads (offsets [2, 58]); hs/hm: the horizontal passes of
-// the separable 5-tap reduces, aliased with the blend arrays of the later phases.
-template <int CN, int S>
-struct MbLds {
-    static constexpr int HS = S <= 2 ? S : 1;   // slots per separable-pass group
-    uint8_t g0[S][kMbUsed * kMbUsed * CN];
-    int32_t g1[S][kMbN1 * kMbN1 * CN];
-    int32_t g2[S][kMbN2 * kMbN2 * CN];
-    uint16_t m1[S][kMbN1 * kMbN1];
-    int32_t m2[S][kMbN2 * kMbN2];
-    uint8_t own[kMbUsed * kMbUsed];
-    union {
-        struct {   // phases 2-3 (separable reduce passes)
-            uint16_t hs[HS][kMbUsed * kMbN1 * CN];
-            uint8_t hm[HS][kMbUsed * kMbN1];
-            int32_t hs2[HS][kMbN1 * kMbN2 * CN];
-            int32_t hm2[HS][kMbN1 * kMbN2];
-        };
-        struct {   // phases 4-6
-            double b2[kMbN2 * kMbN2 * CN];
-            double r1[kMbNR * kMbNR * CN];
-        };
-    };
-};
 
 // Geometry of one multi-band tile: level sizes and the origins of the arrays held per level.
 struct MbGeo {
     int W, H, w1, h1, w2, h2;
     int X0, Y0, RX, RY, X1, Y1, X2, Y2, XR, YR;
+    bool interior;
 };
+
+__device__ __forceinline__ MbGeo mb_geo(const KParams &P, int t)
+{
+    MbGeo G;
+    G.W = P.out_w;
+    G.H = P.out_h;
+    G.w1 = (G.W + 1) / 2, G.h1 = (G.H + 1) / 2, G.w2 = (G.w1 + 1) / 2, G.h2 = (G.h1 + 1) / 2;
+    const int gx = (G.W + kBlendTile - 1) / kBlendTile;
+    G.X0 = (t % gx) * kBlendTile, G.Y0 = (t / gx) * kBlendTile;
+    G.RX = G.X0 - kBlendHalo, G.RY = G.Y0 - kBlendHalo;         // level-0 origin
+    G.X1 = G.X0 / 2 - kMbO1, G.Y1 = G.Y0 / 2 - kMbO1;             // level-1 origin
+    G.X2 = G.X0 / 4 - kMbO2, G.Y2 = G.Y0 / 4 - kMbO2;             // level-2 origin
+    G.XR = G.X0 / 2 - kMbOR, G.YR = G.Y0 / 2 - kMbOR;             // R1 origin
+    G.interior = G.RX >= 0 && G.RY >= 0 && G.RX + kMbR0 <= G.W && G.RY + kMbR0 <= G.H;
+    return G;
+}
 
 // Level coordinate -> reflected coordinate.  IN (interior tile): every coordinate the tile
 // touches lies inside its level, so the reflection is the identity and index arithmetic folds.
@@ -333,182 +338,380 @@ __device__ __forceinline__ int ix2(int c, int o, int n)
     return IN ? c - o : min(max(c - o, 0), n - 1);
 }
 
-// One capture through the pyramid phases 2-6 (g0 and the owner map already in LDS).
-template <int CN, int S, bool IN>
-__device__ __forceinline__ void mb_phases(const KParams &P, const MbGeo &G, MbLds<CN, S> &L,
-                                          int ns, int f)
+// Replicate-border bilinear sample of slot s at output (x, y) (sample_replicate) as an 8-byte
+// window descriptor: off = byte offset of tap row a in the frame (bit 31: tap row b is the next
+// row, else the same row); meta = fx | fy << 5 | (left tap on byte CN) << 10 | (right tap on
+// byte CN) << 11 | d << 12, where d = bytes both windows start earlier so that row b's window
+// ends inside the frame (the taps then sit at bytes d and d + CN).  Every capture's load is then
+// unconditional.  Frames with (h - 1) * w * CN < 16 bytes take load8's guarded path instead.
+template <int CN, int INTERP>
+__device__ __forceinline__ uint2 mb_desc(const KParams &P, int s, int x, int y)
 {
-    const int tid = threadIdx.x, nt = blockDim.x;
+    int x32, y32, cam, w, h;
+    slot_xy<INTERP>(P, s, x, y, x32, y32, cam, w, h);
+    const int sx = x32 >> 5, sy = y32 >> 5;
+    const int c = w >= 2 ? min(max(sx, 0), w - 2) : 0;
+    const uint32_t a_hi = min(max(sx, 0), w - 1) > c;
+    const uint32_t b_hi = min(max(sx + 1, 0), w - 1) > c;
+    const int ya = min(max(sy, 0), h - 1), yb = min(max(sy + 1, 0), h - 1);
+    const int64_t pitch = (int64_t)w * CN, fbytes = pitch * h;
+    const int64_t oa = ya * pitch + (int64_t)c * CN, ob = oa + (yb > ya ? pitch : 0);
+    const uint32_t d = (uint32_t)min(max(ob + 8 - fbytes, (int64_t)0), (int64_t)7);
+    uint2 r;
+    r.x = (uint32_t)oa | (yb > ya ? 0x80000000u : 0u);
+    r.y = (uint32_t)(x32 & 31) | ((uint32_t)(y32 & 31) << 5) | (a_hi << 10) | (b_hi << 11) |
+          (d << 12);
+    return r;
+}
+
+// The descriptor's 15-bit weights folded onto the taps' window bytes as u16 pairs (row a,
+// row b), so that mb_tap() gives sample_replicate's (sum p w + 2^14) >> 15 exactly.
+__device__ __forceinline__ void mb_weights(uint32_t meta, uint32_t &wa, uint32_t &wb)
+{
+    const uint32_t fx = meta & 31u, fy = (meta >> 5) & 31u;
+    const uint32_t w00 = (32 - fx) * (32 - fy) * 32, w01 = fx * (32 - fy) * 32;
+    const uint32_t w10 = (32 - fx) * fy * 32, w11 = fx * fy * 32;
+    const uint32_t sa = (meta & 1024u) ? 16u : 0u, sb = (meta & 2048u) ? 16u : 0u;
+    wa = (w00 << sa) + (w01 << sb);
+    wb = (w10 << sa) + (w11 << sb);
+}
+
+// Channel k of a descriptor's sample from its two (shifted) row windows.
+template <int CN>
+__device__ __forceinline__ uint32_t mb_tap(uint2 r0, uint2 r1, uint32_t wa, uint32_t wb, int k,
+                                           uint32_t d)
+{
+    typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+    const uint32_t sel = ((uint32_t)k | (0x0cu << 8) | ((uint32_t)(CN + k) << 16) | (0x0cu << 24)) +
+                         d * 0x00010001u;
+    const uint32_t a0 = __builtin_amdgcn_perm(r0.y, r0.x, sel);
+    const uint32_t a1 = __builtin_amdgcn_perm(r1.y, r1.x, sel);
+    uint32_t v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, a0), __builtin_bit_cast(us2, wa),
+                                        16384u, false);
+    v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, a1), __builtin_bit_cast(us2, wb), v, false);
+    return v >> 15;
+}
+
+// Local slot j (0 .. popc(mask) - 1) -> plan slot: the j-th set bit of mask.
+__device__ __forceinline__ int mb_slot(uint32_t mask, int j)
+{
+    for (int q = 0; q < j; q++) mask &= mask - 1;
+    return __ffs(mask) - 1;
+}
+
+// ---- prep (once per plan): grid (listed tiles), block kMbPrepThreads ---------------------------
+template <int CN, int INTERP>
+__device__ __forceinline__ void mb_prep(const KMbArgs &a)
+{
+    __shared__ uint8_t own[kMbU];
+    __shared__ int32_t m1[kBlendSlots][kMbN1 * kMbN1];
+    __shared__ int32_t m2[kBlendSlots][kMbN2 * kMbN2];
+    const KParams &P = a.P;
+    const int bt = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+    const uint32_t mask = (uint32_t)a.list[2 + 2 * bt];
+    const int ns = __popc(mask);
+    const MbGeo G = mb_geo(P, a.list[1 + 2 * bt]);
     const int w5[5] = {1, 4, 6, 4, 1};
-    const int RX2 = G.RX + kMbFirst, RY2 = G.RY + kMbFirst;   // origin of the level-0 arrays
-    auto i0 = [&](int cx, int cy) {
-        return ix2<IN>(cy, RY2, kMbUsed) * kMbUsed + ix2<IN>(cx, RX2, kMbUsed);
+    // owner map of the used neighbourhood as local slot indices (bit rank in `mask`)
+    for (int i = tid; i < kMbU; i += nt) {
+        const int cx = refl(G.RX + kMbFirst + i % kMbUsed, G.W);
+        const int cy = refl(G.RY + kMbFirst + i / kMbUsed, G.H);
+        const int o = a.owner[(int64_t)cy * G.W + cx];
+        own[i] = (uint8_t)((o != kBlendNone && ((mask >> o) & 1u))
+                               ? __popc(mask & ((1u << o) - 1u)) : kBlendNone);
+    }
+    // every owner's level-0 sample windows
+    for (int i = tid; i < kMbU * ns; i += nt) {
+        const int j = i / kMbU, e = i % kMbU;
+        const int cx = refl(G.RX + kMbFirst + e % kMbUsed, G.W);
+        const int cy = refl(G.RY + kMbFirst + e / kMbUsed, G.H);
+        const uint2 v = mb_desc<CN, INTERP>(P, mb_slot(mask, j), cx, cy);
+        a.desc[((int64_t)bt * a.slots + j) * kMbU + e] = (uint64_t)v.x | ((uint64_t)v.y << 32);
+    }
+    __syncthreads();
+    const int RX2 = G.RX + kMbFirst, RY2 = G.RY + kMbFirst;
+    // m1 = reduce(owner == slot) over the level-1 array (25-tap form with reflection)
+    for (int i = tid; i < kMbN1 * kMbN1 * ns; i += nt) {
+        const int j = i / (kMbN1 * kMbN1), e = i % (kMbN1 * kMbN1);
+        const int qx = refl(G.X1 + e % kMbN1, G.w1), qy = refl(G.Y1 + e / kMbN1, G.h1);
+        int macc = 0;
+        for (int u = 0; u < 5; u++) {
+            const int cy = refl(2 * qy + u - 2, G.H);
+            for (int v = 0; v < 5; v++) {
+                const int cx = refl(2 * qx + v - 2, G.W);
+                const int p = ix2<false>(cy, RY2, kMbUsed) * kMbUsed + ix2<false>(cx, RX2, kMbUsed);
+                macc += own[p] == j ? w5[u] * w5[v] : 0;
+            }
+        }
+        m1[j][e] = macc;
+    }
+    __syncthreads();
+    // m2 = reduce(m1)
+    for (int i = tid; i < kMbN2 * kMbN2 * ns; i += nt) {
+        const int j = i / (kMbN2 * kMbN2), e = i % (kMbN2 * kMbN2);
+        const int zx = refl(G.X2 + e % kMbN2, G.w2), zy = refl(G.Y2 + e / kMbN2, G.h2);
+        int macc = 0;
+        for (int u = 0; u < 5; u++) {
+            const int qy = refl(2 * zy + u - 2, G.h1);
+            for (int v = 0; v < 5; v++) {
+                const int qx = refl(2 * zx + v - 2, G.w1);
+                const int p = ix2<false>(qy, G.Y1, kMbN1) * kMbN1 + ix2<false>(qx, G.X1, kMbN1);
+                macc += w5[u] * w5[v] * m1[j][p];
+            }
+        }
+        m2[j][e] = macc;
+    }
+    __syncthreads();
+    // table: m1 (R1 region) [slots], m2 [slots], d1 (R1 region), d2
+    int32_t *tab = a.tab + (int64_t)bt * mb_tab_words(a.slots);
+    int32_t *t_m1 = tab, *t_m2 = tab + a.slots * kMbNR * kMbNR;
+    int32_t *t_d1 = t_m2 + a.slots * kMbN2 * kMbN2, *t_d2 = t_d1 + kMbNR * kMbNR;
+    for (int e = tid; e < kMbNR * kMbNR; e += nt) {
+        const int p = (e / kMbNR + kMbRS) * kMbN1 + e % kMbNR + kMbRS;
+        int d = 0;
+        for (int j = 0; j < a.slots; j++) {
+            const int v = j < ns ? m1[j][p] : 0;
+            t_m1[j * kMbNR * kMbNR + e] = v;
+            d += v;
+        }
+        t_d1[e] = d;
+    }
+    for (int e = tid; e < kMbN2 * kMbN2; e += nt) {
+        int d = 0;
+        for (int j = 0; j < a.slots; j++) {
+            const int v = j < ns ? m2[j][e] : 0;
+            t_m2[j * kMbN2 * kMbN2 + e] = v;
+            d += v;
+        }
+        t_d2[e] = d;
+    }
+}
+
+// ---- levels: grid (listed tiles, slots, ceil(nf / kMbLvFrames)), block kMbLvThreads -------------
+template <int CN>
+struct MbLvLds {
+    uint32_t g0[kMbU];                 // level 0: channel k in byte k
+    uint2 g1[kMbN1 * kMbN1];           // 256 G1 <= 65280 as u16 lanes: x = (c0, c2), y = (c1, c3)
+    union {
+        uint2 hs[kMbUsed * kMbN1];     // horizontal pass of level 1 (<= 4080), lanes as g1
+        int4 hs2[kMbN1 * kMbN2];       // horizontal pass of level 2, one int per channel
     };
-    auto i1 = [&](int cx, int cy) {
-        return ix2<IN>(cy, G.Y1, kMbN1) * kMbN1 + ix2<IN>(cx, G.X1, kMbN1);
-    };
+};
+
+// u16 lane of channel k in a packed level-1 entry (x = (c0, c2), y = (c1, c3))
+__device__ __forceinline__ int ch16(uint2 v, int k)
+{
+    return (int)((((k & 1) ? v.y : v.x) >> ((k & 2) ? 16 : 0)) & 0xffffu);
+}
+
+template <int CN>
+__device__ __forceinline__ void mb_levels(const KMbArgs &a, MbLvLds<CN> &L)
+{
+    constexpr int NT = kMbLvThreads, KJ = (kMbU + NT - 1) / NT;
+    const KParams &P = a.P;
+    const int bt = blockIdx.x, j = blockIdx.y, tid = threadIdx.x;
+    const uint32_t mask = (uint32_t)a.list[2 + 2 * bt];
+    if (j >= __popc(mask)) return;   // uniform: the whole block leaves before any barrier
+    const MbGeo G = mb_geo(P, a.list[1 + 2 * bt]);
+    int cam, w, h;
+    slot_info(P, mb_slot(mask, j), cam, w, h);
+    const int64_t pitch = (int64_t)w * CN, fbytes = pitch * h;
+    const bool shifted = (h - 1) * pitch >= 16;
+    // this owner's sample windows, once for the block's captures (frames with
+    // (h - 1) * pitch < 16 bytes re-read them per capture and take load8's guarded path)
+    uint32_t doff[KJ], dmeta[KJ];
+    const uint64_t *dsc = a.desc + ((int64_t)bt * a.slots + j) * kMbU;
+#pragma unroll
+    for (int kk = 0; kk < KJ; kk++) {
+        const int i = tid + kk * NT;
+        const uint64_t v = (shifted && i < kMbU) ? dsc[i] : 0ull;
+        doff[kk] = (uint32_t)v;
+        dmeta[kk] = (uint32_t)(v >> 32);
+    }
+    const int w5[5] = {1, 4, 6, 4, 1};
+    const int fl0 = blockIdx.z * kMbLvFrames, fl1 = min(a.nf, fl0 + kMbLvFrames);
+    for (int fl = fl0; fl < fl1; fl++) {
+        const uint8_t *fb = P.cams[cam] + (int64_t)(a.f0 + fl) * P.cam_fstride[cam];
+        // level 0.  The descriptors are made opaque per capture so that the compiler does not
+        // hoist their decoding out of the loop (which would hold ~5 registers per sample).
+        if (shifted) {
+#pragma unroll
+            for (int kk = 0; kk < KJ; kk++) {
+                asm volatile("" : "+v"(doff[kk]), "+v"(dmeta[kk]));
+                const uint32_t d = dmeta[kk] >> 12;
+                const uint32_t o = (doff[kk] & 0x7fffffffu) - d;
+                const uint32_t ob = o + ((doff[kk] >> 31) ? (uint32_t)pitch : 0u);
+                uint2 r0, r1;
+                __builtin_memcpy(&r0, fb + o, 8);
+                __builtin_memcpy(&r1, fb + ob, 8);
+                const int i = tid + kk * NT;
+                if (i < kMbU) {
+                    uint32_t wa, wb, px = 0;
+                    mb_weights(dmeta[kk], wa, wb);
+#pragma unroll
+                    for (int k = 0; k < CN; k++) px |= mb_tap<CN>(r0, r1, wa, wb, k, d) << (8 * k);
+                    L.g0[i] = px;
+                }
+            }
+        } else {
+            for (int i = tid; i < kMbU; i += NT) {
+                const uint64_t v = dsc[i];
+                const uint32_t o = (uint32_t)v & 0x7fffffffu;
+                const uint32_t ob = o + (((uint32_t)v >> 31) ? (uint32_t)pitch : 0u);
+                const uint2 r0 = load8<2 * CN>(fb, o, fbytes), r1 = load8<2 * CN>(fb, ob, fbytes);
+                uint32_t wa, wb, px = 0;
+                mb_weights((uint32_t)(v >> 32), wa, wb);
+#pragma unroll
+                for (int k = 0; k < CN; k++) px |= mb_tap<CN>(r0, r1, wa, wb, k, 0u) << (8 * k);
+                L.g0[i] = px;
+            }
+        }
+        __syncthreads();
+        const int64_t job = ((int64_t)bt * a.slots + j) * a.chunk + fl;
+        uint2 *og1 = reinterpret_cast<uint2 *>(a.g1) + job * (kMbNR * kMbNR);
+        int32_t *og2 = a.g2 + job * (kMbN2 * kMbN2 * CN);
+        if (G.interior) {
+            // separable 5-tap reduces, all channels at once in 16-bit lanes up to level 1 (the
+            // sums stay below 2^16: exact), then per channel.  Level-1 entry e reads level-0
+            // offsets 2e + [0, 5); level-2 entry z reads level-1 entries 2z + [0, 5).
+            for (int i = tid; i < kMbUsed * kMbN1; i += NT) {
+                const int r = i / kMbN1, e = i % kMbN1;
+                const uint32_t *g = &L.g0[r * kMbUsed + 2 * e];
+                uint32_t lo = 0, hi = 0;
+#pragma unroll
+                for (int v = 0; v < 5; v++) {
+                    const uint32_t t = g[v];
+                    lo += (uint32_t)w5[v] * (t & 0x00ff00ffu);
+                    hi += (uint32_t)w5[v] * ((t >> 8) & 0x00ff00ffu);
+                }
+                L.hs[i] = make_uint2(lo, hi);
+            }
+            __syncthreads();
+            for (int i = tid; i < kMbN1 * kMbN1; i += NT) {
+                const int ey = i / kMbN1, ex = i % kMbN1;
+                uint32_t lo = 0, hi = 0;
+#pragma unroll
+                for (int u = 0; u < 5; u++) {
+                    const uint2 t = L.hs[(2 * ey + u) * kMbN1 + ex];
+                    lo += (uint32_t)w5[u] * t.x;
+                    hi += (uint32_t)w5[u] * t.y;
+                }
+                L.g1[i] = make_uint2(lo, hi);
+            }
+            __syncthreads();
+            for (int i = tid; i < kMbN1 * kMbN2; i += NT) {
+                const int r = i / kMbN2, e = i % kMbN2;
+                int acc[4] = {0, 0, 0, 0};
+#pragma unroll
+                for (int v = 0; v < 5; v++) {
+                    const uint2 t = L.g1[r * kMbN1 + 2 * e + v];
+#pragma unroll
+                    for (int k = 0; k < CN; k++) acc[k] += w5[v] * ch16(t, k);
+                }
+                L.hs2[i] = make_int4(acc[0], acc[1], acc[2], acc[3]);
+            }
+            __syncthreads();
+            for (int i = tid; i < kMbN2 * kMbN2; i += NT) {
+                const int ey = i / kMbN2, ex = i % kMbN2;
+                int acc[4] = {0, 0, 0, 0};
+#pragma unroll
+                for (int u = 0; u < 5; u++) {
+                    const int4 t = L.hs2[(2 * ey + u) * kMbN2 + ex];
+                    acc[0] += w5[u] * t.x;
+                    acc[1] += w5[u] * t.y;
+                    acc[2] += w5[u] * t.z;
+                    acc[3] += w5[u] * t.w;
+                }
+#pragma unroll
+                for (int k = 0; k < CN; k++) og2[i * CN + k] = acc[k];
+            }
+        } else {
+            // mosaic-border tiles: 25-tap form with reflection at every level
+            const int RX2 = G.RX + kMbFirst, RY2 = G.RY + kMbFirst;
+            for (int e = tid; e < kMbN1 * kMbN1; e += NT) {
+                const int qx = refl(G.X1 + e % kMbN1, G.w1), qy = refl(G.Y1 + e / kMbN1, G.h1);
+                uint32_t lo = 0, hi = 0;
+                for (int u = 0; u < 5; u++) {
+                    const int cy = ix2<false>(refl(2 * qy + u - 2, G.H), RY2, kMbUsed);
+#pragma unroll
+                    for (int v = 0; v < 5; v++) {
+                        const int cx = ix2<false>(refl(2 * qx + v - 2, G.W), RX2, kMbUsed);
+                        const uint32_t t = L.g0[cy * kMbUsed + cx], wt = w5[u] * w5[v];
+                        lo += wt * (t & 0x00ff00ffu);
+                        hi += wt * ((t >> 8) & 0x00ff00ffu);
+                    }
+                }
+                L.g1[e] = make_uint2(lo, hi);
+            }
+            __syncthreads();
+            for (int e = tid; e < kMbN2 * kMbN2; e += NT) {
+                const int zx = refl(G.X2 + e % kMbN2, G.w2), zy = refl(G.Y2 + e / kMbN2, G.h2);
+                int acc[4] = {0, 0, 0, 0};
+                for (int u = 0; u < 5; u++) {
+                    const int qy = ix2<false>(refl(2 * zy + u - 2, G.h1), G.Y1, kMbN1);
+#pragma unroll
+                    for (int v = 0; v < 5; v++) {
+                        const int qx = ix2<false>(refl(2 * zx + v - 2, G.w1), G.X1, kMbN1);
+                        const uint2 t = L.g1[qy * kMbN1 + qx];
+                        const int wt = w5[u] * w5[v];
+#pragma unroll
+                        for (int k = 0; k < CN; k++) acc[k] += wt * ch16(t, k);
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < CN; k++) og2[e * CN + k] = acc[k];
+            }
+        }
+        // the R1 region of g1 (level-1 entries [kMbRS, kMbRS + 18) of the 27-entry array)
+        for (int e = tid; e < kMbNR * kMbNR; e += NT)
+            og1[e] = L.g1[(e / kMbNR + kMbRS) * kMbN1 + e % kMbNR + kMbRS];
+        __syncthreads();   // the next capture overwrites level 0 and the pass arrays
+    }
+}
+
+// ---- blend: grid (listed tiles, nf), block kMbBlThreads ------------------------------------------
+template <int CN>
+struct MbBlLds {
+    uint2 g1[kBlendSlots][kMbNR * kMbNR];   // packed as in mb_levels
+    int32_t g2[kBlendSlots][kMbN2 * kMbN2 * CN];
+    double b2[kMbN2 * kMbN2 * CN];
+    double r1[kMbNR * kMbNR * CN];
+};
+
+template <int CN, bool IN>
+__device__ __forceinline__ void mb_blend_tile(const KMbArgs &a, const MbGeo &G, MbBlLds<CN> &L,
+                                              uint32_t mask, int ns, int f)
+{
+    const KParams &P = a.P;
+    const int tid = threadIdx.x, nt = blockDim.x;
+    const int32_t *tab = a.tab + (int64_t)blockIdx.x * mb_tab_words(a.slots);
+    const int32_t *t_m1 = tab, *t_m2 = tab + a.slots * kMbNR * kMbNR;
+    const int32_t *t_d1 = t_m2 + a.slots * kMbN2 * kMbN2, *t_d2 = t_d1 + kMbNR * kMbNR;
     auto i2 = [&](int cx, int cy) {
         return ix2<IN>(cy, G.Y2, kMbN2) * kMbN2 + ix2<IN>(cx, G.X2, kMbN2);
     };
-    auto ir = [&](int cx, int cy) {
+    auto ir = [&](int cx, int cy) {   // the R1 region (g1, m1, d1, r1)
         return ix2<IN>(cy, G.YR, kMbNR) * kMbNR + ix2<IN>(cx, G.XR, kMbNR);
     };
-    if (IN) {
-        // 2-3, interior tiles: separable 5-tap reduces (integer sums: the same values as the
-        // 25-tap form).  Level-1 entry e reads level-0 offsets 2e + [0, 5) of the 57-wide
-        // arrays; level-2 entry z reads level-1 entries 2z + [0, 5).
-        constexpr int HS = MbLds<CN, S>::HS;
-        for (int jg = 0; jg < ns; jg += HS) {
-            for (int i = tid; i < kMbUsed * kMbN1 * HS; i += nt) {
-                const int jl = i / (kMbUsed * kMbN1), e0 = i % (kMbUsed * kMbN1), j = jg + jl;
-                if (j >= ns) break;
-                const int r = e0 / kMbN1, e = e0 % kMbN1;
-                const uint8_t *g = &L.g0[j][(r * kMbUsed + 2 * e) * CN];
-                const uint8_t *ow = &L.own[r * kMbUsed + 2 * e];
-                int acc[CN], macc = 0;
-#pragma unroll
-                for (int k = 0; k < CN; k++) acc[k] = 0;
-#pragma unroll
-                for (int v = 0; v < 5; v++) {
-                    macc += ow[v] == j ? w5[v] : 0;
-#pragma unroll
-                    for (int k = 0; k < CN; k++) acc[k] += w5[v] * g[v * CN + k];
-                }
-                L.hm[jl][e0] = (uint8_t)macc;
-#pragma unroll
-                for (int k = 0; k < CN; k++) L.hs[jl][e0 * CN + k] = (uint16_t)acc[k];
-            }
-            __syncthreads();
-            for (int i = tid; i < kMbN1 * kMbN1 * HS; i += nt) {
-                const int jl = i / (kMbN1 * kMbN1), e0 = i % (kMbN1 * kMbN1), j = jg + jl;
-                if (j >= ns) break;
-                const int ey = e0 / kMbN1, ex = e0 % kMbN1;
-                int acc[CN], macc = 0;
-#pragma unroll
-                for (int k = 0; k < CN; k++) acc[k] = 0;
-#pragma unroll
-                for (int u = 0; u < 5; u++) {
-                    const int q = (2 * ey + u) * kMbN1 + ex;
-                    macc += w5[u] * L.hm[jl][q];
-#pragma unroll
-                    for (int k = 0; k < CN; k++) acc[k] += w5[u] * L.hs[jl][q * CN + k];
-                }
-                L.m1[j][e0] = (uint16_t)macc;
-#pragma unroll
-                for (int k = 0; k < CN; k++) L.g1[j][e0 * CN + k] = acc[k];
-            }
-            __syncthreads();
-            for (int i = tid; i < kMbN1 * kMbN2 * HS; i += nt) {
-                const int jl = i / (kMbN1 * kMbN2), e0 = i % (kMbN1 * kMbN2), j = jg + jl;
-                if (j >= ns) break;
-                const int r = e0 / kMbN2, e = e0 % kMbN2;
-                int acc[CN], macc = 0;
-#pragma unroll
-                for (int k = 0; k < CN; k++) acc[k] = 0;
-#pragma unroll
-                for (int v = 0; v < 5; v++) {
-                    const int q = r * kMbN1 + 2 * e + v;
-                    macc += w5[v] * L.m1[j][q];
-#pragma unroll
-                    for (int k = 0; k < CN; k++) acc[k] += w5[v] * L.g1[j][q * CN + k];
-                }
-                L.hm2[jl][e0] = macc;
-#pragma unroll
-                for (int k = 0; k < CN; k++) L.hs2[jl][e0 * CN + k] = acc[k];
-            }
-            __syncthreads();
-            for (int i = tid; i < kMbN2 * kMbN2 * HS; i += nt) {
-                const int jl = i / (kMbN2 * kMbN2), e0 = i % (kMbN2 * kMbN2), j = jg + jl;
-                if (j >= ns) break;
-                const int ey = e0 / kMbN2, ex = e0 % kMbN2;
-                int acc[CN], macc = 0;
-#pragma unroll
-                for (int k = 0; k < CN; k++) acc[k] = 0;
-#pragma unroll
-                for (int u = 0; u < 5; u++) {
-                    const int q = (2 * ey + u) * kMbN2 + ex;
-                    macc += w5[u] * L.hm2[jl][q];
-#pragma unroll
-                    for (int k = 0; k < CN; k++) acc[k] += w5[u] * L.hs2[jl][q * CN + k];
-                }
-                L.m2[j][e0] = macc;
-#pragma unroll
-                for (int k = 0; k < CN; k++) L.g2[j][e0 * CN + k] = acc[k];
-            }
-            __syncthreads();
-        }
-    } else {
-        // 2. level 1: g1 = reduce(g0), m1 = reduce(owner == slot)
-        for (int i = tid; i < kMbN1 * kMbN1 * S; i += nt) {
-            const int j = i / (kMbN1 * kMbN1), e = i % (kMbN1 * kMbN1);
-            if (j >= ns) break;
-            const int qx = refl(G.X1 + e % kMbN1, G.w1), qy = refl(G.Y1 + e / kMbN1, G.h1);
-            int macc = 0, acc[CN];
-#pragma unroll
-            for (int k = 0; k < CN; k++) acc[k] = 0;
-#pragma unroll
-            for (int u = 0; u < 5; u++) {
-                const int cy = refl(2 * qy + u - 2, G.H);
-#pragma unroll
-                for (int v = 0; v < 5; v++) {
-                    const int cx = refl(2 * qx + v - 2, G.W), wt = w5[u] * w5[v];
-                    const int p = i0(cx, cy);
-                    macc += L.own[p] == j ? wt : 0;
-#pragma unroll
-                    for (int k = 0; k < CN; k++) acc[k] += wt * L.g0[j][p * CN + k];
-                }
-            }
-            L.m1[j][e] = (uint16_t)macc;
-#pragma unroll
-            for (int k = 0; k < CN; k++) L.g1[j][e * CN + k] = acc[k];
-        }
-        __syncthreads();
-        // 3. level 2: g2 = reduce(g1), m2 = reduce(m1)
-        for (int i = tid; i < kMbN2 * kMbN2 * S; i += nt) {
-            const int j = i / (kMbN2 * kMbN2), e = i % (kMbN2 * kMbN2);
-            if (j >= ns) break;
-            const int zx = refl(G.X2 + e % kMbN2, G.w2), zy = refl(G.Y2 + e / kMbN2, G.h2);
-            int macc = 0, acc[CN];
-#pragma unroll
-            for (int k = 0; k < CN; k++) acc[k] = 0;
-#pragma unroll
-            for (int u = 0; u < 5; u++) {
-                const int qy = refl(2 * zy + u - 2, G.h1);
-#pragma unroll
-                for (int v = 0; v < 5; v++) {
-                    const int qx = refl(2 * zx + v - 2, G.w1), wt = w5[u] * w5[v];
-                    const int p = i1(qx, qy);
-                    macc += wt * L.m1[j][p];
-#pragma unroll
-                    for (int k = 0; k < CN; k++) acc[k] += wt * L.g1[j][p * CN + k];
-                }
-            }
-            L.m2[j][e] = macc;
-#pragma unroll
-            for (int k = 0; k < CN; k++) L.g2[j][e * CN + k] = acc[k];
-        }
-        __syncthreads();
-    }
-    // 4. B2 = sum m2 g2 / (sum m2 * 65536)
+    // B2 = sum m2 g2 / (sum m2 * 65536)
     for (int i = tid; i < kMbN2 * kMbN2 * CN; i += nt) {
         const int e = i / CN, k = i % CN;
-        int64_t num = 0, den = 0;
-        for (int j = 0; j < ns; j++) {
-            num += (int64_t)L.m2[j][e] * L.g2[j][e * CN + k];
-            den += L.m2[j][e];
-        }
+        int64_t num = 0;
+        for (int j = 0; j < ns; j++)
+            num += (int64_t)t_m2[j * kMbN2 * kMbN2 + e] * L.g2[j][e * CN + k];
+        const int den = t_d2[e];
         L.b2[i] = den ? (double)num / ((double)den * 65536.0) : 0.0;
     }
     __syncthreads();
-    // 5. R1 = B1 + up(B2), B1 = sum m1 (16384 g1 - E(g2)) / (sum m1 * 4194304)
+    // R1 = B1 + up(B2), B1 = sum m1 (16384 g1 - E(g2)) / (sum m1 * 4194304)
     for (int i = tid; i < kMbNR * kMbNR * CN; i += nt) {
         const int e = i / CN, k = i % CN;
         const int qx = rf<IN>(G.XR + e % kMbNR, G.w1), qy = rf<IN>(G.YR + e / kMbNR, G.h1);
         int iy[3], wy[3], ix[3], wx[3];
-        exp_taps(qy, G.h2, iy, wy);
-        exp_taps(qx, G.w2, ix, wx);
-        int64_t num = 0, den = 0;
-        const int p1 = i1(qx, qy);
+        exp_taps<IN>(qy, G.h2, iy, wy);
+        exp_taps<IN>(qx, G.w2, ix, wx);
+        int64_t num = 0;
+        const int p1 = ir(qx, qy);
         for (int j = 0; j < ns; j++) {
             int e2 = 0;   // <= 64 * 65536 * 255 < 2^31: exact in int32
 #pragma unroll
@@ -516,10 +719,10 @@ __device__ __forceinline__ void mb_phases(const KParams &P, const MbGeo &G, MbLd
 #pragma unroll
                 for (int v = 0; v < 3; v++)
                     e2 += wy[u] * wx[v] * L.g2[j][i2(ix[v], iy[u]) * CN + k];
-            const int l1 = 16384 * L.g1[j][p1 * CN + k] - e2;
-            num += (int64_t)L.m1[j][p1] * l1;
-            den += L.m1[j][p1];
+            const int l1 = 16384 * ch16(L.g1[j][p1], k) - e2;
+            num += (int64_t)t_m1[j * kMbNR * kMbNR + p1] * l1;
         }
+        const int den = t_d1[p1];
         const double b1 = den ? (double)num / ((double)den * 4194304.0) : 0.0;
         double acc = 0.0;
 #pragma unroll
@@ -530,21 +733,26 @@ __device__ __forceinline__ void mb_phases(const KParams &P, const MbGeo &G, MbLd
         L.r1[i] = b1 + acc / 64.0;
     }
     __syncthreads();
-    // 6. R0 = L0_owner / 16384 + up(R1) over the tile's own pixels
+    // R0 = L0_owner / 16384 + up(R1) over the tile's own pixels; L0 = 16384 g0 - E(g1), g0 = the
+    // owner sample already in the mosaic
     for (int i = tid; i < kBlendTile * kBlendTile; i += nt) {
         const int x = G.X0 + (i % kBlendTile), y = G.Y0 + i / kBlendTile;
         if (!IN && (x >= G.W || y >= G.H)) continue;
-        const int p0 = i0(x, y), s = L.own[p0];
-        uint8_t *o = P.out + (int64_t)f * P.out_fstride + (int64_t)y * P.out_pitch + x * CN;
-        if (s == kBlendNone) {
+        const int o = a.owner[(int64_t)y * G.W + x];
+        uint8_t *po = P.out + (int64_t)f * P.out_fstride + (int64_t)y * P.out_pitch + x * CN;
+        if (o == kBlendNone) {
 #pragma unroll
-            for (int k = 0; k < CN; k++) o[k] = 0;
+            for (int k = 0; k < CN; k++) po[k] = 0;
             continue;
         }
+        const int s = __popc(mask & ((1u << o) - 1u));
         int iy[3], wy[3], ix[3], wx[3];
-        exp_taps(y, G.h1, iy, wy);
-        exp_taps(x, G.w1, ix, wx);
+        exp_taps<IN>(y, G.h1, iy, wy);
+        exp_taps<IN>(x, G.w1, ix, wx);
+        uint32_t px = 0;
 #pragma unroll
+        for (int k = 0; k < CN; k++) px |= (uint32_t)po[k] << (8 * k);
+#pragma unroll 1
         for (int k = 0; k < CN; k++) {
             int e1 = 0;   // <= 64 * 256 * 255: exact in int32
             double acc = 0.0;
@@ -552,69 +760,35 @@ __device__ __forceinline__ void mb_phases(const KParams &P, const MbGeo &G, MbLd
             for (int u = 0; u < 3; u++)
 #pragma unroll
                 for (int v = 0; v < 3; v++) {
-                    e1 += wy[u] * wx[v] * L.g1[s][i1(ix[v], iy[u]) * CN + k];
-                    acc += (double)(wy[u] * wx[v]) * L.r1[ir(ix[v], iy[u]) * CN + k];
+                    const int p = ir(ix[v], iy[u]);
+                    e1 += wy[u] * wx[v] * ch16(L.g1[s][p], k);
+                    acc += (double)(wy[u] * wx[v]) * L.r1[p * CN + k];
                 }
-            const int l0 = 16384 * (int)L.g0[s][p0 * CN + k] - e1;
+            const int l0 = 16384 * (int)((px >> (8 * k)) & 0xffu) - e1;
             const double r0 = (double)l0 / 16384.0 + acc / 64.0;
             const double vf = floor(r0 + 0.5);
-            o[k] = (uint8_t)(vf < 0.0 ? 0.0 : (vf > 255.0 ? 255.0 : vf));
+            po[k] = (uint8_t)(vf < 0.0 ? 0.0 : (vf > 255.0 ? 255.0 : vf));
         }
     }
-    __syncthreads();   // the next capture overwrites the level arrays
 }
 
-template <int CN, int INTERP, int S>
-__device__ __forceinline__ void multiband_tile(const KBlendArgs &a, MbLds<CN, S> &L)
+template <int CN>
+__device__ __forceinline__ void mb_blend(const KMbArgs &a, MbBlLds<CN> &L)
 {
-    const KParams &P = a.P;
-    MbGeo G;
-    G.W = P.out_w;
-    G.H = P.out_h;
-    G.w1 = (G.W + 1) / 2, G.h1 = (G.H + 1) / 2, G.w2 = (G.w1 + 1) / 2, G.h2 = (G.h1 + 1) / 2;
-    const int gx = (G.W + kBlendTile - 1) / kBlendTile;
-    const int t = a.list[1 + 2 * blockIdx.x];
-    const uint32_t mask = (uint32_t)a.list[2 + 2 * blockIdx.x];
-    G.X0 = (t % gx) * kBlendTile, G.Y0 = (t / gx) * kBlendTile;
-    G.RX = G.X0 - kBlendHalo, G.RY = G.Y0 - kBlendHalo;         // level-0 origin
-    G.X1 = G.X0 / 2 - kMbO1, G.Y1 = G.Y0 / 2 - kMbO1;             // level-1 origin
-    G.X2 = G.X0 / 4 - kMbO2, G.Y2 = G.Y0 / 4 - kMbO2;             // level-2 origin
-    G.XR = G.X0 / 2 - kMbOR, G.YR = G.Y0 / 2 - kMbOR;             // R1 origin
-    const bool interior = G.RX >= 0 && G.RY >= 0 && G.RX + kMbR0 <= G.W && G.RY + kMbR0 <= G.H;
+    const int bt = blockIdx.x, fl = blockIdx.y, tid = threadIdx.x, nt = blockDim.x;
+    const uint32_t mask = (uint32_t)a.list[2 + 2 * bt];
     const int ns = __popc(mask);
-    const int tid = threadIdx.x, nt = blockDim.x;
-    // owner map of the used neighbourhood as local slot indices (bit rank in `mask`)
-    for (int i = tid; i < kMbUsed * kMbUsed; i += nt) {
-        const int cx = refl(G.RX + kMbFirst + i % kMbUsed, G.W);
-        const int cy = refl(G.RY + kMbFirst + i / kMbUsed, G.H);
-        const int o = a.owner[(int64_t)cy * G.W + cx];
-        L.own[i] = (uint8_t)((o != kBlendNone && ((mask >> o) & 1u))
-                                 ? __popc(mask & ((1u << o) - 1u)) : kBlendNone);
+    const MbGeo G = mb_geo(a.P, a.list[1 + 2 * bt]);
+    for (int j = 0; j < ns; j++) {
+        const int64_t job = ((int64_t)bt * a.slots + j) * a.chunk + fl;
+        const uint2 *s1 = reinterpret_cast<const uint2 *>(a.g1) + job * (kMbNR * kMbNR);
+        const int32_t *s2 = a.g2 + job * (kMbN2 * kMbN2 * CN);
+        for (int i = tid; i < kMbNR * kMbNR; i += nt) L.g1[j][i] = s1[i];
+        for (int i = tid; i < kMbN2 * kMbN2 * CN; i += nt) L.g2[j][i] = s2[i];
     }
-    const int f1 = min(a.n_frames, (int)(blockIdx.y + 1) * kMbFrames);
-    for (int f = blockIdx.y * kMbFrames; f < f1; f++) {
-        // 1. the owners' warped images over the used neighbourhood, capture f
-        uint32_t mrem = mask;
-        for (int j = 0; j < ns; j++) {
-            const int s = __ffs(mrem) - 1;
-            mrem &= mrem - 1;
-            int cam, w, h;
-            slot_info(P, s, cam, w, h);
-            const uint8_t *fb = P.cams[cam] + (int64_t)f * P.cam_fstride[cam];
-            for (int i = tid; i < kMbUsed * kMbUsed; i += nt) {
-                const int cx = refl(G.RX + kMbFirst + i % kMbUsed, G.W);
-                const int cy = refl(G.RY + kMbFirst + i / kMbUsed, G.H);
-                int x32, y32, c_, w_, h_;
-                slot_xy<INTERP>(P, s, cx, cy, x32, y32, c_, w_, h_);
-                const uint32_t v = sample_replicate<CN>(fb, w, h, x32, y32);
-#pragma unroll
-                for (int k = 0; k < CN; k++) L.g0[j][i * CN + k] = (uint8_t)(v >> (8 * k));
-            }
-        }
-        __syncthreads();
-        if (interior) mb_phases<CN, S, true>(P, G, L, ns, f);
-        else mb_phases<CN, S, false>(P, G, L, ns, f);
-    }
+    __syncthreads();
+    if (G.interior) mb_blend_tile<CN, true>(a, G, L, mask, ns, a.f0 + fl);
+    else mb_blend_tile<CN, false>(a, G, L, mask, ns, a.f0 + fl);
 }
 
 }  // namespace mcs

@@ -40,6 +40,12 @@ struct mcs_plan {
     uint8_t *d_owner = nullptr;
     uint32_t *d_binfo = nullptr;
     int *d_blist = nullptr;
+    // multi-band: per (tile, owner) sample windows, per-tile masks, level scratch per chunk
+    uint64_t *d_mbdesc = nullptr;
+    int32_t *d_mbtab = nullptr;
+    uint16_t *d_mbg1 = nullptr;
+    int32_t *d_mbg2 = nullptr;
+    int mb_chunk = 0;
     // cylindrical plans: per-column (sin, cos) and per-row h, host copy and device table
     bool cyl = false;
     std::vector<double> cyl_tab;
@@ -73,7 +79,9 @@ struct Kernels {
     hipFunction_t blend_classify = nullptr;
     hipFunction_t seam_sample[5][2] = {};  // [channels][interp]
     hipFunction_t feather[5][2] = {};     // [channels][interp]
-    hipFunction_t multiband[5][2][2] = {};   // [channels][interp][<= 2 owners : <= 4]
+    hipFunction_t mb_prep[5][2] = {};     // [channels][interp]
+    hipFunction_t mb_levels[5] = {};      // [channels]
+    hipFunction_t mb_blend[5] = {};       // [channels]
 };
 Kernels g_k[kMaxDevices];
 std::mutex g_k_mu;
@@ -95,15 +103,17 @@ int kernels(const Api *A, int device, const Kernels **out)
             rc = fn(name, &k.stream[c]);
             snprintf(name, sizeof(name), "mcs_resize_c%d", c);
             if (rc == MCS_OK) rc = fn(name, &k.resize[c]);
+            snprintf(name, sizeof(name), "mcs_mb_levels_c%d", c);
+            if (rc == MCS_OK) rc = fn(name, &k.mb_levels[c]);
+            snprintf(name, sizeof(name), "mcs_mb_blend_c%d", c);
+            if (rc == MCS_OK) rc = fn(name, &k.mb_blend[c]);
             for (int i = 0; i < 2 && rc == MCS_OK; i++) {
                 snprintf(name, sizeof(name), "mcs_prepare_c%d_i%d", c, i);
                 rc = fn(name, &k.prepare[c][i]);
                 snprintf(name, sizeof(name), "mcs_feather_c%d_i%d", c, i);
                 if (rc == MCS_OK) rc = fn(name, &k.feather[c][i]);
-                snprintf(name, sizeof(name), "mcs_multiband_c%d_i%d_s2", c, i);
-                if (rc == MCS_OK) rc = fn(name, &k.multiband[c][i][0]);
-                snprintf(name, sizeof(name), "mcs_multiband_c%d_i%d_s4", c, i);
-                if (rc == MCS_OK) rc = fn(name, &k.multiband[c][i][1]);
+                snprintf(name, sizeof(name), "mcs_mb_prep_c%d_i%d", c, i);
+                if (rc == MCS_OK) rc = fn(name, &k.mb_prep[c][i]);
                 snprintf(name, sizeof(name), "mcs_seam_sample_c%d_i%d", c, i);
                 if (rc == MCS_OK) rc = fn(name, &k.seam_sample[c][i]);
                 for (int o = 0; o < 2 && rc == MCS_OK; o++) {
@@ -182,6 +192,51 @@ int launch_args(const Api *A, hipFunction_t f, unsigned gx, unsigned gy, unsigne
     return MCS_OK;
 }
 
+void mb_args(const mcs_plan *p, const mcs::KParams &P, mcs::KMbArgs &a)
+{
+    a.P = P;
+    a.owner = p->d_owner;
+    a.list = p->d_blist;
+    a.desc = p->d_mbdesc;
+    a.tab = p->d_mbtab;
+    a.g1 = p->d_mbg1;
+    a.g2 = p->d_mbg2;
+    a.slots = p->mb_slots;
+    a.chunk = p->mb_chunk;
+    a.f0 = 0;
+    a.nf = 0;
+}
+
+// Multi-band: per (tile, owner) level-0 sample windows and per-tile masks (once), and the level
+// scratch for chunks of mb_chunk captures (budget kMbScratchBytes).
+int prepare_multiband(const Api *A, mcs_plan *p, const Kernels *k, hipStream_t s)
+{
+    const int n = p->n_blend, S = p->mb_slots, C = p->fd.channels;
+    const mcs::KParams &P = p->kp;
+    for (int c = 0; c <= P.n_stages; c++) {
+        const int64_t w = c == 0 ? P.cam0_w : P.st[c - 1].src_w;
+        const int64_t h = c == 0 ? P.cam0_h : P.st[c - 1].src_h;
+        if (w * h * C >= (int64_t(1) << 31))
+            return mcs::fail(MCS_E_UNSUPPORTED, "multi-band: camera frames must be < 2 GiB");
+    }
+    const int64_t per_f = (int64_t)n * S * (mcs::kMbNRPx * mcs::kMbNRPx * 8 +
+                                            mcs::kMbN2Px * mcs::kMbN2Px * C * 4);
+    int chunk = (int)std::max<int64_t>(1, std::min<int64_t>(64, mcs::kMbScratchBytes / per_f));
+    if (chunk > mcs::kMbLvFrames) chunk -= chunk % mcs::kMbLvFrames;
+    const int64_t samples = (int64_t)mcs::kMbUsedPx * mcs::kMbUsedPx;
+    HIP_TRY(A->hipMalloc((void **)&p->d_mbdesc, (size_t)(n * S * samples) * sizeof(uint64_t)));
+    HIP_TRY(A->hipMalloc((void **)&p->d_mbtab, (size_t)n * mcs::mb_tab_words(S) * sizeof(int32_t)));
+    HIP_TRY(A->hipMalloc((void **)&p->d_mbg1,
+                         (size_t)n * S * chunk * mcs::kMbNRPx * mcs::kMbNRPx * 8));
+    HIP_TRY(A->hipMalloc((void **)&p->d_mbg2,
+                         (size_t)n * S * chunk * mcs::kMbN2Px * mcs::kMbN2Px * C * 4));
+    p->mb_chunk = chunk;
+    mcs::KMbArgs a;
+    mb_args(p, p->kp, a);
+    return launch_args(A, k->mb_prep[C][p->fd.interp], (unsigned)n, 1, mcs::kMbPrepThreads, 1,
+                       &a, sizeof(a), s);
+}
+
 // Blended modes: the owner map and the list of 32-px tiles the blend kernels recompute.
 int prepare_blend(const Api *A, mcs_plan *p, const Kernels *k, hipStream_t s)
 {
@@ -216,6 +271,7 @@ int prepare_blend(const Api *A, mcs_plan *p, const Kernels *k, hipStream_t s)
         return mcs::fail(MCS_E_UNSUPPORTED, "multi-band: %d tiles have more than %d cameras "
                          "meeting within %d px", overflow, mcs::kBlendSlots, mcs::kBlendHalo);
     p->n_blend = n;
+    if (p->blend == MCS_BLEND_MULTIBAND && n > 0) return prepare_multiband(A, p, k, s);
     return MCS_OK;
 }
 
@@ -225,8 +281,15 @@ void release_tables(const Api *A, mcs_plan *p)
     if (p->stream) (void)A->hipStreamSynchronize(p->stream);
     if (p->side) (void)A->hipStreamSynchronize(p->side);
     for (void *q : {(void *)p->d_tiles, (void *)p->d_desc, (void *)p->d_fallback,
-                    (void *)p->d_owner, (void *)p->d_binfo, (void *)p->d_blist})
+                    (void *)p->d_owner, (void *)p->d_binfo, (void *)p->d_blist,
+                    (void *)p->d_mbdesc, (void *)p->d_mbtab, (void *)p->d_mbg1,
+                    (void *)p->d_mbg2})
         if (q) (void)A->hipFree(q);
+    p->d_mbdesc = nullptr;
+    p->d_mbtab = nullptr;
+    p->d_mbg1 = nullptr;
+    p->d_mbg2 = nullptr;
+    p->mb_chunk = 0;
     p->d_tiles = nullptr;
     p->d_desc = nullptr;
     p->d_fallback = nullptr;
@@ -353,12 +416,26 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
         if (p->blend == MCS_BLEND_FEATHER)
             rc = launch_args(A, k->feather[p->fd.channels][p->fd.interp], p->n_blend, n_frames,
                              256, 1, &b, sizeof(b), s);
-        else
-        {
-            const bool two = p->mb_slots <= 2;
-            rc = launch_args(A, k->multiband[p->fd.channels][p->fd.interp][two ? 0 : 1],
-                             p->n_blend, (n_frames + mcs::kMbFrames - 1) / mcs::kMbFrames,
-                             two ? mcs::kMbThreads2 : mcs::kMbThreads4, 1, &b, sizeof(b), s);
+        else {
+            // multi-band: levels then blend, per chunk of captures (scratch stride mb_chunk)
+            mcs::KMbArgs m;
+            mb_args(p, P, m);
+            const int C = p->fd.channels;
+            rc = MCS_OK;
+            for (int f0 = 0; f0 < n_frames && rc == MCS_OK; f0 += p->mb_chunk) {
+                m.f0 = f0;
+                m.nf = std::min(p->mb_chunk, n_frames - f0);
+                const unsigned gz = (unsigned)((m.nf + mcs::kMbLvFrames - 1) / mcs::kMbLvFrames);
+                void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, (void *)&m,
+                               HIP_LAUNCH_PARAM_BUFFER_SIZE, nullptr, HIP_LAUNCH_PARAM_END};
+                size_t sz = sizeof(m);
+                cfg[3] = &sz;
+                HIP_TRY(A->hipModuleLaunchKernel(k->mb_levels[C], (unsigned)p->n_blend,
+                                                 (unsigned)p->mb_slots, gz, mcs::kMbLvThreads, 1,
+                                                 1, 0, s, nullptr, cfg));
+                rc = launch_args(A, k->mb_blend[C], (unsigned)p->n_blend, (unsigned)m.nf,
+                                 mcs::kMbBlThreads, 1, &m, sizeof(m), s);
+            }
         }
         if (rc) return rc;
     }
@@ -674,6 +751,10 @@ int mcs_plan_destroy(mcs_plan *p)
             if (p->d_owner) (void)A->hipFree(p->d_owner);
             if (p->d_binfo) (void)A->hipFree(p->d_binfo);
             if (p->d_blist) (void)A->hipFree(p->d_blist);
+            if (p->d_mbdesc) (void)A->hipFree(p->d_mbdesc);
+            if (p->d_mbtab) (void)A->hipFree(p->d_mbtab);
+            if (p->d_mbg1) (void)A->hipFree(p->d_mbg1);
+            if (p->d_mbg2) (void)A->hipFree(p->d_mbg2);
             if (p->d_cyl) (void)A->hipFree(p->d_cyl);
             if (p->d_seam) (void)A->hipFree(p->d_seam);
             if (p->d_map) (void)A->hipFree(p->d_map);

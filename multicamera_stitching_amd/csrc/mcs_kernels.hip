@@ -175,6 +175,20 @@ __device__ __forceinline__ int owner(const KParams &P, int x, int y)
     return sel;
 }
 
+// Channel k of a pixel from its two row windows: v_perm_b32 + 2 x v_dot2_u32_u16.
+template <int CN>
+__device__ __forceinline__ uint32_t blend(uint2 r0, uint2 r1, uint32_t w0, uint32_t w1, int k)
+{
+    typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+    const uint32_t sel = (uint32_t)k | (0x0cu << 8) | ((uint32_t)(CN + k) << 16) | (0x0cu << 24);
+    const uint32_t a0 = __builtin_amdgcn_perm(r0.y, r0.x, sel);
+    const uint32_t a1 = __builtin_amdgcn_perm(r1.y, r1.x, sel);
+    uint32_t s = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, a0), __builtin_bit_cast(us2, w0),
+                                        16384u, false);
+    s = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, a1), __builtin_bit_cast(us2, w1), s, false);
+    return s >> 15;
+}
+
 }  // namespace mcs
 
 #include "mcs_blend.h"
@@ -350,20 +364,6 @@ __device__ __forceinline__ Desc<OFF32> describe(const KParams &P, int x, int y)
     d.w1 = g.w1;
     d.shift = (uint32_t)sh0 | ((uint32_t)sh1 << 4);
     return d;
-}
-
-// Channel k of a pixel from its two row windows: v_perm_b32 + 2 x v_dot2_u32_u16.
-template <int CN>
-__device__ __forceinline__ uint32_t blend(uint2 r0, uint2 r1, uint32_t w0, uint32_t w1, int k)
-{
-    typedef unsigned short us2 __attribute__((ext_vector_type(2)));
-    const uint32_t sel = (uint32_t)k | (0x0cu << 8) | ((uint32_t)(CN + k) << 16) | (0x0cu << 24);
-    const uint32_t a0 = __builtin_amdgcn_perm(r0.y, r0.x, sel);
-    const uint32_t a1 = __builtin_amdgcn_perm(r1.y, r1.x, sel);
-    uint32_t s = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, a0), __builtin_bit_cast(us2, w0),
-                                        16384u, false);
-    s = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, a1), __builtin_bit_cast(us2, w1), s, false);
-    return s >> 15;
 }
 
 __device__ __forceinline__ uint2 shr_bytes(uint2 v, uint32_t n)
@@ -959,18 +959,30 @@ extern "C" __global__ __launch_bounds__(256) void mcs_blend_classify(const mcs::
     {                                                                                          \
         mcs::feather_tile<CN, IN>(a);                                                          \
     }                                                                                          \
-    extern "C" __global__ __launch_bounds__(512) void mcs_multiband_c##CN##_i##IN##_s2(        \
-        const mcs::KBlendArgs a)                                                               \
+    extern "C" __global__ __launch_bounds__(256) void mcs_mb_prep_c##CN##_i##IN(               \
+        const mcs::KMbArgs a)                                                                  \
     {                                                                                          \
-        __shared__ mcs::MbLds<CN, 2> lds;                                                      \
-        mcs::multiband_tile<CN, IN, 2>(a, lds);                                                \
-    }                                                                                          \
-    extern "C" __global__ __launch_bounds__(1024) void mcs_multiband_c##CN##_i##IN##_s4(       \
-        const mcs::KBlendArgs a)                                                               \
-    {                                                                                          \
-        __shared__ mcs::MbLds<CN, 4> lds;                                                      \
-        mcs::multiband_tile<CN, IN, 4>(a, lds);                                                \
+        mcs::mb_prep<CN, IN>(a);                                                               \
     }
+#ifndef MCS_MB_WAVES
+#define MCS_MB_WAVES 4
+#endif
+#define MCS_MB_ENTRY(CN)                                                                       \
+    extern "C" __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(MCS_MB_WAVES))) \
+    void mcs_mb_levels_c##CN(const mcs::KMbArgs a)                                             \
+    {                                                                                          \
+        __shared__ mcs::MbLvLds<CN> lds;                                                       \
+        mcs::mb_levels<CN>(a, lds);                                                            \
+    }                                                                                          \
+    extern "C" __global__ __launch_bounds__(256) void mcs_mb_blend_c##CN(const mcs::KMbArgs a)  \
+    {                                                                                          \
+        __shared__ mcs::MbBlLds<CN> lds;                                                       \
+        mcs::mb_blend<CN>(a, lds);                                                             \
+    }
+MCS_MB_ENTRY(1)
+MCS_MB_ENTRY(2)
+MCS_MB_ENTRY(3)
+MCS_MB_ENTRY(4)
 MCS_BLEND_ENTRY(1, 0)
 MCS_BLEND_ENTRY(1, 1)
 MCS_BLEND_ENTRY(2, 0)

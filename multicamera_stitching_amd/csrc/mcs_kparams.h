@@ -136,9 +136,20 @@ constexpr int kBlendTile = 32;
 constexpr int kBlendHalo = 16;
 constexpr int kBlendSlots = 4;
 constexpr int kBlendNone = 255;
-constexpr int kMbThreads2 = 512;   // multi-band block, <= 2 owners per tile (2 blocks per CU)
-constexpr int kMbThreads4 = 1024;  // multi-band block, 3-4 owners per tile
-constexpr int kMbFrames = 4;       // captures per multi-band block (source maps reused)
+// multi-band kernels (mcs_blend.h): prep once per plan, then per chunk of captures levels + blend
+constexpr int kMbPrepThreads = 256;
+constexpr int kMbLvThreads = 512;
+constexpr int kMbLvFrames = 4;      // captures per levels block (sample windows held in registers)
+constexpr int kMbBlThreads = 256;
+constexpr int64_t kMbScratchBytes = 64ll << 20;   // level scratch budget per plan
+constexpr int kMbUsedPx = 57;       // level-0 neighbourhood side a tile's pyramid reads
+constexpr int kMbNRPx = 18;         // R1 region side (level 1)
+constexpr int kMbN2Px = 12;         // level-2 side
+// per-tile mask table (int32 words): m1 (R1 region) [slots], m2 [slots], d1 (R1 region), d2
+constexpr int mb_tab_words(int slots)
+{
+    return slots * (kMbNRPx * kMbNRPx + kMbN2Px * kMbN2Px) + kMbNRPx * kMbNRPx + kMbN2Px * kMbN2Px;
+}
 struct KBlendPrepArgs {
     KParams P;
     uint8_t *owner;
@@ -146,6 +157,18 @@ struct KBlendPrepArgs {
     int *list;
     int *overflow;
     int mode, pad_;
+};
+struct KMbArgs {
+    KParams P;
+    const uint8_t *owner;          // owner map of the mosaic
+    const int *list;               // blend tile list: list[1 + 2i] = tile, list[2 + 2i] = mask
+    uint64_t *desc;                // [tiles][slots][57 * 57] level-0 sample windows (prep)
+    int32_t *tab;                  // [tiles][mb_tab_words(slots)] masks + denominators (prep)
+    uint16_t *g1;                  // scratch [tiles][slots][chunk][18 * 18][4] (u16 lanes)
+    int32_t *g2;                   // scratch [tiles][slots][chunk][12 * 12 * CN]
+    int slots;                     // owners per tile (the tables' slot dimension)
+    int chunk;                     // scratch capture stride
+    int f0, nf;                    // captures [f0, f0 + nf) of this launch
 };
 struct KBlendArgs {
     KParams P;

@@ -3,7 +3,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/variants
-timeout -k 10 400 python -m pytest tests/test_gpu_blend.py -x -q > gpurun_out/pytest_gpu.log 2>&1 && \
+[ -n "$NO_TESTS" ] || timeout -k 10 400 python -u -m pytest tests/test_gpu_blend.py tests/test_gpu_cylinder.py -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 && \
 timeout -k 10 200 python bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/variants/main.log 2>&1 && \
 for v in build/variants/*.so; do
   [ -e "$v" ] || continue
