@@ -288,6 +288,7 @@ constexpr int kMbN2 = kMbN2Px, kMbO2 = 2;             // level 2: [X0/4 - 2, X0/
 constexpr int kMbNR = kMbNRPx, kMbOR = 1;             // R1:      [X0/2 - 1, X0/2 + 16]
 constexpr int kMbFirst = 2, kMbUsed = kMbUsedPx;      // level-0 offsets the pyramid reads
 constexpr int kMbU = kMbUsed * kMbUsed;               // level-0 samples per owner
+constexpr int kMbFoot = 24576;                         // bytes of one LDS footprint buffer
 constexpr int kMbRS = kMbO1 - kMbOR;                  // R1 region origin in the level-1 array (5)
 
 // Expand taps of fine index x into a coarse level of size n (IN: no reflection needed).
@@ -338,30 +339,56 @@ __device__ __forceinline__ int ix2(int c, int o, int n)
     return IN ? c - o : min(max(c - o, 0), n - 1);
 }
 
-// Replicate-border bilinear sample of slot s at output (x, y) (sample_replicate) as an 8-byte
-// window descriptor: off = byte offset of tap row a in the frame (bit 31: tap row b is the next
-// row, else the same row); meta = fx | fy << 5 | (left tap on byte CN) << 10 | (right tap on
-// byte CN) << 11 | d << 12, where d = bytes both windows start earlier so that row b's window
-// ends inside the frame (the taps then sit at bytes d and d + CN).  Every capture's load is then
-// unconditional.  Frames with (h - 1) * w * CN < 16 bytes take load8's guarded path instead.
-template <int CN, int INTERP>
-__device__ __forceinline__ uint2 mb_desc(const KParams &P, int s, int x, int y)
+// Replicate-border bilinear sample of slot s at output (x, y) (sample_replicate): tap rows ya,
+// yb, left tap column c (the window's first pixel), meta = fx | fy << 5 | (left tap on the
+// window's pixel 1) << 10 | (right tap on pixel 1) << 11.
+struct MbSrc {
+    int ya, yb, c;
+    uint32_t meta;
+};
+
+template <int INTERP>
+__device__ __forceinline__ MbSrc mb_src(const KParams &P, int s, int x, int y)
 {
     int x32, y32, cam, w, h;
     slot_xy<INTERP>(P, s, x, y, x32, y32, cam, w, h);
     const int sx = x32 >> 5, sy = y32 >> 5;
-    const int c = w >= 2 ? min(max(sx, 0), w - 2) : 0;
-    const uint32_t a_hi = min(max(sx, 0), w - 1) > c;
-    const uint32_t b_hi = min(max(sx + 1, 0), w - 1) > c;
-    const int ya = min(max(sy, 0), h - 1), yb = min(max(sy + 1, 0), h - 1);
-    const int64_t pitch = (int64_t)w * CN, fbytes = pitch * h;
-    const int64_t oa = ya * pitch + (int64_t)c * CN, ob = oa + (yb > ya ? pitch : 0);
-    const uint32_t d = (uint32_t)min(max(ob + 8 - fbytes, (int64_t)0), (int64_t)7);
-    uint2 r;
-    r.x = (uint32_t)oa | (yb > ya ? 0x80000000u : 0u);
-    r.y = (uint32_t)(x32 & 31) | ((uint32_t)(y32 & 31) << 5) | (a_hi << 10) | (b_hi << 11) |
-          (d << 12);
+    MbSrc r;
+    r.c = w >= 2 ? min(max(sx, 0), w - 2) : 0;
+    const uint32_t a_hi = min(max(sx, 0), w - 1) > r.c;
+    const uint32_t b_hi = min(max(sx + 1, 0), w - 1) > r.c;
+    r.ya = min(max(sy, 0), h - 1);
+    r.yb = min(max(sy + 1, 0), h - 1);
+    r.meta = (uint32_t)(x32 & 31) | ((uint32_t)(y32 & 31) << 5) | (a_hi << 10) | (b_hi << 11);
     return r;
+}
+
+// Global-memory window descriptor of a sample (frame of w x h x CN): .x = byte offset of tap row
+// a in the frame (bit 31: tap row b is the next row, else the same row); .y = meta | d << 12,
+// where d = bytes both windows start earlier so that row b's window ends inside the frame (the
+// taps then sit at bytes d and d + CN).  Every capture's load is then unconditional.  Frames
+// with (h - 1) * w * CN < 16 bytes take load8's guarded path instead.
+template <int CN>
+__device__ __forceinline__ uint2 mb_desc(const MbSrc &q, int w, int h)
+{
+    const int64_t pitch = (int64_t)w * CN, fbytes = pitch * h;
+    const int64_t oa = q.ya * pitch + (int64_t)q.c * CN, ob = oa + (q.yb > q.ya ? pitch : 0);
+    const uint32_t d = (uint32_t)min(max(ob + 8 - fbytes, (int64_t)0), (int64_t)7);
+    return make_uint2((uint32_t)oa | (q.yb > q.ya ? 0x80000000u : 0u), q.meta | (d << 12));
+}
+
+// Source footprint of one (tile, owner) staged in LDS per capture (mb_levels): rows
+// [rmin, rmin + rows), bytes [cal, cal + stride) of each (cal 16-byte aligned, stride a multiple
+// of 16), rows `stride` bytes apart in LDS.  The frame's last row is fetched `e` bytes earlier so
+// that no 16-byte chunk crosses the frame end.  A sample's LDS descriptor: .x = LDS offsets of
+// its two tap-row windows (16 bits each), .y = meta.
+struct MbFoot {
+    int rmin, rows, cal, stride, e, fits, pad0, pad1;
+};
+
+__device__ __forceinline__ uint32_t mb_foot_off(const MbFoot &F, int row, int byte, int h)
+{
+    return (uint32_t)((row - F.rmin) * F.stride + byte - F.cal + (row == h - 1 ? F.e : 0));
 }
 
 // The descriptor's 15-bit weights folded onto the taps' window bytes as u16 pairs (row a,
@@ -392,6 +419,20 @@ __device__ __forceinline__ uint32_t mb_tap(uint2 r0, uint2 r1, uint32_t wa, uint
     return v >> 15;
 }
 
+// Makes a register array opaque to the optimiser (one asm per capture): values derived from it
+// are then recomputed per capture instead of being hoisted out of the capture loop and held.
+template <int N>
+__device__ __forceinline__ void mb_opaque(uint32_t (&v)[N])
+{
+#pragma unroll
+    for (int i = 0; i < N; i += 4) {
+        if (i + 3 < N) asm volatile("" : "+v"(v[i]), "+v"(v[i + 1]), "+v"(v[i + 2]), "+v"(v[i + 3]));
+        else if (i + 2 < N) asm volatile("" : "+v"(v[i]), "+v"(v[i + 1]), "+v"(v[i + 2]));
+        else if (i + 1 < N) asm volatile("" : "+v"(v[i]), "+v"(v[i + 1]));
+        else asm volatile("" : "+v"(v[i]));
+    }
+}
+
 // Local slot j (0 .. popc(mask) - 1) -> plan slot: the j-th set bit of mask.
 __device__ __forceinline__ int mb_slot(uint32_t mask, int j)
 {
@@ -420,15 +461,67 @@ __device__ __forceinline__ void mb_prep(const KMbArgs &a)
         own[i] = (uint8_t)((o != kBlendNone && ((mask >> o) & 1u))
                                ? __popc(mask & ((1u << o) - 1u)) : kBlendNone);
     }
-    // every owner's level-0 sample windows
+    // every owner's source footprint (bounding box of its taps) ...
+    __shared__ int f_rmin[kBlendSlots], f_rmax[kBlendSlots], f_bmin[kBlendSlots],
+        f_bmax[kBlendSlots];
+    __shared__ MbFoot foot[kBlendSlots];
+    if (tid < kBlendSlots) {
+        f_rmin[tid] = f_bmin[tid] = 0x7fffffff;
+        f_rmax[tid] = f_bmax[tid] = -1;
+    }
+    __syncthreads();
     for (int i = tid; i < kMbU * ns; i += nt) {
         const int j = i / kMbU, e = i % kMbU;
         const int cx = refl(G.RX + kMbFirst + e % kMbUsed, G.W);
         const int cy = refl(G.RY + kMbFirst + e / kMbUsed, G.H);
-        const uint2 v = mb_desc<CN, INTERP>(P, mb_slot(mask, j), cx, cy);
-        a.desc[((int64_t)bt * a.slots + j) * kMbU + e] = (uint64_t)v.x | ((uint64_t)v.y << 32);
+        const MbSrc q = mb_src<INTERP>(P, mb_slot(mask, j), cx, cy);
+        atomicMin(&f_rmin[j], q.ya);
+        atomicMax(&f_rmax[j], q.yb);
+        atomicMin(&f_bmin[j], q.c * CN);
+        atomicMax(&f_bmax[j], q.c * CN + 2 * CN);
     }
     __syncthreads();
+    if (tid < ns) {
+        int cam, w, h;
+        slot_info(P, mb_slot(mask, tid), cam, w, h);
+        const int64_t pitch = (int64_t)w * CN;
+        MbFoot F;
+        F.rmin = f_rmin[tid];
+        F.rows = f_rmax[tid] - f_rmin[tid] + 1;
+        F.cal = f_bmin[tid] & ~15;
+        F.stride = (f_bmax[tid] - F.cal + 15) & ~15;
+        F.e = 0;
+        // (rows above the last one may run into the next row, never past the frame)
+        F.fits = F.rows * F.stride + kLdsSlack <= kMbFoot && F.stride <= 16 * kWave &&
+                 F.cal + F.stride <= 2 * pitch;
+        if (f_rmax[tid] == h - 1 && F.cal + F.stride > pitch) {
+            F.e = (int)(F.cal + F.stride - pitch);
+            if ((int64_t)(h - 1) * pitch + F.cal - F.e < 0) F.fits = 0;
+        }
+        F.pad0 = F.pad1 = 0;
+        foot[tid] = F;
+        reinterpret_cast<MbFoot *>(a.foot)[(int64_t)bt * a.slots + tid] = F;
+    }
+    __syncthreads();
+    // ... and every level-0 sample's windows: LDS offsets in the footprint, or frame offsets
+    for (int i = tid; i < kMbU * ns; i += nt) {
+        const int j = i / kMbU, e = i % kMbU;
+        const int cx = refl(G.RX + kMbFirst + e % kMbUsed, G.W);
+        const int cy = refl(G.RY + kMbFirst + e / kMbUsed, G.H);
+        const int sj = mb_slot(mask, j);
+        const MbSrc q = mb_src<INTERP>(P, sj, cx, cy);
+        int cam, w, h;
+        slot_info(P, sj, cam, w, h);
+        const MbFoot &F = foot[j];
+        uint2 v;
+        if (F.fits) {
+            v.x = mb_foot_off(F, q.ya, q.c * CN, h) | (mb_foot_off(F, q.yb, q.c * CN, h) << 16);
+            v.y = q.meta;
+        } else {
+            v = mb_desc<CN>(q, w, h);
+        }
+        a.desc[((int64_t)bt * a.slots + j) * kMbU + e] = (uint64_t)v.x | ((uint64_t)v.y << 32);
+    }
     const int RX2 = G.RX + kMbFirst, RY2 = G.RY + kMbFirst;
     // m1 = reduce(owner == slot) over the level-1 array (25-tap form with reflection)
     for (int i = tid; i < kMbN1 * kMbN1 * ns; i += nt) {
@@ -490,6 +583,7 @@ __device__ __forceinline__ void mb_prep(const KMbArgs &a)
 // ---- levels: grid (listed tiles, slots, ceil(nf / kMbLvFrames)), block kMbLvThreads -------------
 template <int CN>
 struct MbLvLds {
+    uint8_t foot[2][kMbFoot] __attribute__((aligned(16)));   // source footprints (double buffer)
     uint32_t g0[kMbU];                 // level 0: channel k in byte k
     uint2 g1[kMbN1 * kMbN1];           // 256 G1 <= 65280 as u16 lanes: x = (c0, c2), y = (c1, c3)
     union {
@@ -516,43 +610,90 @@ __device__ __forceinline__ void mb_levels(const KMbArgs &a, MbLvLds<CN> &L)
     int cam, w, h;
     slot_info(P, mb_slot(mask, j), cam, w, h);
     const int64_t pitch = (int64_t)w * CN, fbytes = pitch * h;
+    const MbFoot F = reinterpret_cast<const MbFoot *>(a.foot)[(int64_t)bt * a.slots + j];
+    const bool staged = F.fits;                      // footprint through LDS (else global loads)
     const bool shifted = (h - 1) * pitch >= 16;
-    // this owner's sample windows, once for the block's captures (frames with
-    // (h - 1) * pitch < 16 bytes re-read them per capture and take load8's guarded path)
+    // this owner's sample windows, once for the block's captures (global path with frames of
+    // (h - 1) * pitch < 16 bytes: re-read per capture, load8's guarded path)
     uint32_t doff[KJ], dmeta[KJ];
     const uint64_t *dsc = a.desc + ((int64_t)bt * a.slots + j) * kMbU;
 #pragma unroll
     for (int kk = 0; kk < KJ; kk++) {
         const int i = tid + kk * NT;
-        const uint64_t v = (shifted && i < kMbU) ? dsc[i] : 0ull;
+        const uint64_t v = ((staged || shifted) && i < kMbU) ? dsc[i] : 0ull;
         doff[kk] = (uint32_t)v;
         dmeta[kk] = (uint32_t)(v >> 32);
     }
     const int w5[5] = {1, 4, 6, 4, 1};
     const int fl0 = blockIdx.z * kMbLvFrames, fl1 = min(a.nf, fl0 + kMbLvFrames);
+    // LDS-DMA of capture fl's footprint into buffer b: row r by wave r % 8, lane = 16-byte chunk
+    const int wave = __builtin_amdgcn_readfirstlane(tid / kWave), lane = tid % kWave;
+    auto stage = [&](int fl, int b) {
+        const uint8_t *fb = P.cams[cam] + (int64_t)(a.f0 + fl) * P.cam_fstride[cam];
+        for (int r = wave; r < F.rows; r += NT / kWave) {
+            const int row = F.rmin + r;
+            const uint8_t *src = fb + (int64_t)row * pitch + F.cal - (row == h - 1 ? F.e : 0);
+            if (lane < (F.stride >> 4))
+                __builtin_amdgcn_global_load_lds(src + 16 * lane,
+                                                 ((lds_u8 *)L.foot[b]) + r * F.stride, 16, 0, 0);
+        }
+    };
+    if (staged && fl0 < fl1) stage(fl0, 0);
     for (int fl = fl0; fl < fl1; fl++) {
         const uint8_t *fb = P.cams[cam] + (int64_t)(a.f0 + fl) * P.cam_fstride[cam];
         // level 0.  The descriptors are made opaque per capture so that the compiler does not
         // hoist their decoding out of the loop (which would hold ~5 registers per sample).
-        if (shifted) {
+        if (staged) {
+            // this capture's footprint has landed (every wave's DMA: wait + barrier); the next
+            // one streams in while this one is processed
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (fl + 1 < fl1) stage(fl + 1, (fl + 1 - fl0) & 1);
+            const uint8_t *buf = L.foot[(fl - fl0) & 1];
+            // all samples into registers first: a level-0 store between them would order the
+            // next sample's LDS reads behind it (the compiler cannot tell the arrays apart)
+            uint32_t px[KJ];
+            mb_opaque(doff);
+            mb_opaque(dmeta);
 #pragma unroll
             for (int kk = 0; kk < KJ; kk++) {
-                asm volatile("" : "+v"(doff[kk]), "+v"(dmeta[kk]));
+                const uint2 r0 = lds_window(buf, doff[kk] & 0xffffu);
+                const uint2 r1 = lds_window(buf, doff[kk] >> 16);
+                uint32_t wa, wb;
+                mb_weights(dmeta[kk], wa, wb);
+                px[kk] = 0;
+#pragma unroll
+                for (int k = 0; k < CN; k++) px[kk] |= mb_tap<CN>(r0, r1, wa, wb, k, 0u) << (8 * k);
+            }
+#pragma unroll
+            for (int kk = 0; kk < KJ; kk++)
+                if (tid + kk * NT < kMbU) L.g0[tid + kk * NT] = px[kk];
+        } else if (shifted) {
+            struct __attribute__((packed)) U2 {
+                uint32_t x, y;
+            };
+            typedef __attribute__((address_space(1))) const uint8_t gu8;
+            typedef __attribute__((address_space(1))) const U2 gu2;
+            const gu8 *gfb = (const gu8 *)fb;
+            uint32_t px[KJ];
+            mb_opaque(doff);
+            mb_opaque(dmeta);
+#pragma unroll
+            for (int kk = 0; kk < KJ; kk++) {
                 const uint32_t d = dmeta[kk] >> 12;
                 const uint32_t o = (doff[kk] & 0x7fffffffu) - d;
                 const uint32_t ob = o + ((doff[kk] >> 31) ? (uint32_t)pitch : 0u);
-                uint2 r0, r1;
-                __builtin_memcpy(&r0, fb + o, 8);
-                __builtin_memcpy(&r1, fb + ob, 8);
-                const int i = tid + kk * NT;
-                if (i < kMbU) {
-                    uint32_t wa, wb, px = 0;
-                    mb_weights(dmeta[kk], wa, wb);
+                const U2 ra = *(const gu2 *)(gfb + o), rb = *(const gu2 *)(gfb + ob);
+                const uint2 r0 = make_uint2(ra.x, ra.y), r1 = make_uint2(rb.x, rb.y);
+                uint32_t wa, wb;
+                mb_weights(dmeta[kk], wa, wb);
+                px[kk] = 0;
 #pragma unroll
-                    for (int k = 0; k < CN; k++) px |= mb_tap<CN>(r0, r1, wa, wb, k, d) << (8 * k);
-                    L.g0[i] = px;
-                }
+                for (int k = 0; k < CN; k++) px[kk] |= mb_tap<CN>(r0, r1, wa, wb, k, d) << (8 * k);
             }
+#pragma unroll
+            for (int kk = 0; kk < KJ; kk++)
+                if (tid + kk * NT < kMbU) L.g0[tid + kk * NT] = px[kk];
         } else {
             for (int i = tid; i < kMbU; i += NT) {
                 const uint64_t v = dsc[i];
@@ -574,29 +715,49 @@ __device__ __forceinline__ void mb_levels(const KMbArgs &a, MbLvLds<CN> &L)
             // separable 5-tap reduces, all channels at once in 16-bit lanes up to level 1 (the
             // sums stay below 2^16: exact), then per channel.  Level-1 entry e reads level-0
             // offsets 2e + [0, 5); level-2 entry z reads level-1 entries 2z + [0, 5).
-            for (int i = tid; i < kMbUsed * kMbN1; i += NT) {
-                const int r = i / kMbN1, e = i % kMbN1;
-                const uint32_t *g = &L.g0[r * kMbUsed + 2 * e];
-                uint32_t lo = 0, hi = 0;
+            // (each thread's items are computed before any is stored, so that their LDS reads
+            // are not ordered behind the stores)
+            {
+                constexpr int IT = (kMbUsed * kMbN1 + NT - 1) / NT;
+                uint2 res[IT];
 #pragma unroll
-                for (int v = 0; v < 5; v++) {
-                    const uint32_t t = g[v];
-                    lo += (uint32_t)w5[v] * (t & 0x00ff00ffu);
-                    hi += (uint32_t)w5[v] * ((t >> 8) & 0x00ff00ffu);
+                for (int q = 0; q < IT; q++) {
+                    const int i = min(tid + q * NT, kMbUsed * kMbN1 - 1);
+                    const int r = i / kMbN1, e = i % kMbN1;
+                    const uint32_t *g = &L.g0[r * kMbUsed + 2 * e];
+                    uint32_t lo = 0, hi = 0;
+#pragma unroll
+                    for (int v = 0; v < 5; v++) {
+                        const uint32_t t = g[v];
+                        lo += (uint32_t)w5[v] * (t & 0x00ff00ffu);
+                        hi += (uint32_t)w5[v] * ((t >> 8) & 0x00ff00ffu);
+                    }
+                    res[q] = make_uint2(lo, hi);
                 }
-                L.hs[i] = make_uint2(lo, hi);
+#pragma unroll
+                for (int q = 0; q < IT; q++)
+                    if (tid + q * NT < kMbUsed * kMbN1) L.hs[tid + q * NT] = res[q];
             }
             __syncthreads();
-            for (int i = tid; i < kMbN1 * kMbN1; i += NT) {
-                const int ey = i / kMbN1, ex = i % kMbN1;
-                uint32_t lo = 0, hi = 0;
+            {
+                constexpr int IT = (kMbN1 * kMbN1 + NT - 1) / NT;
+                uint2 res[IT];
 #pragma unroll
-                for (int u = 0; u < 5; u++) {
-                    const uint2 t = L.hs[(2 * ey + u) * kMbN1 + ex];
-                    lo += (uint32_t)w5[u] * t.x;
-                    hi += (uint32_t)w5[u] * t.y;
+                for (int q = 0; q < IT; q++) {
+                    const int i = min(tid + q * NT, kMbN1 * kMbN1 - 1);
+                    const int ey = i / kMbN1, ex = i % kMbN1;
+                    uint32_t lo = 0, hi = 0;
+#pragma unroll
+                    for (int u = 0; u < 5; u++) {
+                        const uint2 t = L.hs[(2 * ey + u) * kMbN1 + ex];
+                        lo += (uint32_t)w5[u] * t.x;
+                        hi += (uint32_t)w5[u] * t.y;
+                    }
+                    res[q] = make_uint2(lo, hi);
                 }
-                L.g1[i] = make_uint2(lo, hi);
+#pragma unroll
+                for (int q = 0; q < IT; q++)
+                    if (tid + q * NT < kMbN1 * kMbN1) L.g1[tid + q * NT] = res[q];
             }
             __syncthreads();
             for (int i = tid; i < kMbN1 * kMbN2; i += NT) {
@@ -694,43 +855,67 @@ __device__ __forceinline__ void mb_blend_tile(const KMbArgs &a, const MbGeo &G, 
         return ix2<IN>(cy, G.YR, kMbNR) * kMbNR + ix2<IN>(cx, G.XR, kMbNR);
     };
     // B2 = sum m2 g2 / (sum m2 * 65536)
-    for (int i = tid; i < kMbN2 * kMbN2 * CN; i += nt) {
-        const int e = i / CN, k = i % CN;
-        int64_t num = 0;
-        for (int j = 0; j < ns; j++)
-            num += (int64_t)t_m2[j * kMbN2 * kMbN2 + e] * L.g2[j][e * CN + k];
+    for (int e = tid; e < kMbN2 * kMbN2; e += nt) {
+        int64_t num[CN];
+#pragma unroll
+        for (int k = 0; k < CN; k++) num[k] = 0;
+        for (int j = 0; j < ns; j++) {
+            const int64_t m = t_m2[j * kMbN2 * kMbN2 + e];
+#pragma unroll
+            for (int k = 0; k < CN; k++) num[k] += m * L.g2[j][e * CN + k];
+        }
         const int den = t_d2[e];
-        L.b2[i] = den ? (double)num / ((double)den * 65536.0) : 0.0;
+#pragma unroll
+        for (int k = 0; k < CN; k++)
+            L.b2[e * CN + k] = den ? (double)num[k] / ((double)den * 65536.0) : 0.0;
     }
     __syncthreads();
     // R1 = B1 + up(B2), B1 = sum m1 (16384 g1 - E(g2)) / (sum m1 * 4194304)
-    for (int i = tid; i < kMbNR * kMbNR * CN; i += nt) {
-        const int e = i / CN, k = i % CN;
+    for (int e = tid; e < kMbNR * kMbNR; e += nt) {
         const int qx = rf<IN>(G.XR + e % kMbNR, G.w1), qy = rf<IN>(G.YR + e / kMbNR, G.h1);
         int iy[3], wy[3], ix[3], wx[3];
         exp_taps<IN>(qy, G.h2, iy, wy);
         exp_taps<IN>(qx, G.w2, ix, wx);
-        int64_t num = 0;
-        const int p1 = ir(qx, qy);
-        for (int j = 0; j < ns; j++) {
-            int e2 = 0;   // <= 64 * 65536 * 255 < 2^31: exact in int32
-#pragma unroll
-            for (int u = 0; u < 3; u++)
-#pragma unroll
-                for (int v = 0; v < 3; v++)
-                    e2 += wy[u] * wx[v] * L.g2[j][i2(ix[v], iy[u]) * CN + k];
-            const int l1 = 16384 * ch16(L.g1[j][p1], k) - e2;
-            num += (int64_t)t_m1[j * kMbNR * kMbNR + p1] * l1;
-        }
-        const int den = t_d1[p1];
-        const double b1 = den ? (double)num / ((double)den * 4194304.0) : 0.0;
-        double acc = 0.0;
+        int tp[9], tw[9];
 #pragma unroll
         for (int u = 0; u < 3; u++)
 #pragma unroll
-            for (int v = 0; v < 3; v++)
-                acc += (double)(wy[u] * wx[v]) * L.b2[i2(ix[v], iy[u]) * CN + k];
-        L.r1[i] = b1 + acc / 64.0;
+            for (int v = 0; v < 3; v++) {
+                tp[3 * u + v] = i2(ix[v], iy[u]) * CN;
+                tw[3 * u + v] = wy[u] * wx[v];
+            }
+        const int p1 = ir(qx, qy);
+        int64_t num[CN];
+#pragma unroll
+        for (int k = 0; k < CN; k++) num[k] = 0;
+        for (int j = 0; j < ns; j++) {
+            int e2[CN];   // <= 64 * 65536 * 255 < 2^31: exact in int32
+#pragma unroll
+            for (int k = 0; k < CN; k++) e2[k] = 0;
+#pragma unroll
+            for (int t = 0; t < 9; t++)
+#pragma unroll
+                for (int k = 0; k < CN; k++) e2[k] += tw[t] * L.g2[j][tp[t] + k];
+            const uint2 g1 = L.g1[j][p1];
+            const int64_t m = t_m1[j * kMbNR * kMbNR + p1];
+#pragma unroll
+            for (int k = 0; k < CN; k++) num[k] += m * (16384 * ch16(g1, k) - e2[k]);
+        }
+        const int den = t_d1[p1];
+        double acc[CN];
+#pragma unroll
+        for (int k = 0; k < CN; k++) acc[k] = 0.0;
+#pragma unroll
+        for (int t = 0; t < 9; t++) {
+            const double wt = (double)tw[t];
+#pragma unroll
+            for (int k = 0; k < CN; k++) acc[k] += wt * L.b2[tp[t] + k];
+        }
+#pragma unroll
+        for (int k = 0; k < CN; k++) {
+            const double b1 = den ? (double)num[k] / ((double)den * 4194304.0) : 0.0;
+            L.r1[e * CN + k] = b1 + acc[k] / 64.0;
+        }
     }
     __syncthreads();
     // R0 = L0_owner / 16384 + up(R1) over the tile's own pixels; L0 = 16384 g0 - E(g1), g0 = the
@@ -738,8 +923,11 @@ __device__ __forceinline__ void mb_blend_tile(const KMbArgs &a, const MbGeo &G, 
     for (int i = tid; i < kBlendTile * kBlendTile; i += nt) {
         const int x = G.X0 + (i % kBlendTile), y = G.Y0 + i / kBlendTile;
         if (!IN && (x >= G.W || y >= G.H)) continue;
-        const int o = a.owner[(int64_t)y * G.W + x];
-        uint8_t *po = P.out + (int64_t)f * P.out_fstride + (int64_t)y * P.out_pitch + x * CN;
+        // (global address space: the stores cannot alias the LDS arrays read by later pixels)
+        typedef __attribute__((address_space(1))) uint8_t gu8;
+        typedef __attribute__((address_space(1))) const uint8_t cgu8;
+        const int o = ((const cgu8 *)a.owner)[(int64_t)y * G.W + x];
+        gu8 *po = (gu8 *)(P.out + (int64_t)f * P.out_fstride + (int64_t)y * P.out_pitch + x * CN);
         if (o == kBlendNone) {
 #pragma unroll
             for (int k = 0; k < CN; k++) po[k] = 0;
@@ -749,23 +937,27 @@ __device__ __forceinline__ void mb_blend_tile(const KMbArgs &a, const MbGeo &G, 
         int iy[3], wy[3], ix[3], wx[3];
         exp_taps<IN>(y, G.h1, iy, wy);
         exp_taps<IN>(x, G.w1, ix, wx);
-        uint32_t px = 0;
+        int e1[CN];   // <= 64 * 256 * 255: exact in int32
+        double acc[CN];
 #pragma unroll
-        for (int k = 0; k < CN; k++) px |= (uint32_t)po[k] << (8 * k);
-#pragma unroll 1
-        for (int k = 0; k < CN; k++) {
-            int e1 = 0;   // <= 64 * 256 * 255: exact in int32
-            double acc = 0.0;
+        for (int k = 0; k < CN; k++) e1[k] = 0, acc[k] = 0.0;
 #pragma unroll
-            for (int u = 0; u < 3; u++)
+        for (int u = 0; u < 3; u++)
 #pragma unroll
-                for (int v = 0; v < 3; v++) {
-                    const int p = ir(ix[v], iy[u]);
-                    e1 += wy[u] * wx[v] * ch16(L.g1[s][p], k);
-                    acc += (double)(wy[u] * wx[v]) * L.r1[p * CN + k];
+            for (int v = 0; v < 3; v++) {
+                const int p = ir(ix[v], iy[u]), wt = wy[u] * wx[v];
+                const uint2 g1 = L.g1[s][p];
+                const double wd = (double)wt;
+#pragma unroll
+                for (int k = 0; k < CN; k++) {
+                    e1[k] += wt * ch16(g1, k);
+                    acc[k] += wd * L.r1[p * CN + k];
                 }
-            const int l0 = 16384 * (int)((px >> (8 * k)) & 0xffu) - e1;
-            const double r0 = (double)l0 / 16384.0 + acc / 64.0;
+            }
+#pragma unroll
+        for (int k = 0; k < CN; k++) {
+            const int l0 = 16384 * (int)po[k] - e1[k];
+            const double r0 = (double)l0 / 16384.0 + acc[k] / 64.0;
             const double vf = floor(r0 + 0.5);
             po[k] = (uint8_t)(vf < 0.0 ? 0.0 : (vf > 255.0 ? 255.0 : vf));
         }

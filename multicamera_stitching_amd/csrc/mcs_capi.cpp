@@ -43,6 +43,7 @@ struct mcs_plan {
     // multi-band: per (tile, owner) sample windows, per-tile masks, level scratch per chunk
     uint64_t *d_mbdesc = nullptr;
     int32_t *d_mbtab = nullptr;
+    int32_t *d_mbfoot = nullptr;
     uint16_t *d_mbg1 = nullptr;
     int32_t *d_mbg2 = nullptr;
     int mb_chunk = 0;
@@ -199,6 +200,7 @@ void mb_args(const mcs_plan *p, const mcs::KParams &P, mcs::KMbArgs &a)
     a.list = p->d_blist;
     a.desc = p->d_mbdesc;
     a.tab = p->d_mbtab;
+    a.foot = p->d_mbfoot;
     a.g1 = p->d_mbg1;
     a.g2 = p->d_mbg2;
     a.slots = p->mb_slots;
@@ -226,6 +228,7 @@ int prepare_multiband(const Api *A, mcs_plan *p, const Kernels *k, hipStream_t s
     const int64_t samples = (int64_t)mcs::kMbUsedPx * mcs::kMbUsedPx;
     HIP_TRY(A->hipMalloc((void **)&p->d_mbdesc, (size_t)(n * S * samples) * sizeof(uint64_t)));
     HIP_TRY(A->hipMalloc((void **)&p->d_mbtab, (size_t)n * mcs::mb_tab_words(S) * sizeof(int32_t)));
+    HIP_TRY(A->hipMalloc((void **)&p->d_mbfoot, (size_t)n * S * 8 * sizeof(int32_t)));
     HIP_TRY(A->hipMalloc((void **)&p->d_mbg1,
                          (size_t)n * S * chunk * mcs::kMbNRPx * mcs::kMbNRPx * 8));
     HIP_TRY(A->hipMalloc((void **)&p->d_mbg2,
@@ -282,11 +285,12 @@ void release_tables(const Api *A, mcs_plan *p)
     if (p->side) (void)A->hipStreamSynchronize(p->side);
     for (void *q : {(void *)p->d_tiles, (void *)p->d_desc, (void *)p->d_fallback,
                     (void *)p->d_owner, (void *)p->d_binfo, (void *)p->d_blist,
-                    (void *)p->d_mbdesc, (void *)p->d_mbtab, (void *)p->d_mbg1,
+                    (void *)p->d_mbdesc, (void *)p->d_mbtab, (void *)p->d_mbfoot, (void *)p->d_mbg1,
                     (void *)p->d_mbg2})
         if (q) (void)A->hipFree(q);
     p->d_mbdesc = nullptr;
     p->d_mbtab = nullptr;
+    p->d_mbfoot = nullptr;
     p->d_mbg1 = nullptr;
     p->d_mbg2 = nullptr;
     p->mb_chunk = 0;
@@ -753,6 +757,7 @@ int mcs_plan_destroy(mcs_plan *p)
             if (p->d_blist) (void)A->hipFree(p->d_blist);
             if (p->d_mbdesc) (void)A->hipFree(p->d_mbdesc);
             if (p->d_mbtab) (void)A->hipFree(p->d_mbtab);
+            if (p->d_mbfoot) (void)A->hipFree(p->d_mbfoot);
             if (p->d_mbg1) (void)A->hipFree(p->d_mbg1);
             if (p->d_mbg2) (void)A->hipFree(p->d_mbg2);
             if (p->d_cyl) (void)A->hipFree(p->d_cyl);

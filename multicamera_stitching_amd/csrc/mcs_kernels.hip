@@ -175,6 +175,21 @@ __device__ __forceinline__ int owner(const KParams &P, int x, int y)
     return sel;
 }
 
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+// 8 bytes of LDS starting at byte a (any alignment): three dword reads + v_alignbyte.
+__device__ __forceinline__ uint2 lds_window(const uint8_t *smem, uint32_t a)
+{
+    const lds_u32 *d = (const lds_u32 *)(((const lds_u8 *)smem) + (a & ~3u));
+    const uint32_t sh = a & 3u;
+    const uint32_t x0 = d[0], x1 = d[1], x2 = d[2];
+    uint2 r;
+    r.x = __builtin_amdgcn_alignbyte(x1, x0, sh);
+    r.y = __builtin_amdgcn_alignbyte(x2, x1, sh);
+    return r;
+}
+
 // Channel k of a pixel from its two row windows: v_perm_b32 + 2 x v_dot2_u32_u16.
 template <int CN>
 __device__ __forceinline__ uint32_t blend(uint2 r0, uint2 r1, uint32_t w0, uint32_t w1, int k)
@@ -447,8 +462,6 @@ __device__ __forceinline__ void tile_pixel(int bx, int by, int lane, int wave, i
     y = by * kTileH + wave * kRowsPerWave + lane / kLanesPerRow;
 }
 
-typedef __attribute__((address_space(3))) uint8_t lds_u8;
-typedef __attribute__((address_space(3))) uint32_t lds_u32;
 
 struct FootprintLds {
     int rmin[MCS_MAX_CAMS], rmax[MCS_MAX_CAMS], cmin[MCS_MAX_CAMS], cmax[MCS_MAX_CAMS];
@@ -560,17 +573,6 @@ __device__ __forceinline__ void prepare_tile(const KParams &P, TileHdr *tiles, u
 #pragma unroll
     for (int i = 0; i < kPx * kDescWords / 4; i++)
         o[i] = make_uint4(d[4 * i], d[4 * i + 1], d[4 * i + 2], d[4 * i + 3]);
-}
-
-__device__ __forceinline__ uint2 lds_window(const uint8_t *smem, uint32_t a)
-{
-    const lds_u32 *d = (const lds_u32 *)(((const lds_u8 *)smem) + (a & ~3u));
-    const uint32_t sh = a & 3u;
-    const uint32_t x0 = d[0], x1 = d[1], x2 = d[2];
-    uint2 r;
-    r.x = __builtin_amdgcn_alignbyte(x1, x0, sh);
-    r.y = __builtin_amdgcn_alignbyte(x2, x1, sh);
-    return r;
 }
 
 // Experiment knobs: cache policy of the footprint DMA (aux bits: 2 = nt) and of mosaic stores.

@@ -139,7 +139,7 @@ constexpr int kBlendNone = 255;
 // multi-band kernels (mcs_blend.h): prep once per plan, then per chunk of captures levels + blend
 constexpr int kMbPrepThreads = 256;
 constexpr int kMbLvThreads = 512;
-constexpr int kMbLvFrames = 4;      // captures per levels block (sample windows held in registers)
+constexpr int kMbLvFrames = 8;      // captures per levels block (sample windows held in registers)
 constexpr int kMbBlThreads = 256;
 constexpr int64_t kMbScratchBytes = 64ll << 20;   // level scratch budget per plan
 constexpr int kMbUsedPx = 57;       // level-0 neighbourhood side a tile's pyramid reads
@@ -164,6 +164,7 @@ struct KMbArgs {
     const int *list;               // blend tile list: list[1 + 2i] = tile, list[2 + 2i] = mask
     uint64_t *desc;                // [tiles][slots][57 * 57] level-0 sample windows (prep)
     int32_t *tab;                  // [tiles][mb_tab_words(slots)] masks + denominators (prep)
+    int32_t *foot;                 // [tiles][slots][8] source footprint per owner (prep)
     uint16_t *g1;                  // scratch [tiles][slots][chunk][18 * 18][4] (u16 lanes)
     int32_t *g2;                   // scratch [tiles][slots][chunk][12 * 12 * CN]
     int slots;                     // owners per tile (the tables' slot dimension)
