@@ -60,6 +60,8 @@ def parse():
     ap.add_argument("--gather", action="store_true",
                     help="after timing, gather one mosaic per rank onto rank 0 (RCCL)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-paste-ref", action="store_true",
+                    help="skip the paste-only reference launch (PMC passes: one plan's dispatches)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
     return ap.parse_args()
 
@@ -173,7 +175,7 @@ def main():
     # the same launch with the reference's paste (cylinder: the hard seam) and no blend pass:
     # the blend's share of the time
     paste_ms = None
-    if blend not in (_capi.MCS_BLEND_NONE, _capi.MCS_BLEND_SEAM):
+    if blend not in (_capi.MCS_BLEND_NONE, _capi.MCS_BLEND_SEAM) and not args.no_paste_ref:
         ref = make_plan()
         if cyl:
             ref.set_blend(_capi.MCS_BLEND_SEAM)
@@ -254,7 +256,7 @@ def main():
             "roofline": {
                 "bound": "hbm",
                 "kernel": "mcs_stream_c%d%s (one launch)" % (
-                    C, {"multiband": " + mcs_multiband_c%d_i1" % C,
+                    C, {"multiband": " + mcs_mb_levels_c%d + mcs_mb_blend_c%d" % (C, C),
                         "feather": " + mcs_feather_c%d_i1" % C, "none": "",
                         "seam": ""}[args.blend]),
                 "achieved": round(achieved, 1),

@@ -13,8 +13,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PMC = os.environ.get("MCS_PMC_DIR", os.path.join(ROOT, "gpurun_out", "pmc"))
 
 
-def family_counters(prefix):
-    """Per-dispatch averages of every counter over the dispatches of kernels named prefix*."""
+def family_counters(prefix, totals=False):
+    """Per-dispatch averages of every counter over the dispatches of kernels named prefix*
+    (totals=True: (sum over the dispatches, dispatches per pass))."""
     vals = defaultdict(lambda: defaultdict(float))     # (pass, dispatch) -> counter -> value
     for f in sorted(glob.glob(os.path.join(PMC, "pass*", "**", "*counter_collection.csv"),
                               recursive=True)):
@@ -24,9 +25,14 @@ def family_counters(prefix):
                 continue
             vals[(p, int(r["Dispatch_Id"]))][r["Counter_Name"]] += float(r["Counter_Value"])
     per_counter = defaultdict(list)
-    for cs in vals.values():
+    passes = defaultdict(int)
+    for (p, _), cs in vals.items():
+        passes[p] += 1
         for c, v in cs.items():
             per_counter[c].append(v)
+    if totals:
+        n = max(passes.values()) if passes else 0
+        return {c: sum(v) * n / max(len(v), 1) for c, v in per_counter.items()}, n
     return {c: sum(v) / len(v) for c, v in per_counter.items()}
 
 
@@ -54,16 +60,24 @@ def derived(avg):
 
 
 def main(prefixes=("mcs_stream_c3",), workload=None, out=None):
-    """One stitch launch = one dispatch of each kernel family in `prefixes`; HBM bytes per launch
-    = the families' per-dispatch FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE, summed."""
+    """Launches = the dispatches of the first family (one per stitch launch; the PMC runs use
+    bench.py --no-paste-ref so only the measured plan dispatches); HBM bytes per launch = every
+    family's FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE over its dispatches, / launches."""
     res = {"kernels": list(prefixes), "workload": workload, "per_kernel": {}}
     total = 0
+    launches = None
     for pre in prefixes:
         avg = family_counters(pre)
+        tot, n = family_counters(pre, totals=True)
+        if launches is None:
+            launches = max(n, 1)
         d = derived(avg)
         d["counters_per_dispatch"] = avg
+        d["dispatches_per_launch"] = n / launches
+        per_launch = derived({c: v / launches for c, v in tot.items()})
+        d["hbm_bytes_per_launch"] = per_launch.get("hbm_bytes")
         res["per_kernel"][pre] = d
-        total += d.get("hbm_bytes", 0)
+        total += per_launch.get("hbm_bytes", 0)
     res["hbm_bytes_per_launch"] = int(total) if total else None
     text = json.dumps(res, indent=1, sort_keys=True)
     print(text)
@@ -74,6 +88,7 @@ def main(prefixes=("mcs_stream_c3",), workload=None, out=None):
 
 if __name__ == "__main__":
     wl = sys.argv[1] if len(sys.argv) > 1 else "4x1920x1080x3-linear-super0-F64-multiband"
-    kernels = sys.argv[2].split(",") if len(sys.argv) > 2 else ["mcs_stream_c3", "mcs_multiband"]
+    kernels = (sys.argv[2].split(",") if len(sys.argv) > 2
+               else ["mcs_stream_c3", "mcs_mb_levels_c3", "mcs_mb_blend_c3"])
     out = sys.argv[3] if len(sys.argv) > 3 else os.path.join(ROOT, "profiles", "pmc_latest.json")
     main(prefixes=kernels, workload=wl, out=out)
