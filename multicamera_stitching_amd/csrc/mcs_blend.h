@@ -340,8 +340,9 @@ __device__ __forceinline__ int ix2(int c, int o, int n)
 }
 
 // Replicate-border bilinear sample of slot s at output (x, y) (sample_replicate): tap rows ya,
-// yb, left tap column c (the window's first pixel), meta = fx | fy << 5 | (left tap on the
-// window's pixel 1) << 10 | (right tap on pixel 1) << 11.
+// yb, the window's first pixel c, meta = fx' | fy << 6, where fx' is the horizontal fraction
+// with the replicate border folded in: both taps on the window's pixel 0 -> 0, both on pixel 1
+// -> 32 (the weights then sum onto one pixel, as the clamped taps do).
 struct MbSrc {
     int ya, yb, c;
     uint32_t meta;
@@ -355,11 +356,12 @@ __device__ __forceinline__ MbSrc mb_src(const KParams &P, int s, int x, int y)
     const int sx = x32 >> 5, sy = y32 >> 5;
     MbSrc r;
     r.c = w >= 2 ? min(max(sx, 0), w - 2) : 0;
-    const uint32_t a_hi = min(max(sx, 0), w - 1) > r.c;
-    const uint32_t b_hi = min(max(sx + 1, 0), w - 1) > r.c;
+    const bool a_hi = min(max(sx, 0), w - 1) > r.c;       // left tap on pixel 1
+    const bool b_hi = min(max(sx + 1, 0), w - 1) > r.c;   // right tap on pixel 1
+    const uint32_t fx = a_hi ? 32u : (b_hi ? (uint32_t)(x32 & 31) : 0u);
     r.ya = min(max(sy, 0), h - 1);
     r.yb = min(max(sy + 1, 0), h - 1);
-    r.meta = (uint32_t)(x32 & 31) | ((uint32_t)(y32 & 31) << 5) | (a_hi << 10) | (b_hi << 11);
+    r.meta = fx | ((uint32_t)(y32 & 31) << 6);
     return r;
 }
 
@@ -391,16 +393,15 @@ __device__ __forceinline__ uint32_t mb_foot_off(const MbFoot &F, int row, int by
     return (uint32_t)((row - F.rmin) * F.stride + byte - F.cal + (row == h - 1 ? F.e : 0));
 }
 
-// The descriptor's 15-bit weights folded onto the taps' window bytes as u16 pairs (row a,
-// row b), so that mb_tap() gives sample_replicate's (sum p w + 2^14) >> 15 exactly.
+// The descriptor's 15-bit weights as u16 pairs on the window's pixels 0 / 1, row a and row b:
+// (32 - fx', fx') * 32 (32 - fy) and * 32 fy (each lane <= 32768: no carry between lanes), so
+// that mb_tap() gives sample_replicate's (sum p w + 2^14) >> 15 exactly.
 __device__ __forceinline__ void mb_weights(uint32_t meta, uint32_t &wa, uint32_t &wb)
 {
-    const uint32_t fx = meta & 31u, fy = (meta >> 5) & 31u;
-    const uint32_t w00 = (32 - fx) * (32 - fy) * 32, w01 = fx * (32 - fy) * 32;
-    const uint32_t w10 = (32 - fx) * fy * 32, w11 = fx * fy * 32;
-    const uint32_t sa = (meta & 1024u) ? 16u : 0u, sb = (meta & 2048u) ? 16u : 0u;
-    wa = (w00 << sa) + (w01 << sb);
-    wb = (w10 << sa) + (w11 << sb);
+    const uint32_t fx = meta & 63u, fy = (meta >> 6) & 31u;
+    const uint32_t wx = (32u - fx) | (fx << 16);
+    wa = wx * ((32u - fy) << 5);
+    wb = wx * (fy << 5);
 }
 
 // Channel k of a descriptor's sample from its two (shifted) row windows.
@@ -839,9 +840,16 @@ struct MbBlLds {
     double r1[kMbNR * kMbNR * CN];
 };
 
+constexpr int kMbPQ = kBlendTile * kBlendTile / kMbBlThreads;   // tile pixels per thread
+template <int CN>
+struct MbPix {
+    int own[kMbPQ];          // owner slot of each of the thread's pixels (kBlendNone: none)
+    uint32_t v[kMbPQ];       // its owner sample (the stitch kernel's output), channel k in byte k
+};
+
 template <int CN, bool IN>
 __device__ __forceinline__ void mb_blend_tile(const KMbArgs &a, const MbGeo &G, MbBlLds<CN> &L,
-                                              uint32_t mask, int ns, int f)
+                                              const MbPix<CN> &px, uint32_t mask, int ns, int f)
 {
     const KParams &P = a.P;
     const int tid = threadIdx.x, nt = blockDim.x;
@@ -920,14 +928,15 @@ __device__ __forceinline__ void mb_blend_tile(const KMbArgs &a, const MbGeo &G, 
     __syncthreads();
     // R0 = L0_owner / 16384 + up(R1) over the tile's own pixels; L0 = 16384 g0 - E(g1), g0 = the
     // owner sample already in the mosaic
-    for (int i = tid; i < kBlendTile * kBlendTile; i += nt) {
+#pragma unroll
+    for (int q = 0; q < kMbPQ; q++) {
+        const int i = tid + q * kMbBlThreads;
         const int x = G.X0 + (i % kBlendTile), y = G.Y0 + i / kBlendTile;
         if (!IN && (x >= G.W || y >= G.H)) continue;
         // (global address space: the stores cannot alias the LDS arrays read by later pixels)
         typedef __attribute__((address_space(1))) uint8_t gu8;
-        typedef __attribute__((address_space(1))) const uint8_t cgu8;
-        const int o = ((const cgu8 *)a.owner)[(int64_t)y * G.W + x];
         gu8 *po = (gu8 *)(P.out + (int64_t)f * P.out_fstride + (int64_t)y * P.out_pitch + x * CN);
+        const int o = px.own[q];
         if (o == kBlendNone) {
 #pragma unroll
             for (int k = 0; k < CN; k++) po[k] = 0;
@@ -956,7 +965,7 @@ __device__ __forceinline__ void mb_blend_tile(const KMbArgs &a, const MbGeo &G, 
             }
 #pragma unroll
         for (int k = 0; k < CN; k++) {
-            const int l0 = 16384 * (int)po[k] - e1[k];
+            const int l0 = 16384 * (int)((px.v[q] >> (8 * k)) & 0xffu) - e1[k];
             const double r0 = (double)l0 / 16384.0 + acc[k] / 64.0;
             const double vf = floor(r0 + 0.5);
             po[k] = (uint8_t)(vf < 0.0 ? 0.0 : (vf > 255.0 ? 255.0 : vf));
@@ -967,20 +976,62 @@ __device__ __forceinline__ void mb_blend_tile(const KMbArgs &a, const MbGeo &G, 
 template <int CN>
 __device__ __forceinline__ void mb_blend(const KMbArgs &a, MbBlLds<CN> &L)
 {
-    const int bt = blockIdx.x, fl = blockIdx.y, tid = threadIdx.x, nt = blockDim.x;
+    typedef __attribute__((address_space(1))) const uint8_t cgu8;
+    typedef __attribute__((address_space(1))) const uint2 cgu2;
+    typedef __attribute__((address_space(1))) const int32_t cgi32;
+    const KParams &P = a.P;
+    const int bt = blockIdx.x, fl = blockIdx.y, tid = threadIdx.x;
     const uint32_t mask = (uint32_t)a.list[2 + 2 * bt];
-    const int ns = __popc(mask);
-    const MbGeo G = mb_geo(a.P, a.list[1 + 2 * bt]);
-    for (int j = 0; j < ns; j++) {
+    const int ns = __popc(mask), f = a.f0 + fl;
+    const MbGeo G = mb_geo(P, a.list[1 + 2 * bt]);
+    // every global read of the block issued up front (one memory round trip): the tile pixels'
+    // owners and owner samples, and the owners' level scratch
+    MbPix<CN> px;
+#pragma unroll
+    for (int q = 0; q < kMbPQ; q++) {
+        const int i = tid + q * kMbBlThreads;
+        const int x = G.X0 + (i % kBlendTile), y = G.Y0 + i / kBlendTile;
+        px.own[q] = kBlendNone;
+        px.v[q] = 0;
+        if (x < G.W && y < G.H) {
+            px.own[q] = ((cgu8 *)a.owner)[(int64_t)y * G.W + x];
+            const cgu8 *po = (const cgu8 *)(P.out + (int64_t)f * P.out_fstride +
+                                            (int64_t)y * P.out_pitch + x * CN);
+#pragma unroll
+            for (int k = 0; k < CN; k++) px.v[q] |= (uint32_t)po[k] << (8 * k);
+        }
+    }
+    constexpr int N1 = (kMbNR * kMbNR + kMbBlThreads - 1) / kMbBlThreads;
+    constexpr int N2 = (kMbN2 * kMbN2 * CN + kMbBlThreads - 1) / kMbBlThreads;
+    uint2 r1[kBlendSlots][N1];
+    int32_t r2[kBlendSlots][N2];
+#pragma unroll
+    for (int j = 0; j < kBlendSlots; j++) {
+        if (j >= ns) break;
         const int64_t job = ((int64_t)bt * a.slots + j) * a.chunk + fl;
-        const uint2 *s1 = reinterpret_cast<const uint2 *>(a.g1) + job * (kMbNR * kMbNR);
-        const int32_t *s2 = a.g2 + job * (kMbN2 * kMbN2 * CN);
-        for (int i = tid; i < kMbNR * kMbNR; i += nt) L.g1[j][i] = s1[i];
-        for (int i = tid; i < kMbN2 * kMbN2 * CN; i += nt) L.g2[j][i] = s2[i];
+        const cgu2 *s1 = (const cgu2 *)a.g1 + job * (kMbNR * kMbNR);
+        const cgi32 *s2 = (const cgi32 *)a.g2 + job * (kMbN2 * kMbN2 * CN);
+#pragma unroll
+        for (int q = 0; q < N1; q++)
+            r1[j][q] = s1[min(tid + q * kMbBlThreads, kMbNR * kMbNR - 1)];
+#pragma unroll
+        for (int q = 0; q < N2; q++)
+            r2[j][q] = s2[min(tid + q * kMbBlThreads, kMbN2 * kMbN2 * CN - 1)];
+    }
+#pragma unroll
+    for (int j = 0; j < kBlendSlots; j++) {
+        if (j >= ns) break;
+#pragma unroll
+        for (int q = 0; q < N1; q++)
+            if (tid + q * kMbBlThreads < kMbNR * kMbNR) L.g1[j][tid + q * kMbBlThreads] = r1[j][q];
+#pragma unroll
+        for (int q = 0; q < N2; q++)
+            if (tid + q * kMbBlThreads < kMbN2 * kMbN2 * CN)
+                L.g2[j][tid + q * kMbBlThreads] = r2[j][q];
     }
     __syncthreads();
-    if (G.interior) mb_blend_tile<CN, true>(a, G, L, mask, ns, a.f0 + fl);
-    else mb_blend_tile<CN, false>(a, G, L, mask, ns, a.f0 + fl);
+    if (G.interior) mb_blend_tile<CN, true>(a, G, L, px, mask, ns, f);
+    else mb_blend_tile<CN, false>(a, G, L, px, mask, ns, f);
 }
 
 }  // namespace mcs

@@ -368,13 +368,38 @@ int prepare(const Api *A, mcs_plan *p, hipStream_t s)
 
 // One launch pair (stream over all tiles + direct over the fallback tiles) for n_frames captures
 // that share one frame stride.
+// Multi-band level pyramids of captures [f0, f0 + nf) on stream s.
+int launch_mb_levels(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KMbArgs &m, int f0,
+                     int nf, hipStream_t s)
+{
+    m.f0 = f0;
+    m.nf = nf;
+    const unsigned gz = (unsigned)((nf + mcs::kMbLvFrames - 1) / mcs::kMbLvFrames);
+    size_t sz = sizeof(m);
+    void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, (void *)&m, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz,
+                   HIP_LAUNCH_PARAM_END};
+    HIP_TRY(A->hipModuleLaunchKernel(k->mb_levels[p->fd.channels], (unsigned)p->n_blend,
+                                     (unsigned)p->mb_slots, gz, mcs::kMbLvThreads, 1, 1, 0, s,
+                                     nullptr, cfg));
+    return MCS_OK;
+}
+
+// One launch (stream over all tiles, + direct over the fallback tiles, + the blend passes) for
+// n_frames captures that share one frame stride.  Work that does not read the mosaic -- the
+// direct-gather tiles and the first multi-band chunk's level pyramids -- runs on the side stream,
+// concurrently with the HBM-bound streaming kernel.
 int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams &P, int n_frames,
                 hipStream_t s)
 {
-    // the few direct-gather tiles run on the side stream, concurrently with the streaming kernel
-    if (p->n_fallback > 0) {
+    const bool mb = p->blend == MCS_BLEND_MULTIBAND && p->n_blend > 0;
+    const bool fork = p->n_fallback > 0 || mb;
+    mcs::KMbArgs m;
+    if (mb) mb_args(p, P, m);
+    if (fork) {
         HIP_TRY(A->hipEventRecord(p->ev_fork, s));
         HIP_TRY(A->hipStreamWaitEvent(p->side, p->ev_fork, 0));
+    }
+    if (p->n_fallback > 0) {
         mcs::KDirectArgs args;
         args.P = P;
         const bool off32 = offset_base(p, args.P, &args.P.base);
@@ -388,8 +413,12 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
         HIP_TRY(A->hipModuleLaunchKernel(k->direct[p->fd.channels][p->fd.interp][off32 ? 1 : 0],
                                          p->n_fallback, gy, 1, mcs::kWave, mcs::kWavesPerBlock, 1,
                                          0, p->side, nullptr, cfg));
-        HIP_TRY(A->hipEventRecord(p->ev_join, p->side));
     }
+    if (mb) {
+        const int rc = launch_mb_levels(A, p, k, m, 0, std::min(p->mb_chunk, n_frames), p->side);
+        if (rc) return rc;
+    }
+    if (fork) HIP_TRY(A->hipEventRecord(p->ev_join, p->side));
     {
         mcs::KStreamArgs args;
         args.P = P;
@@ -407,38 +436,30 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
                                          mcs::kWavesPerBlock, 1,
                                          mcs::lds_stream_bytes(p->fd.channels), s, nullptr, cfg));
     }
-    if (p->n_fallback > 0) HIP_TRY(A->hipStreamWaitEvent(s, p->ev_join, 0));
+    if (fork) HIP_TRY(A->hipStreamWaitEvent(s, p->ev_join, 0));
     if (p->n_blend > 0) {
         // recompute the blended tiles over the owner-sampled mosaic (same stream: ordered)
-        mcs::KBlendArgs b;
-        b.P = P;
-        b.owner = p->d_owner;
-        b.list = p->d_blist;
-        b.n_frames = n_frames;
-        b.pad_ = 0;
-        int rc;
-        if (p->blend == MCS_BLEND_FEATHER)
+        int rc = MCS_OK;
+        if (p->blend == MCS_BLEND_FEATHER) {
+            mcs::KBlendArgs b;
+            b.P = P;
+            b.owner = p->d_owner;
+            b.list = p->d_blist;
+            b.n_frames = n_frames;
+            b.pad_ = 0;
             rc = launch_args(A, k->feather[p->fd.channels][p->fd.interp], p->n_blend, n_frames,
                              256, 1, &b, sizeof(b), s);
-        else {
-            // multi-band: levels then blend, per chunk of captures (scratch stride mb_chunk)
-            mcs::KMbArgs m;
-            mb_args(p, P, m);
-            const int C = p->fd.channels;
-            rc = MCS_OK;
+        } else {
+            // multi-band: per chunk of captures (scratch stride mb_chunk) levels (chunk 0's
+            // already ran on the side stream) then blend
             for (int f0 = 0; f0 < n_frames && rc == MCS_OK; f0 += p->mb_chunk) {
+                const int nf = std::min(p->mb_chunk, n_frames - f0);
+                if (f0 > 0) rc = launch_mb_levels(A, p, k, m, f0, nf, s);
                 m.f0 = f0;
-                m.nf = std::min(p->mb_chunk, n_frames - f0);
-                const unsigned gz = (unsigned)((m.nf + mcs::kMbLvFrames - 1) / mcs::kMbLvFrames);
-                void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, (void *)&m,
-                               HIP_LAUNCH_PARAM_BUFFER_SIZE, nullptr, HIP_LAUNCH_PARAM_END};
-                size_t sz = sizeof(m);
-                cfg[3] = &sz;
-                HIP_TRY(A->hipModuleLaunchKernel(k->mb_levels[C], (unsigned)p->n_blend,
-                                                 (unsigned)p->mb_slots, gz, mcs::kMbLvThreads, 1,
-                                                 1, 0, s, nullptr, cfg));
-                rc = launch_args(A, k->mb_blend[C], (unsigned)p->n_blend, (unsigned)m.nf,
-                                 mcs::kMbBlThreads, 1, &m, sizeof(m), s);
+                m.nf = nf;
+                if (rc == MCS_OK)
+                    rc = launch_args(A, k->mb_blend[p->fd.channels], (unsigned)p->n_blend,
+                                     (unsigned)nf, mcs::kMbBlThreads, 1, &m, sizeof(m), s);
             }
         }
         if (rc) return rc;
@@ -446,10 +467,12 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
     return MCS_OK;
 }
 
-// Side stream + fork/join events for the direct-gather tiles (created once per plan).
+// Side stream + fork/join events for the direct-gather tiles and the multi-band levels (created
+// once per plan).
 int ensure_side(const Api *A, mcs_plan *p)
 {
-    if (p->n_fallback == 0 || p->side) return MCS_OK;
+    const bool mb = p->blend == MCS_BLEND_MULTIBAND && p->n_blend > 0;
+    if ((p->n_fallback == 0 && !mb) || p->side) return MCS_OK;
     HIP_TRY(A->hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming));
     HIP_TRY(A->hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming));
     HIP_TRY(A->hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking));

@@ -141,7 +141,7 @@ constexpr int kMbPrepThreads = 256;
 constexpr int kMbLvThreads = 512;
 constexpr int kMbLvFrames = 8;      // captures per levels block (sample windows held in registers)
 constexpr int kMbBlThreads = 256;
-constexpr int64_t kMbScratchBytes = 64ll << 20;   // level scratch budget per plan
+constexpr int64_t kMbScratchBytes = 1ll << 30;    // level scratch budget per plan (<= 64 captures)
 constexpr int kMbUsedPx = 57;       // level-0 neighbourhood side a tile's pyramid reads
 constexpr int kMbNRPx = 18;         // R1 region side (level 1)
 constexpr int kMbN2Px = 12;         // level-2 side
