@@ -434,6 +434,13 @@ __device__ __forceinline__ void mb_opaque(uint32_t (&v)[N])
     }
 }
 
+// e / D for 0 <= e < 2^16 / D (multiply-shift, exact in that range: D = 12, 18 here)
+template <int D>
+__device__ __forceinline__ int div_small(int e)
+{
+    return (int)(__umul24((unsigned)e, (65536u + D - 1) / D) >> 16);
+}
+
 // Local slot j (0 .. popc(mask) - 1) -> plan slot: the j-th set bit of mask.
 __device__ __forceinline__ int mb_slot(uint32_t mask, int j)
 {
@@ -785,7 +792,7 @@ __device__ __forceinline__ void mb_levels(const KMbArgs &a, MbLvLds<CN> &L)
                     acc[3] += w5[u] * t.w;
                 }
 #pragma unroll
-                for (int k = 0; k < CN; k++) og2[i * CN + k] = acc[k];
+                for (int k = 0; k < CN; k++) og2[k * (kMbN2 * kMbN2) + i] = acc[k];
             }
         } else {
             // mosaic-border tiles: 25-tap form with reflection at every level
@@ -821,7 +828,7 @@ __device__ __forceinline__ void mb_levels(const KMbArgs &a, MbLvLds<CN> &L)
                     }
                 }
 #pragma unroll
-                for (int k = 0; k < CN; k++) og2[e * CN + k] = acc[k];
+                for (int k = 0; k < CN; k++) og2[k * (kMbN2 * kMbN2) + e] = acc[k];
             }
         }
         // the R1 region of g1 (level-1 entries [kMbRS, kMbRS + 18) of the 27-entry array)
@@ -835,9 +842,9 @@ __device__ __forceinline__ void mb_levels(const KMbArgs &a, MbLvLds<CN> &L)
 template <int CN>
 struct MbBlLds {
     uint2 g1[kBlendSlots][kMbNR * kMbNR];   // packed as in mb_levels
-    int32_t g2[kBlendSlots][kMbN2 * kMbN2 * CN];
-    double b2[kMbN2 * kMbN2 * CN];
-    double r1[kMbNR * kMbNR * CN];
+    int32_t g2[kBlendSlots][CN][kMbN2 * kMbN2];   // channel-planar: indices need no * CN
+    double b2[CN][kMbN2 * kMbN2];
+    double r1[CN][kMbNR * kMbNR];
 };
 
 constexpr int kMbPQ = kBlendTile * kBlendTile / kMbBlThreads;   // tile pixels per thread
@@ -856,31 +863,34 @@ __device__ __forceinline__ void mb_blend_tile(const KMbArgs &a, const MbGeo &G, 
     const int32_t *tab = a.tab + (int64_t)blockIdx.x * mb_tab_words(a.slots);
     const int32_t *t_m1 = tab, *t_m2 = tab + a.slots * kMbNR * kMbNR;
     const int32_t *t_d1 = t_m2 + a.slots * kMbN2 * kMbN2, *t_d2 = t_d1 + kMbNR * kMbNR;
+    // (24-bit multiplies: full-rate v_mul_u32_u24 instead of quarter-rate v_mul_lo_u32)
     auto i2 = [&](int cx, int cy) {
-        return ix2<IN>(cy, G.Y2, kMbN2) * kMbN2 + ix2<IN>(cx, G.X2, kMbN2);
+        return (int)__umul24((unsigned)ix2<IN>(cy, G.Y2, kMbN2), kMbN2) + ix2<IN>(cx, G.X2, kMbN2);
     };
     auto ir = [&](int cx, int cy) {   // the R1 region (g1, m1, d1, r1)
-        return ix2<IN>(cy, G.YR, kMbNR) * kMbNR + ix2<IN>(cx, G.XR, kMbNR);
+        return (int)__umul24((unsigned)ix2<IN>(cy, G.YR, kMbNR), kMbNR) + ix2<IN>(cx, G.XR, kMbNR);
     };
     // B2 = sum m2 g2 / (sum m2 * 65536)
     for (int e = tid; e < kMbN2 * kMbN2; e += nt) {
-        int64_t num[CN];
+        // (integer sums in double: every product < 2^41, every sum < 2^43 -- exact)
+        double num[CN];
 #pragma unroll
-        for (int k = 0; k < CN; k++) num[k] = 0;
+        for (int k = 0; k < CN; k++) num[k] = 0.0;
         for (int j = 0; j < ns; j++) {
-            const int64_t m = t_m2[j * kMbN2 * kMbN2 + e];
+            const double m = (double)t_m2[__umul24((unsigned)j, kMbN2 * kMbN2) + e];
 #pragma unroll
-            for (int k = 0; k < CN; k++) num[k] += m * L.g2[j][e * CN + k];
+            for (int k = 0; k < CN; k++) num[k] += m * (double)L.g2[j][k][e];
         }
         const int den = t_d2[e];
 #pragma unroll
         for (int k = 0; k < CN; k++)
-            L.b2[e * CN + k] = den ? (double)num[k] / ((double)den * 65536.0) : 0.0;
+            L.b2[k][e] = den ? num[k] / ((double)den * 65536.0) : 0.0;
     }
     __syncthreads();
     // R1 = B1 + up(B2), B1 = sum m1 (16384 g1 - E(g2)) / (sum m1 * 4194304)
     for (int e = tid; e < kMbNR * kMbNR; e += nt) {
-        const int qx = rf<IN>(G.XR + e % kMbNR, G.w1), qy = rf<IN>(G.YR + e / kMbNR, G.h1);
+        const int ey = div_small<kMbNR>(e), ex = e - (int)__umul24((unsigned)ey, kMbNR);
+        const int qx = rf<IN>(G.XR + ex, G.w1), qy = rf<IN>(G.YR + ey, G.h1);
         int iy[3], wy[3], ix[3], wx[3];
         exp_taps<IN>(qy, G.h2, iy, wy);
         exp_taps<IN>(qx, G.w2, ix, wx);
@@ -889,13 +899,14 @@ __device__ __forceinline__ void mb_blend_tile(const KMbArgs &a, const MbGeo &G, 
         for (int u = 0; u < 3; u++)
 #pragma unroll
             for (int v = 0; v < 3; v++) {
-                tp[3 * u + v] = i2(ix[v], iy[u]) * CN;
+                tp[3 * u + v] = i2(ix[v], iy[u]);
                 tw[3 * u + v] = wy[u] * wx[v];
             }
         const int p1 = ir(qx, qy);
-        int64_t num[CN];
+        // (integer sums in double: every product < 2^39, every sum < 2^41 -- exact)
+        double num[CN];
 #pragma unroll
-        for (int k = 0; k < CN; k++) num[k] = 0;
+        for (int k = 0; k < CN; k++) num[k] = 0.0;
         for (int j = 0; j < ns; j++) {
             int e2[CN];   // <= 64 * 65536 * 255 < 2^31: exact in int32
 #pragma unroll
@@ -903,11 +914,12 @@ __device__ __forceinline__ void mb_blend_tile(const KMbArgs &a, const MbGeo &G, 
 #pragma unroll
             for (int t = 0; t < 9; t++)
 #pragma unroll
-                for (int k = 0; k < CN; k++) e2[k] += tw[t] * L.g2[j][tp[t] + k];
+                for (int k = 0; k < CN; k++)   // (tw <= 36, g2 < 2^24: a 24-bit multiply)
+                    e2[k] += (int)__umul24((unsigned)tw[t], (unsigned)L.g2[j][k][tp[t]]);
             const uint2 g1 = L.g1[j][p1];
-            const int64_t m = t_m1[j * kMbNR * kMbNR + p1];
+            const double m = (double)t_m1[__umul24((unsigned)j, kMbNR * kMbNR) + p1];
 #pragma unroll
-            for (int k = 0; k < CN; k++) num[k] += m * (16384 * ch16(g1, k) - e2[k]);
+            for (int k = 0; k < CN; k++) num[k] += m * (double)(16384 * ch16(g1, k) - e2[k]);
         }
         const int den = t_d1[p1];
         double acc[CN];
@@ -917,12 +929,12 @@ __device__ __forceinline__ void mb_blend_tile(const KMbArgs &a, const MbGeo &G, 
         for (int t = 0; t < 9; t++) {
             const double wt = (double)tw[t];
 #pragma unroll
-            for (int k = 0; k < CN; k++) acc[k] += wt * L.b2[tp[t] + k];
+            for (int k = 0; k < CN; k++) acc[k] += wt * L.b2[k][tp[t]];
         }
 #pragma unroll
         for (int k = 0; k < CN; k++) {
-            const double b1 = den ? (double)num[k] / ((double)den * 4194304.0) : 0.0;
-            L.r1[e * CN + k] = b1 + acc[k] / 64.0;
+            const double b1 = den ? num[k] / ((double)den * 4194304.0) : 0.0;
+            L.r1[k][e] = b1 + acc[k] / 64.0;
         }
     }
     __syncthreads();
@@ -960,7 +972,7 @@ __device__ __forceinline__ void mb_blend_tile(const KMbArgs &a, const MbGeo &G, 
 #pragma unroll
                 for (int k = 0; k < CN; k++) {
                     e1[k] += wt * ch16(g1, k);
-                    acc[k] += wd * L.r1[p * CN + k];
+                    acc[k] += wd * L.r1[k][p];
                 }
             }
 #pragma unroll
@@ -1027,7 +1039,7 @@ __device__ __forceinline__ void mb_blend(const KMbArgs &a, MbBlLds<CN> &L)
 #pragma unroll
         for (int q = 0; q < N2; q++)
             if (tid + q * kMbBlThreads < kMbN2 * kMbN2 * CN)
-                L.g2[j][tid + q * kMbBlThreads] = r2[j][q];
+                (&L.g2[j][0][0])[tid + q * kMbBlThreads] = r2[j][q];
     }
     __syncthreads();
     if (G.interior) mb_blend_tile<CN, true>(a, G, L, px, mask, ns, f);

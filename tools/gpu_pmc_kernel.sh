@@ -11,5 +11,5 @@ for c in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ
          "SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_INSTS_FLAT GRBM_GUI_ACTIVE" \
          "FETCH_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d "$R/gpurun_out/pmck/pass$i" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 --frames 16 --no-cpu-baseline "$@" > "$R/gpurun_out/pmck/pass$i.log" 2>&1 || exit $?
+  timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d "$R/gpurun_out/pmck/pass$i" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 --frames 64 --no-cpu-baseline --no-paste-ref "$@" > "$R/gpurun_out/pmck/pass$i.log" 2>&1 || exit $?
 done
