@@ -31,6 +31,9 @@ struct mcs_plan {
     // side stream for the direct-gather tiles, forked from / joined to the caller's stream
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    // second side stream: the multi-band level pyramids (concurrent with both of the above)
+    hipStream_t side2 = nullptr;
+    hipEvent_t ev_join2 = nullptr;
     // host path with frames off their calibrated size: upload buffers for the resize pre-pass
     uint8_t *d_raw[MCS_MAX_CAMS] = {};
     size_t raw_bytes[MCS_MAX_CAMS] = {};
@@ -283,6 +286,7 @@ void release_tables(const Api *A, mcs_plan *p)
 {
     if (p->stream) (void)A->hipStreamSynchronize(p->stream);
     if (p->side) (void)A->hipStreamSynchronize(p->side);
+    if (p->side2) (void)A->hipStreamSynchronize(p->side2);
     for (void *q : {(void *)p->d_tiles, (void *)p->d_desc, (void *)p->d_fallback,
                     (void *)p->d_owner, (void *)p->d_binfo, (void *)p->d_blist,
                     (void *)p->d_mbdesc, (void *)p->d_mbtab, (void *)p->d_mbfoot, (void *)p->d_mbg1,
@@ -386,7 +390,7 @@ int launch_mb_levels(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KMb
 
 // One launch (stream over all tiles, + direct over the fallback tiles, + the blend passes) for
 // n_frames captures that share one frame stride.  Work that does not read the mosaic -- the
-// direct-gather tiles and the first multi-band chunk's level pyramids -- runs on the side stream,
+// direct-gather tiles and the first multi-band chunk's level pyramids -- runs on two side streams,
 // concurrently with the HBM-bound streaming kernel.
 int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams &P, int n_frames,
                 hipStream_t s)
@@ -395,11 +399,9 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
     const bool fork = p->n_fallback > 0 || mb;
     mcs::KMbArgs m;
     if (mb) mb_args(p, P, m);
-    if (fork) {
-        HIP_TRY(A->hipEventRecord(p->ev_fork, s));
-        HIP_TRY(A->hipStreamWaitEvent(p->side, p->ev_fork, 0));
-    }
+    if (fork) HIP_TRY(A->hipEventRecord(p->ev_fork, s));
     if (p->n_fallback > 0) {
+        HIP_TRY(A->hipStreamWaitEvent(p->side, p->ev_fork, 0));
         mcs::KDirectArgs args;
         args.P = P;
         const bool off32 = offset_base(p, args.P, &args.P.base);
@@ -413,12 +415,14 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
         HIP_TRY(A->hipModuleLaunchKernel(k->direct[p->fd.channels][p->fd.interp][off32 ? 1 : 0],
                                          p->n_fallback, gy, 1, mcs::kWave, mcs::kWavesPerBlock, 1,
                                          0, p->side, nullptr, cfg));
+        HIP_TRY(A->hipEventRecord(p->ev_join, p->side));
     }
     if (mb) {
-        const int rc = launch_mb_levels(A, p, k, m, 0, std::min(p->mb_chunk, n_frames), p->side);
+        HIP_TRY(A->hipStreamWaitEvent(p->side2, p->ev_fork, 0));
+        const int rc = launch_mb_levels(A, p, k, m, 0, std::min(p->mb_chunk, n_frames), p->side2);
         if (rc) return rc;
+        HIP_TRY(A->hipEventRecord(p->ev_join2, p->side2));
     }
-    if (fork) HIP_TRY(A->hipEventRecord(p->ev_join, p->side));
     {
         mcs::KStreamArgs args;
         args.P = P;
@@ -436,7 +440,8 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
                                          mcs::kWavesPerBlock, 1,
                                          mcs::lds_stream_bytes(p->fd.channels), s, nullptr, cfg));
     }
-    if (fork) HIP_TRY(A->hipStreamWaitEvent(s, p->ev_join, 0));
+    if (p->n_fallback > 0) HIP_TRY(A->hipStreamWaitEvent(s, p->ev_join, 0));
+    if (mb) HIP_TRY(A->hipStreamWaitEvent(s, p->ev_join2, 0));
     if (p->n_blend > 0) {
         // recompute the blended tiles over the owner-sampled mosaic (same stream: ordered)
         int rc = MCS_OK;
@@ -467,15 +472,21 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
     return MCS_OK;
 }
 
-// Side stream + fork/join events for the direct-gather tiles and the multi-band levels (created
-// once per plan).
+// Side streams + fork/join events for the direct-gather tiles and the multi-band levels (created
+// once per plan, when needed).
 int ensure_side(const Api *A, mcs_plan *p)
 {
     const bool mb = p->blend == MCS_BLEND_MULTIBAND && p->n_blend > 0;
-    if ((p->n_fallback == 0 && !mb) || p->side) return MCS_OK;
-    HIP_TRY(A->hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming));
-    HIP_TRY(A->hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming));
-    HIP_TRY(A->hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking));
+    if ((p->n_fallback > 0 || mb) && !p->ev_fork)
+        HIP_TRY(A->hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming));
+    if (p->n_fallback > 0 && !p->side) {
+        HIP_TRY(A->hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming));
+        HIP_TRY(A->hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking));
+    }
+    if (mb && !p->side2) {
+        HIP_TRY(A->hipEventCreateWithFlags(&p->ev_join2, hipEventDisableTiming));
+        HIP_TRY(A->hipStreamCreateWithFlags(&p->side2, hipStreamNonBlocking));
+    }
     return MCS_OK;
 }
 
@@ -760,7 +771,7 @@ int mcs_undistort_map_host(const double *K, const double *dist, int n_dist, int 
 int mcs_plan_destroy(mcs_plan *p)
 {
     if (!p) return MCS_OK;
-    bool touched = p->stream || p->d_out || p->d_tiles || p->side;
+    bool touched = p->stream || p->d_out || p->d_tiles || p->side || p->side2;
     for (int i = 0; i < MCS_MAX_CAMS; i++) touched = touched || p->d_cams[i];
     if (touched) {
         const Api *A = mcs::rt::api();
@@ -787,10 +798,13 @@ int mcs_plan_destroy(mcs_plan *p)
             if (p->d_seam) (void)A->hipFree(p->d_seam);
             if (p->d_map) (void)A->hipFree(p->d_map);
             if (p->side) (void)A->hipStreamSynchronize(p->side);
+            if (p->side2) (void)A->hipStreamSynchronize(p->side2);
             if (p->stream) (void)A->hipStreamDestroy(p->stream);
             if (p->side) (void)A->hipStreamDestroy(p->side);
+            if (p->side2) (void)A->hipStreamDestroy(p->side2);
             if (p->ev_fork) (void)A->hipEventDestroy(p->ev_fork);
             if (p->ev_join) (void)A->hipEventDestroy(p->ev_join);
+            if (p->ev_join2) (void)A->hipEventDestroy(p->ev_join2);
         }
     }
     delete p;
