@@ -586,6 +586,57 @@ __device__ __forceinline__ void mb_prep(const KMbArgs &a)
         }
         t_d2[e] = d;
     }
+    // The blend work lists.  A pixel's collapse equals its owner's sample exactly (bit for bit)
+    // when no other owner's level-2 mask reaches a level-2 tap of its level-1 taps: B1 and B2 are
+    // then the owner's own l1 / 2^22 and g2 / 2^16 (one-term quotients of exact integers), R1 =
+    // g1 / 256 and R0 = g0 exactly (all dyadic, no rounding).  The stitch kernel has written that
+    // sample (or the border 0 where no camera covers the pixel), so the blend kernel computes only
+    // the other ("mixed") pixels and the R1 entries they read.
+    __shared__ int need_r1[kMbNR * kMbNR];
+    __shared__ int n_px, n_r1;
+    int32_t *t_cnt = t_d2 + kMbN2 * kMbN2;
+    uint16_t *t_px = reinterpret_cast<uint16_t *>(t_cnt + 2);
+    uint16_t *t_r1 = t_px + kBlendTile * kBlendTile;
+    for (int e = tid; e < kMbNR * kMbNR; e += nt) need_r1[e] = 0;
+    if (tid == 0) n_px = n_r1 = 0;
+    __syncthreads();
+    for (int i = tid; i < kBlendTile * kBlendTile; i += nt) {
+        const int x = G.X0 + i % kBlendTile, y = G.Y0 + i / kBlendTile;
+        if (x >= G.W || y >= G.H) continue;
+        const int o = a.owner[(int64_t)y * G.W + x];
+        if (o == kBlendNone) continue;
+        const int s = __popc(mask & ((1u << o) - 1u));
+        int iy[3], wy[3], ix[3], wx[3];
+        exp_taps<false>(y, G.h1, iy, wy);
+        exp_taps<false>(x, G.w1, ix, wx);
+        bool mixed = false;
+        for (int u = 0; u < 3; u++)
+            for (int v = 0; v < 3; v++) {
+                int zy[3], uy[3], zx[3], ux[3];
+                exp_taps<false>(iy[u], G.h2, zy, uy);
+                exp_taps<false>(ix[v], G.w2, zx, ux);
+                for (int b = 0; b < 3; b++)
+                    for (int c = 0; c < 3; c++) {
+                        const int e2 = ix2<false>(zy[b], G.Y2, kMbN2) * kMbN2 +
+                                       ix2<false>(zx[c], G.X2, kMbN2);
+                        for (int j = 0; j < ns; j++)
+                            mixed = mixed || (j != s && m2[j][e2] > 0);
+                    }
+            }
+        if (!mixed) continue;
+        t_px[atomicAdd(&n_px, 1)] = (uint16_t)i;
+        for (int u = 0; u < 3; u++)
+            for (int v = 0; v < 3; v++)
+                need_r1[ix2<false>(iy[u], G.YR, kMbNR) * kMbNR + ix2<false>(ix[v], G.XR, kMbNR)] = 1;
+    }
+    __syncthreads();
+    for (int e = tid; e < kMbNR * kMbNR; e += nt)
+        if (need_r1[e]) t_r1[atomicAdd(&n_r1, 1)] = (uint16_t)e;
+    __syncthreads();
+    if (tid == 0) {
+        t_cnt[0] = n_px;
+        t_cnt[1] = n_r1;
+    }
 }
 
 // ---- levels: grid (listed tiles, slots, ceil(nf / kMbLvFrames)), block kMbLvThreads -------------
@@ -850,6 +901,7 @@ struct MbBlLds {
 constexpr int kMbPQ = kBlendTile * kBlendTile / kMbBlThreads;   // tile pixels per thread
 template <int CN>
 struct MbPix {
+    int i[kMbPQ];            // the thread's mixed pixels (tile index, -1: none)
     int own[kMbPQ];          // owner slot of each of the thread's pixels (kBlendNone: none)
     uint32_t v[kMbPQ];       // its owner sample (the stitch kernel's output), channel k in byte k
 };
@@ -888,7 +940,11 @@ __device__ __forceinline__ void mb_blend_tile(const KMbArgs &a, const MbGeo &G, 
     }
     __syncthreads();
     // R1 = B1 + up(B2), B1 = sum m1 (16384 g1 - E(g2)) / (sum m1 * 4194304)
-    for (int e = tid; e < kMbNR * kMbNR; e += nt) {
+    const int n_r1 = t_d2[kMbN2 * kMbN2 + 1];
+    const uint16_t *t_r1 =
+        reinterpret_cast<const uint16_t *>(t_d2 + kMbN2 * kMbN2 + 2) + kBlendTile * kBlendTile;
+    for (int l = tid; l < n_r1; l += nt) {
+        const int e = t_r1[l];
         const int ey = div_small<kMbNR>(e), ex = e - (int)__umul24((unsigned)ey, kMbNR);
         const int qx = rf<IN>(G.XR + ex, G.w1), qy = rf<IN>(G.YR + ey, G.h1);
         int iy[3], wy[3], ix[3], wx[3];
@@ -942,9 +998,9 @@ __device__ __forceinline__ void mb_blend_tile(const KMbArgs &a, const MbGeo &G, 
     // owner sample already in the mosaic
 #pragma unroll
     for (int q = 0; q < kMbPQ; q++) {
-        const int i = tid + q * kMbBlThreads;
+        const int i = px.i[q];
+        if (i < 0) continue;
         const int x = G.X0 + (i % kBlendTile), y = G.Y0 + i / kBlendTile;
-        if (!IN && (x >= G.W || y >= G.H)) continue;
         // (global address space: the stores cannot alias the LDS arrays read by later pixels)
         typedef __attribute__((address_space(1))) uint8_t gu8;
         gu8 *po = (gu8 *)(P.out + (int64_t)f * P.out_fstride + (int64_t)y * P.out_pitch + x * CN);
@@ -999,13 +1055,26 @@ __device__ __forceinline__ void mb_blend(const KMbArgs &a, MbBlLds<CN> &L)
     // every global read of the block issued up front (one memory round trip): the tile pixels'
     // owners and owner samples, and the owners' level scratch
     MbPix<CN> px;
+    {
+        const cgi32 *tc = (const cgi32 *)a.tab + (int64_t)bt * mb_tab_words(a.slots) +
+                          a.slots * (kMbNR * kMbNR + kMbN2 * kMbN2) + kMbNR * kMbNR +
+                          kMbN2 * kMbN2;
+        typedef __attribute__((address_space(1))) const uint16_t cgu16;
+        const int n_px = tc[0];
+        const cgu16 *lp = (const cgu16 *)(tc + 2);
+#pragma unroll
+        for (int q = 0; q < kMbPQ; q++) {
+            const int l = tid + q * kMbBlThreads;
+            px.i[q] = l < n_px ? (int)lp[l] : -1;
+        }
+    }
 #pragma unroll
     for (int q = 0; q < kMbPQ; q++) {
-        const int i = tid + q * kMbBlThreads;
+        const int i = px.i[q];
         const int x = G.X0 + (i % kBlendTile), y = G.Y0 + i / kBlendTile;
         px.own[q] = kBlendNone;
         px.v[q] = 0;
-        if (x < G.W && y < G.H) {
+        if (i >= 0) {
             px.own[q] = ((cgu8 *)a.owner)[(int64_t)y * G.W + x];
             const cgu8 *po = (const cgu8 *)(P.out + (int64_t)f * P.out_fstride +
                                             (int64_t)y * P.out_pitch + x * CN);

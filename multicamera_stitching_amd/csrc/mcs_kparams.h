@@ -145,10 +145,14 @@ constexpr int64_t kMbScratchBytes = 1ll << 30;    // level scratch budget per pl
 constexpr int kMbUsedPx = 57;       // level-0 neighbourhood side a tile's pyramid reads
 constexpr int kMbNRPx = 18;         // R1 region side (level 1)
 constexpr int kMbN2Px = 12;         // level-2 side
-// per-tile mask table (int32 words): m1 (R1 region) [slots], m2 [slots], d1 (R1 region), d2
+// per-tile table (int32 words): m1 (R1 region) [slots], m2 [slots], d1 (R1 region), d2, then
+// the blend work lists: n_px, n_r1, the tile pixels to blend (u16, 1024 slots) and the R1
+// entries they read (u16, 18 * 18 slots)
+constexpr int kMbTabLists = 2 + 32 * 32 / 2 + kMbNRPx * kMbNRPx / 2;
 constexpr int mb_tab_words(int slots)
 {
-    return slots * (kMbNRPx * kMbNRPx + kMbN2Px * kMbN2Px) + kMbNRPx * kMbNRPx + kMbN2Px * kMbN2Px;
+    return slots * (kMbNRPx * kMbNRPx + kMbN2Px * kMbN2Px) + kMbNRPx * kMbNRPx + kMbN2Px * kMbN2Px +
+           kMbTabLists;
 }
 struct KBlendPrepArgs {
     KParams P;
