@@ -441,6 +441,13 @@ __device__ __forceinline__ int div_small(int e)
     return (int)(__umul24((unsigned)e, (65536u + D - 1) / D) >> 16);
 }
 
+// Sample e of a tile's compacted level-0 columns [a0, a0 + w0) -> its 57 x 57 array index.
+__device__ __forceinline__ int mb_sample_index(int e, int a0, int w0)
+{
+    const int r = e / w0;
+    return r * kMbUsed + a0 + (e - r * w0);
+}
+
 // Local slot j (0 .. popc(mask) - 1) -> plan slot: the j-th set bit of mask.
 __device__ __forceinline__ int mb_slot(uint32_t mask, int j)
 {
@@ -468,67 +475,6 @@ __device__ __forceinline__ void mb_prep(const KMbArgs &a)
         const int o = a.owner[(int64_t)cy * G.W + cx];
         own[i] = (uint8_t)((o != kBlendNone && ((mask >> o) & 1u))
                                ? __popc(mask & ((1u << o) - 1u)) : kBlendNone);
-    }
-    // every owner's source footprint (bounding box of its taps) ...
-    __shared__ int f_rmin[kBlendSlots], f_rmax[kBlendSlots], f_bmin[kBlendSlots],
-        f_bmax[kBlendSlots];
-    __shared__ MbFoot foot[kBlendSlots];
-    if (tid < kBlendSlots) {
-        f_rmin[tid] = f_bmin[tid] = 0x7fffffff;
-        f_rmax[tid] = f_bmax[tid] = -1;
-    }
-    __syncthreads();
-    for (int i = tid; i < kMbU * ns; i += nt) {
-        const int j = i / kMbU, e = i % kMbU;
-        const int cx = refl(G.RX + kMbFirst + e % kMbUsed, G.W);
-        const int cy = refl(G.RY + kMbFirst + e / kMbUsed, G.H);
-        const MbSrc q = mb_src<INTERP>(P, mb_slot(mask, j), cx, cy);
-        atomicMin(&f_rmin[j], q.ya);
-        atomicMax(&f_rmax[j], q.yb);
-        atomicMin(&f_bmin[j], q.c * CN);
-        atomicMax(&f_bmax[j], q.c * CN + 2 * CN);
-    }
-    __syncthreads();
-    if (tid < ns) {
-        int cam, w, h;
-        slot_info(P, mb_slot(mask, tid), cam, w, h);
-        const int64_t pitch = (int64_t)w * CN;
-        MbFoot F;
-        F.rmin = f_rmin[tid];
-        F.rows = f_rmax[tid] - f_rmin[tid] + 1;
-        F.cal = f_bmin[tid] & ~15;
-        F.stride = (f_bmax[tid] - F.cal + 15) & ~15;
-        F.e = 0;
-        // (rows above the last one may run into the next row, never past the frame)
-        F.fits = F.rows * F.stride + kLdsSlack <= kMbFoot && F.stride <= 16 * kWave &&
-                 F.cal + F.stride <= 2 * pitch;
-        if (f_rmax[tid] == h - 1 && F.cal + F.stride > pitch) {
-            F.e = (int)(F.cal + F.stride - pitch);
-            if ((int64_t)(h - 1) * pitch + F.cal - F.e < 0) F.fits = 0;
-        }
-        F.pad0 = F.pad1 = 0;
-        foot[tid] = F;
-        reinterpret_cast<MbFoot *>(a.foot)[(int64_t)bt * a.slots + tid] = F;
-    }
-    __syncthreads();
-    // ... and every level-0 sample's windows: LDS offsets in the footprint, or frame offsets
-    for (int i = tid; i < kMbU * ns; i += nt) {
-        const int j = i / kMbU, e = i % kMbU;
-        const int cx = refl(G.RX + kMbFirst + e % kMbUsed, G.W);
-        const int cy = refl(G.RY + kMbFirst + e / kMbUsed, G.H);
-        const int sj = mb_slot(mask, j);
-        const MbSrc q = mb_src<INTERP>(P, sj, cx, cy);
-        int cam, w, h;
-        slot_info(P, sj, cam, w, h);
-        const MbFoot &F = foot[j];
-        uint2 v;
-        if (F.fits) {
-            v.x = mb_foot_off(F, q.ya, q.c * CN, h) | (mb_foot_off(F, q.yb, q.c * CN, h) << 16);
-            v.y = q.meta;
-        } else {
-            v = mb_desc<CN>(q, w, h);
-        }
-        a.desc[((int64_t)bt * a.slots + j) * kMbU + e] = (uint64_t)v.x | ((uint64_t)v.y << 32);
     }
     const int RX2 = G.RX + kMbFirst, RY2 = G.RY + kMbFirst;
     // m1 = reduce(owner == slot) over the level-1 array (25-tap form with reflection)
@@ -595,7 +541,7 @@ __device__ __forceinline__ void mb_prep(const KMbArgs &a)
     __shared__ int need_r1[kMbNR * kMbNR];
     __shared__ int n_px, n_r1;
     int32_t *t_cnt = t_d2 + kMbN2 * kMbN2;
-    uint16_t *t_px = reinterpret_cast<uint16_t *>(t_cnt + 2);
+    uint16_t *t_px = reinterpret_cast<uint16_t *>(t_cnt + kMbTabCounts);
     uint16_t *t_r1 = t_px + kBlendTile * kBlendTile;
     for (int e = tid; e < kMbNR * kMbNR; e += nt) need_r1[e] = 0;
     if (tid == 0) n_px = n_r1 = 0;
@@ -633,9 +579,109 @@ __device__ __forceinline__ void mb_prep(const KMbArgs &a)
     for (int e = tid; e < kMbNR * kMbNR; e += nt)
         if (need_r1[e]) t_r1[atomicAdd(&n_r1, 1)] = (uint16_t)e;
     __syncthreads();
+    // Column ranges of the level arrays the mixed pixels depend on (interior tiles; mosaic-border
+    // tiles keep the full arrays): R1 entries -> their level-2 taps -> the level-1 entries the R1
+    // region and those taps reduce from -> the level-0 samples.  mb_levels computes only these.
+    __shared__ int r1lo, r1hi, rng[6];
+    if (tid == 0) r1lo = kMbNR, r1hi = -1;
+    __syncthreads();
+    for (int e = tid; e < kMbNR * kMbNR; e += nt)
+        if (need_r1[e]) {
+            atomicMin(&r1lo, e % kMbNR);
+            atomicMax(&r1hi, e % kMbNR);
+        }
+    __syncthreads();
     if (tid == 0) {
+        int a0_ = 0, b0_ = kMbUsed - 1, a1_ = 0, b1_ = kMbN1 - 1, a2_ = 0, b2_ = kMbN2 - 1;
+        if (n_px == 0) {
+            a0_ = a1_ = a2_ = 0;
+            b0_ = b1_ = b2_ = -1;
+        } else if (G.interior) {
+            int zlo = 1 << 30, zhi = -(1 << 30);
+            for (int q = G.XR + r1lo; q <= G.XR + r1hi; q++) {
+                int zi[3], zw[3];
+                exp_taps<true>(q, G.w2, zi, zw);
+                zlo = min(zlo, min(zi[0], zi[1]));
+                zhi = max(zhi, max(zi[1], zi[2]));
+            }
+            a2_ = max(zlo - G.X2, 0);
+            b2_ = min(zhi - G.X2, kMbN2 - 1);
+            a1_ = max(min(G.XR + r1lo, 2 * zlo - 2) - G.X1, 0);
+            b1_ = min(max(G.XR + r1hi, 2 * zhi + 2) - G.X1, kMbN1 - 1);
+            a0_ = max(2 * (a1_ + G.X1) - 2 - (G.RX + kMbFirst), 0);
+            b0_ = min(2 * (b1_ + G.X1) + 2 - (G.RX + kMbFirst), kMbUsed - 1);
+        }
+        rng[0] = a0_, rng[1] = b0_, rng[2] = a1_, rng[3] = b1_, rng[4] = a2_, rng[5] = b2_;
         t_cnt[0] = n_px;
         t_cnt[1] = n_r1;
+        for (int q = 0; q < 6; q++) t_cnt[2 + q] = rng[q];
+    }
+    __syncthreads();
+    const int a0 = rng[0], w0 = rng[1] - rng[0] + 1, n_s = kMbUsed * w0;
+    // every owner's source footprint (bounding box of its taps) ...
+    __shared__ int f_rmin[kBlendSlots], f_rmax[kBlendSlots], f_bmin[kBlendSlots],
+        f_bmax[kBlendSlots];
+    __shared__ MbFoot foot[kBlendSlots];
+    if (tid < kBlendSlots) {
+        f_rmin[tid] = f_bmin[tid] = 0x7fffffff;
+        f_rmax[tid] = f_bmax[tid] = -1;
+    }
+    __syncthreads();
+    for (int i = tid; i < n_s * ns; i += nt) {
+        const int j = i / n_s, e = i % n_s;
+        const int g = mb_sample_index(e, a0, w0);
+        const int cx = refl(G.RX + kMbFirst + g % kMbUsed, G.W);
+        const int cy = refl(G.RY + kMbFirst + g / kMbUsed, G.H);
+        const MbSrc q = mb_src<INTERP>(P, mb_slot(mask, j), cx, cy);
+        atomicMin(&f_rmin[j], q.ya);
+        atomicMax(&f_rmax[j], q.yb);
+        atomicMin(&f_bmin[j], q.c * CN);
+        atomicMax(&f_bmax[j], q.c * CN + 2 * CN);
+    }
+    __syncthreads();
+    if (tid < ns) {
+        int cam, w, h;
+        slot_info(P, mb_slot(mask, tid), cam, w, h);
+        const int64_t pitch = (int64_t)w * CN;
+        MbFoot F;
+        F.rmin = f_rmin[tid];
+        F.rows = f_rmax[tid] - f_rmin[tid] + 1;
+        F.cal = f_bmin[tid] & ~15;
+        F.stride = (f_bmax[tid] - F.cal + 15) & ~15;
+        F.e = 0;
+        // (rows above the last one may run into the next row, never past the frame)
+        F.fits = F.rows * F.stride + kLdsSlack <= kMbFoot && F.stride <= 16 * kWave &&
+                 F.cal + F.stride <= 2 * pitch;
+        if (f_rmax[tid] == h - 1 && F.cal + F.stride > pitch) {
+            F.e = (int)(F.cal + F.stride - pitch);
+            if ((int64_t)(h - 1) * pitch + F.cal - F.e < 0) F.fits = 0;
+        }
+        F.pad0 = F.pad1 = 0;
+        foot[tid] = F;
+        reinterpret_cast<MbFoot *>(a.foot)[(int64_t)bt * a.slots + tid] = F;
+    }
+    __syncthreads();
+    // ... and every needed level-0 sample's windows: LDS offsets in the footprint, or frame
+    // offsets; .y bits 16-27 = its index in the 57 x 57 level-0 array
+    for (int i = tid; i < n_s * ns; i += nt) {
+        const int j = i / n_s, e = i % n_s;
+        const int g = mb_sample_index(e, a0, w0);
+        const int cx = refl(G.RX + kMbFirst + g % kMbUsed, G.W);
+        const int cy = refl(G.RY + kMbFirst + g / kMbUsed, G.H);
+        const int sj = mb_slot(mask, j);
+        const MbSrc q = mb_src<INTERP>(P, sj, cx, cy);
+        int cam, w, h;
+        slot_info(P, sj, cam, w, h);
+        const MbFoot &F = foot[j];
+        uint2 v;
+        if (F.fits) {
+            v.x = mb_foot_off(F, q.ya, q.c * CN, h) | (mb_foot_off(F, q.yb, q.c * CN, h) << 16);
+            v.y = q.meta;
+        } else {
+            v = mb_desc<CN>(q, w, h);
+        }
+        v.y |= (uint32_t)g << 16;
+        a.desc[((int64_t)bt * a.slots + j) * kMbU + e] = (uint64_t)v.x | ((uint64_t)v.y << 32);
     }
 }
 
@@ -666,6 +712,15 @@ __device__ __forceinline__ void mb_levels(const KMbArgs &a, MbLvLds<CN> &L)
     const uint32_t mask = (uint32_t)a.list[2 + 2 * bt];
     if (j >= __popc(mask)) return;   // uniform: the whole block leaves before any barrier
     const MbGeo G = mb_geo(P, a.list[1 + 2 * bt]);
+    // the column ranges the tile's mixed pixels depend on (mb_prep): level 0 [a0, a0 + w0),
+    // level 1 [a1, a1 + w1), level 2 [a2, a2 + w2); all rows
+    const int32_t *rg = a.tab + (int64_t)bt * mb_tab_words(a.slots) +
+                        a.slots * (kMbNR * kMbNR + kMbN2 * kMbN2) + kMbNR * kMbNR + kMbN2 * kMbN2 + 2;
+    const int w0 = rg[1] - rg[0] + 1, a1 = rg[2], w1 = rg[3] - rg[2] + 1;
+    const int a2 = rg[4], w2 = rg[5] - rg[4] + 1;
+    const int n_s = kMbUsed * w0;                    // level-0 samples (compacted columns)
+    if (n_s <= 0) return;                            // no mixed pixel: nothing to do (uniform)
+    const unsigned d1m = (65536u + w1 - 1) / w1, d2m = (65536u + w2 - 1) / w2;   // / w1, / w2
     int cam, w, h;
     slot_info(P, mb_slot(mask, j), cam, w, h);
     const int64_t pitch = (int64_t)w * CN, fbytes = pitch * h;
@@ -679,7 +734,7 @@ __device__ __forceinline__ void mb_levels(const KMbArgs &a, MbLvLds<CN> &L)
 #pragma unroll
     for (int kk = 0; kk < KJ; kk++) {
         const int i = tid + kk * NT;
-        const uint64_t v = ((staged || shifted) && i < kMbU) ? dsc[i] : 0ull;
+        const uint64_t v = ((staged || shifted) && i < n_s) ? dsc[i] : 0ull;
         doff[kk] = (uint32_t)v;
         dmeta[kk] = (uint32_t)(v >> 32);
     }
@@ -726,7 +781,7 @@ __device__ __forceinline__ void mb_levels(const KMbArgs &a, MbLvLds<CN> &L)
             }
 #pragma unroll
             for (int kk = 0; kk < KJ; kk++)
-                if (tid + kk * NT < kMbU) L.g0[tid + kk * NT] = px[kk];
+                if (tid + kk * NT < n_s) L.g0[(dmeta[kk] >> 16) & 0xfffu] = px[kk];
         } else if (shifted) {
             struct __attribute__((packed)) U2 {
                 uint32_t x, y;
@@ -739,7 +794,7 @@ __device__ __forceinline__ void mb_levels(const KMbArgs &a, MbLvLds<CN> &L)
             mb_opaque(dmeta);
 #pragma unroll
             for (int kk = 0; kk < KJ; kk++) {
-                const uint32_t d = dmeta[kk] >> 12;
+                const uint32_t d = (dmeta[kk] >> 12) & 7u;
                 const uint32_t o = (doff[kk] & 0x7fffffffu) - d;
                 const uint32_t ob = o + ((doff[kk] >> 31) ? (uint32_t)pitch : 0u);
                 const U2 ra = *(const gu2 *)(gfb + o), rb = *(const gu2 *)(gfb + ob);
@@ -752,9 +807,9 @@ __device__ __forceinline__ void mb_levels(const KMbArgs &a, MbLvLds<CN> &L)
             }
 #pragma unroll
             for (int kk = 0; kk < KJ; kk++)
-                if (tid + kk * NT < kMbU) L.g0[tid + kk * NT] = px[kk];
+                if (tid + kk * NT < n_s) L.g0[(dmeta[kk] >> 16) & 0xfffu] = px[kk];
         } else {
-            for (int i = tid; i < kMbU; i += NT) {
+            for (int i = tid; i < n_s; i += NT) {
                 const uint64_t v = dsc[i];
                 const uint32_t o = (uint32_t)v & 0x7fffffffu;
                 const uint32_t ob = o + (((uint32_t)v >> 31) ? (uint32_t)pitch : 0u);
@@ -763,7 +818,7 @@ __device__ __forceinline__ void mb_levels(const KMbArgs &a, MbLvLds<CN> &L)
                 mb_weights((uint32_t)(v >> 32), wa, wb);
 #pragma unroll
                 for (int k = 0; k < CN; k++) px |= mb_tap<CN>(r0, r1, wa, wb, k, 0u) << (8 * k);
-                L.g0[i] = px;
+                L.g0[(uint32_t)(v >> 48) & 0xfffu] = px;
             }
         }
         __syncthreads();
@@ -775,14 +830,16 @@ __device__ __forceinline__ void mb_levels(const KMbArgs &a, MbLvLds<CN> &L)
             // sums stay below 2^16: exact), then per channel.  Level-1 entry e reads level-0
             // offsets 2e + [0, 5); level-2 entry z reads level-1 entries 2z + [0, 5).
             // (each thread's items are computed before any is stored, so that their LDS reads
-            // are not ordered behind the stores)
+            // are not ordered behind the stores; only the needed columns, all rows)
             {
                 constexpr int IT = (kMbUsed * kMbN1 + NT - 1) / NT;
+                const int n = kMbUsed * w1;
                 uint2 res[IT];
 #pragma unroll
                 for (int q = 0; q < IT; q++) {
-                    const int i = min(tid + q * NT, kMbUsed * kMbN1 - 1);
-                    const int r = i / kMbN1, e = i % kMbN1;
+                    const int i = min(tid + q * NT, n - 1);
+                    const int r = (int)(__umul24((unsigned)i, d1m) >> 16);
+                    const int e = a1 + i - (int)__umul24((unsigned)r, (unsigned)w1);
                     const uint32_t *g = &L.g0[r * kMbUsed + 2 * e];
                     uint32_t lo = 0, hi = 0;
 #pragma unroll
@@ -794,17 +851,24 @@ __device__ __forceinline__ void mb_levels(const KMbArgs &a, MbLvLds<CN> &L)
                     res[q] = make_uint2(lo, hi);
                 }
 #pragma unroll
-                for (int q = 0; q < IT; q++)
-                    if (tid + q * NT < kMbUsed * kMbN1) L.hs[tid + q * NT] = res[q];
+                for (int q = 0; q < IT; q++) {
+                    const int i = tid + q * NT;
+                    if (i < n) {
+                        const int r = (int)(__umul24((unsigned)i, d1m) >> 16);
+                        L.hs[r * kMbN1 + a1 + i - (int)__umul24((unsigned)r, (unsigned)w1)] = res[q];
+                    }
+                }
             }
             __syncthreads();
             {
                 constexpr int IT = (kMbN1 * kMbN1 + NT - 1) / NT;
+                const int n = kMbN1 * w1;
                 uint2 res[IT];
 #pragma unroll
                 for (int q = 0; q < IT; q++) {
-                    const int i = min(tid + q * NT, kMbN1 * kMbN1 - 1);
-                    const int ey = i / kMbN1, ex = i % kMbN1;
+                    const int i = min(tid + q * NT, n - 1);
+                    const int ey = (int)(__umul24((unsigned)i, d1m) >> 16);
+                    const int ex = a1 + i - (int)__umul24((unsigned)ey, (unsigned)w1);
                     uint32_t lo = 0, hi = 0;
 #pragma unroll
                     for (int u = 0; u < 5; u++) {
@@ -815,12 +879,18 @@ __device__ __forceinline__ void mb_levels(const KMbArgs &a, MbLvLds<CN> &L)
                     res[q] = make_uint2(lo, hi);
                 }
 #pragma unroll
-                for (int q = 0; q < IT; q++)
-                    if (tid + q * NT < kMbN1 * kMbN1) L.g1[tid + q * NT] = res[q];
+                for (int q = 0; q < IT; q++) {
+                    const int i = tid + q * NT;
+                    if (i < n) {
+                        const int ey = (int)(__umul24((unsigned)i, d1m) >> 16);
+                        L.g1[ey * kMbN1 + a1 + i - (int)__umul24((unsigned)ey, (unsigned)w1)] = res[q];
+                    }
+                }
             }
             __syncthreads();
-            for (int i = tid; i < kMbN1 * kMbN2; i += NT) {
-                const int r = i / kMbN2, e = i % kMbN2;
+            for (int i = tid; i < kMbN1 * w2; i += NT) {
+                const int r = (int)(__umul24((unsigned)i, d2m) >> 16);
+                const int e = a2 + i - (int)__umul24((unsigned)r, (unsigned)w2);
                 int acc[4] = {0, 0, 0, 0};
 #pragma unroll
                 for (int v = 0; v < 5; v++) {
@@ -828,11 +898,12 @@ __device__ __forceinline__ void mb_levels(const KMbArgs &a, MbLvLds<CN> &L)
 #pragma unroll
                     for (int k = 0; k < CN; k++) acc[k] += w5[v] * ch16(t, k);
                 }
-                L.hs2[i] = make_int4(acc[0], acc[1], acc[2], acc[3]);
+                L.hs2[r * kMbN2 + e] = make_int4(acc[0], acc[1], acc[2], acc[3]);
             }
             __syncthreads();
-            for (int i = tid; i < kMbN2 * kMbN2; i += NT) {
-                const int ey = i / kMbN2, ex = i % kMbN2;
+            for (int i = tid; i < kMbN2 * w2; i += NT) {
+                const int ey = (int)(__umul24((unsigned)i, d2m) >> 16);
+                const int ex = a2 + i - (int)__umul24((unsigned)ey, (unsigned)w2);
                 int acc[4] = {0, 0, 0, 0};
 #pragma unroll
                 for (int u = 0; u < 5; u++) {
@@ -843,7 +914,7 @@ __device__ __forceinline__ void mb_levels(const KMbArgs &a, MbLvLds<CN> &L)
                     acc[3] += w5[u] * t.w;
                 }
 #pragma unroll
-                for (int k = 0; k < CN; k++) og2[k * (kMbN2 * kMbN2) + i] = acc[k];
+                for (int k = 0; k < CN; k++) og2[k * (kMbN2 * kMbN2) + ey * kMbN2 + ex] = acc[k];
             }
         } else {
             // mosaic-border tiles: 25-tap form with reflection at every level
@@ -942,7 +1013,8 @@ __device__ __forceinline__ void mb_blend_tile(const KMbArgs &a, const MbGeo &G, 
     // R1 = B1 + up(B2), B1 = sum m1 (16384 g1 - E(g2)) / (sum m1 * 4194304)
     const int n_r1 = t_d2[kMbN2 * kMbN2 + 1];
     const uint16_t *t_r1 =
-        reinterpret_cast<const uint16_t *>(t_d2 + kMbN2 * kMbN2 + 2) + kBlendTile * kBlendTile;
+        reinterpret_cast<const uint16_t *>(t_d2 + kMbN2 * kMbN2 + kMbTabCounts) +
+        kBlendTile * kBlendTile;
     for (int l = tid; l < n_r1; l += nt) {
         const int e = t_r1[l];
         const int ey = div_small<kMbNR>(e), ex = e - (int)__umul24((unsigned)ey, kMbNR);
@@ -1055,19 +1127,21 @@ __device__ __forceinline__ void mb_blend(const KMbArgs &a, MbBlLds<CN> &L)
     // every global read of the block issued up front (one memory round trip): the tile pixels'
     // owners and owner samples, and the owners' level scratch
     MbPix<CN> px;
+    int n_px;
     {
         const cgi32 *tc = (const cgi32 *)a.tab + (int64_t)bt * mb_tab_words(a.slots) +
                           a.slots * (kMbNR * kMbNR + kMbN2 * kMbN2) + kMbNR * kMbNR +
                           kMbN2 * kMbN2;
         typedef __attribute__((address_space(1))) const uint16_t cgu16;
-        const int n_px = tc[0];
-        const cgu16 *lp = (const cgu16 *)(tc + 2);
+        n_px = tc[0];
+        const cgu16 *lp = (const cgu16 *)(tc + kMbTabCounts);
 #pragma unroll
         for (int q = 0; q < kMbPQ; q++) {
             const int l = tid + q * kMbBlThreads;
             px.i[q] = l < n_px ? (int)lp[l] : -1;
         }
     }
+    if (n_px == 0) return;   // uniform: no mixed pixel in this tile (before any barrier)
 #pragma unroll
     for (int q = 0; q < kMbPQ; q++) {
         const int i = px.i[q];

@@ -146,9 +146,11 @@ constexpr int kMbUsedPx = 57;       // level-0 neighbourhood side a tile's pyram
 constexpr int kMbNRPx = 18;         // R1 region side (level 1)
 constexpr int kMbN2Px = 12;         // level-2 side
 // per-tile table (int32 words): m1 (R1 region) [slots], m2 [slots], d1 (R1 region), d2, then
-// the blend work lists: n_px, n_r1, the tile pixels to blend (u16, 1024 slots) and the R1
-// entries they read (u16, 18 * 18 slots)
-constexpr int kMbTabLists = 2 + 32 * 32 / 2 + kMbNRPx * kMbNRPx / 2;
+// the work lists: n_px, n_r1, the level-0 / level-1 / level-2 column ranges (first, last) the
+// mixed pixels depend on, the tile pixels to blend (u16, 1024 slots) and the R1 entries they
+// read (u16, 18 * 18 slots)
+constexpr int kMbTabCounts = 8;
+constexpr int kMbTabLists = kMbTabCounts + 32 * 32 / 2 + kMbNRPx * kMbNRPx / 2;
 constexpr int mb_tab_words(int slots)
 {
     return slots * (kMbNRPx * kMbNRPx + kMbN2Px * kMbN2Px) + kMbNRPx * kMbNRPx + kMbN2Px * kMbN2Px +
