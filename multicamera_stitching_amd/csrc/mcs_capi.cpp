@@ -395,10 +395,15 @@ int launch_mb_levels(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KMb
 int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams &P, int n_frames,
                 hipStream_t s)
 {
-    const bool mb = p->blend == MCS_BLEND_MULTIBAND && p->n_blend > 0;
+    const bool mb_all = p->blend == MCS_BLEND_MULTIBAND && p->n_blend > 0;
+    // MCS_MB_CONCURRENT=0 (experiments): the level pyramids on the caller's stream, after the
+    // streaming kernel, instead of beside it
+    static const bool concurrent = !getenv("MCS_MB_CONCURRENT") ||
+                                   strcmp(getenv("MCS_MB_CONCURRENT"), "0") != 0;
+    const bool mb = mb_all && concurrent;
     const bool fork = p->n_fallback > 0 || mb;
     mcs::KMbArgs m;
-    if (mb) mb_args(p, P, m);
+    if (mb_all) mb_args(p, P, m);
     if (fork) HIP_TRY(A->hipEventRecord(p->ev_fork, s));
     if (p->n_fallback > 0) {
         HIP_TRY(A->hipStreamWaitEvent(p->side, p->ev_fork, 0));
@@ -459,7 +464,7 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
             // already ran on the side stream) then blend
             for (int f0 = 0; f0 < n_frames && rc == MCS_OK; f0 += p->mb_chunk) {
                 const int nf = std::min(p->mb_chunk, n_frames - f0);
-                if (f0 > 0) rc = launch_mb_levels(A, p, k, m, f0, nf, s);
+                if (f0 > 0 || !mb) rc = launch_mb_levels(A, p, k, m, f0, nf, s);
                 m.f0 = f0;
                 m.nf = nf;
                 if (rc == MCS_OK)
