@@ -288,7 +288,18 @@ constexpr int kMbN2 = kMbN2Px, kMbO2 = 2;             // level 2: [X0/4 - 2, X0/
 constexpr int kMbNR = kMbNRPx, kMbOR = 1;             // R1:      [X0/2 - 1, X0/2 + 16]
 constexpr int kMbFirst = 2, kMbUsed = kMbUsedPx;      // level-0 offsets the pyramid reads
 constexpr int kMbU = kMbUsed * kMbUsed;               // level-0 samples per owner
-constexpr int kMbFoot = 24576;                         // bytes of one LDS footprint buffer
+#ifndef MCS_MB_FOOT_BYTES
+#define MCS_MB_FOOT_BYTES 24576
+#endif
+#ifndef MCS_MB_FOOT_BUFS
+#define MCS_MB_FOOT_BUFS 2
+#endif
+#ifndef MCS_MB_STAGE
+#define MCS_MB_STAGE 1      // 0: no LDS footprints (global window loads; a 31 KiB levels block)
+#endif
+constexpr int kMbFoot = MCS_MB_FOOT_BYTES;             // bytes of one LDS footprint buffer
+constexpr int kMbFootBufs = MCS_MB_FOOT_BUFS;          // 2: double buffer, 1: refilled during
+                                                       // the reduces
 constexpr int kMbRS = kMbO1 - kMbOR;                  // R1 region origin in the level-1 array (5)
 
 // Expand taps of fine index x into a coarse level of size n (IN: no reflection needed).
@@ -650,8 +661,8 @@ __device__ __forceinline__ void mb_prep(const KMbArgs &a)
         F.stride = (f_bmax[tid] - F.cal + 15) & ~15;
         F.e = 0;
         // (rows above the last one may run into the next row, never past the frame)
-        F.fits = F.rows * F.stride + kLdsSlack <= kMbFoot && F.stride <= 16 * kWave &&
-                 F.cal + F.stride <= 2 * pitch;
+        F.fits = MCS_MB_STAGE && F.rows * F.stride + kLdsSlack <= kMbFoot &&
+                 F.stride <= 16 * kWave && F.cal + F.stride <= 2 * pitch;
         if (f_rmax[tid] == h - 1 && F.cal + F.stride > pitch) {
             F.e = (int)(F.cal + F.stride - pitch);
             if ((int64_t)(h - 1) * pitch + F.cal - F.e < 0) F.fits = 0;
@@ -688,7 +699,7 @@ __device__ __forceinline__ void mb_prep(const KMbArgs &a)
 // ---- levels: grid (listed tiles, slots, ceil(nf / kMbLvFrames)), block kMbLvThreads -------------
 template <int CN>
 struct MbLvLds {
-    uint8_t foot[2][kMbFoot] __attribute__((aligned(16)));   // source footprints (double buffer)
+    uint8_t foot[MCS_MB_STAGE ? kMbFootBufs : 0][kMbFoot] __attribute__((aligned(16)));   // source footprints
     uint32_t g0[kMbU];                 // level 0: channel k in byte k
     uint2 g1[kMbN1 * kMbN1];           // 256 G1 <= 65280 as u16 lanes: x = (c0, c2), y = (c1, c3)
     union {
@@ -762,8 +773,8 @@ __device__ __forceinline__ void mb_levels(const KMbArgs &a, MbLvLds<CN> &L)
             // one streams in while this one is processed
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
-            if (fl + 1 < fl1) stage(fl + 1, (fl + 1 - fl0) & 1);
-            const uint8_t *buf = L.foot[(fl - fl0) & 1];
+            if (kMbFootBufs == 2 && fl + 1 < fl1) stage(fl + 1, (fl + 1 - fl0) & 1);
+            const uint8_t *buf = L.foot[kMbFootBufs == 2 ? (fl - fl0) & 1 : 0];
             // all samples into registers first: a level-0 store between them would order the
             // next sample's LDS reads behind it (the compiler cannot tell the arrays apart)
             uint32_t px[KJ];
@@ -822,6 +833,8 @@ __device__ __forceinline__ void mb_levels(const KMbArgs &a, MbLvLds<CN> &L)
             }
         }
         __syncthreads();
+        // single buffer: the next capture's footprint streams in during this one's reduces
+        if (kMbFootBufs == 1 && staged && fl + 1 < fl1) stage(fl + 1, 0);
         const int64_t job = ((int64_t)bt * a.slots + j) * a.chunk + fl;
         uint2 *og1 = reinterpret_cast<uint2 *>(a.g1) + job * (kMbNR * kMbNR);
         int32_t *og2 = a.g2 + job * (kMbN2 * kMbN2 * CN);

@@ -192,7 +192,10 @@ constexpr int kMaxRing = 6;
 // LDS of a streaming block: the tile header, then a ring of capture footprints, as many slots
 // (2..kMaxRing) as fit.  Sized per channel count to the occupancy the kernel's registers allow:
 // 3 blocks per CU for 3-4 channels (52 KiB each of the CU's 160 KiB), 4 for 1-2 channels.
-constexpr int lds_stream_bytes(int cn) { return cn >= 3 ? 53248 : 40960; }
+#ifndef MCS_STREAM_LDS
+#define MCS_STREAM_LDS 53248
+#endif
+constexpr int lds_stream_bytes(int cn) { return cn >= 3 ? MCS_STREAM_LDS : 40960; }
 constexpr int lds_ring_bytes(int cn) { return lds_stream_bytes(cn) - (int)sizeof(TileHdr); }
 
 
