@@ -28,6 +28,37 @@ struct FeatureKernels {
 FeatureKernels g_fk[mcs::kMaxDevices];
 std::mutex g_fk_mu;
 
+// Scratch buffer + stream of the synchronous per-frame entry points (ORB, Hamming kNN-2, RANSAC:
+// called for every rig capture in the C3 estimation loop), one per thread and device: grown on
+// demand, reused across calls, kept for the thread's lifetime (no per-call hipMalloc / stream
+// creation; released with the process).  The entry points are synchronous, so a thread never has
+// two calls in flight on its workspace.
+struct Workspace {
+    uint8_t *buf = nullptr;
+    size_t cap = 0;
+    hipStream_t s = nullptr;
+};
+thread_local Workspace tl_ws[mcs::kMaxDevices];
+
+int workspace(const Api *A, int device, size_t bytes, uint8_t **buf, hipStream_t *s)
+{
+    if (device < 0 || device >= mcs::kMaxDevices)
+        return mcs::fail(MCS_E_INVALID, "device %d", device);
+    Workspace &w = tl_ws[device];
+    if (!w.s) HIP_TRY(A->hipStreamCreateWithFlags(&w.s, hipStreamNonBlocking));
+    if (w.cap < bytes) {
+        if (w.buf) HIP_TRY(A->hipFree(w.buf));
+        w.buf = nullptr;
+        w.cap = 0;
+        const size_t want = std::max(bytes, (size_t)1 << 20);
+        HIP_TRY(A->hipMalloc((void **)&w.buf, want));
+        w.cap = want;
+    }
+    *buf = w.buf;
+    *s = w.s;
+    return MCS_OK;
+}
+
 int feature_kernels(const Api *A, int device, const FeatureKernels **out)
 {
     if (device < 0 || device >= mcs::kMaxDevices)
@@ -227,22 +258,20 @@ int mcs_match_hamming_knn2_host(const uint8_t *query, int n_query, const uint8_t
     const size_t qb = (size_t)n_query * mcs::kDescBytes, tb = (size_t)n_train * mcs::kDescBytes;
     const size_t ob = (size_t)n_query * 2 * sizeof(int32_t);
     uint8_t *buf = nullptr;
-    HIP_TRY(A->hipMalloc((void **)&buf, qb + tb + 2 * ob + 64));
+    hipStream_t s = nullptr;
+    rc = workspace(A, device, qb + tb + 2 * ob + 64, &buf, &s);
+    if (rc) return rc;
     uint8_t *dq = buf, *dt = buf + qb;
     int32_t *di = reinterpret_cast<int32_t *>(buf + ((qb + tb + 15) & ~(size_t)15));
     int32_t *dd = di + (size_t)n_query * 2;
-    hipStream_t s = nullptr;
-    hipError_t e = A->hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
-    if (e == hipSuccess) e = A->hipMemcpyAsync(dq, query, qb, hipMemcpyHostToDevice, s);
+    hipError_t e = A->hipMemcpyAsync(dq, query, qb, hipMemcpyHostToDevice, s);
     if (e == hipSuccess && tb) e = A->hipMemcpyAsync(dt, train, tb, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) rc = knn2(A, k, dq, n_query, dt, n_train, di, dd, s);
     if (e == hipSuccess && rc == MCS_OK)
         e = A->hipMemcpyAsync(idx2, di, ob, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess && rc == MCS_OK)
         e = A->hipMemcpyAsync(dist2, dd, ob, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess && s) e = A->hipStreamSynchronize(s);
-    if (s) (void)A->hipStreamDestroy(s);
-    (void)A->hipFree(buf);
+    if (e == hipSuccess) e = A->hipStreamSynchronize(s);
     if (e != hipSuccess) return mcs::fail(MCS_E_HIP, "knn2 host path: %s", A->hipGetErrorString(e));
     return rc;
 }
@@ -339,7 +368,9 @@ int mcs_ransac_homography_host(const float *src_xy, const float *dst_xy, int n, 
     const size_t pb = pts.size() * sizeof(double), hb = (size_t)iters * 8 * sizeof(double);
     const size_t sb = (size_t)iters * sizeof(int32_t);
     uint8_t *buf = nullptr;
-    HIP_TRY(A->hipMalloc((void **)&buf, pb + hb + sb + (size_t)n + 64));
+    hipStream_t s = nullptr;
+    rc = workspace(A, device, pb + hb + sb + (size_t)n + 64, &buf, &s);
+    if (rc) return rc;
     mcs::KRansacArgs a;
     a.pts = reinterpret_cast<double *>(buf);
     a.hyps = reinterpret_cast<double *>(buf + pb);
@@ -353,10 +384,7 @@ int mcs_ransac_homography_host(const float *src_xy, const float *dst_xy, int n, 
     std::vector<int32_t> scores((size_t)iters);
     std::vector<uint8_t> m8((size_t)n);
     double hb8[8];
-    hipStream_t s = nullptr;
-    hipError_t e = A->hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
-    if (e == hipSuccess)
-        e = A->hipMemcpyAsync((void *)a.pts, pts.data(), pb, hipMemcpyHostToDevice, s);
+    hipError_t e = A->hipMemcpyAsync((void *)a.pts, pts.data(), pb, hipMemcpyHostToDevice, s);
     if (e == hipSuccess)
         rc = launch(A, k->ransac_score, iters, 1, mcs::kRansacBlock, &a, sizeof(a), s);
     if (e == hipSuccess && rc == MCS_OK)
@@ -377,8 +405,6 @@ int mcs_ransac_homography_host(const float *src_xy, const float *dst_xy, int n, 
             if (e == hipSuccess && rc == MCS_OK) e = A->hipStreamSynchronize(s);
         }
     }
-    if (s) (void)A->hipStreamDestroy(s);
-    (void)A->hipFree(buf);
     if (e != hipSuccess) return mcs::fail(MCS_E_HIP, "ransac: %s", A->hipGetErrorString(e));
     if (rc) return rc;
     if (best_score < 4) return MCS_OK;
@@ -471,16 +497,15 @@ int mcs_orb_detect_host(const uint8_t *image, int w, int h, int channels, int nf
     const size_t o_desc = take((size_t)std::max(nfeatures, 1) * 32);
     const size_t o_or = take((size_t)std::max(nfeatures, 1) * 2 * sizeof(double));
     uint8_t *buf = nullptr;
-    HIP_TRY(A->hipMalloc((void **)&buf, o));
     hipStream_t s = nullptr;
+    rc = workspace(A, device, o, &buf, &s);
+    if (rc) return rc;
     std::vector<int> counts(nlevels);
     std::vector<mcs::OrbCand> cand(cap_total);
     std::vector<int> kp;
     std::vector<double> orient, resp;
-    hipError_t e = A->hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
     uint8_t *lvl0 = buf + o_lvl;
-    if (e == hipSuccess)
-        e = A->hipMemcpyAsync(buf + o_in, image, in_bytes, hipMemcpyHostToDevice, s);
+    hipError_t e = A->hipMemcpyAsync(buf + o_in, image, in_bytes, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = A->hipMemsetAsync(buf + o_cnt, 0, mcs::kOrbMaxLevels * sizeof(int), s);
     if (e == hipSuccess) {
         if (channels == 3) {
@@ -564,8 +589,7 @@ int mcs_orb_detect_host(const uint8_t *image, int w, int h, int channels, int nf
             if (e == hipSuccess && rc == MCS_OK) e = A->hipStreamSynchronize(s);
         }
     }
-    if (s) (void)A->hipStreamDestroy(s);
-    (void)A->hipFree(buf);
+    if (e == hipSuccess && rc != MCS_OK) e = A->hipStreamSynchronize(s);   // drain on error
     if (e != hipSuccess) return mcs::fail(MCS_E_HIP, "orb: %s", A->hipGetErrorString(e));
     if (rc) return rc;
     for (int i = 0; i < n; i++) {

@@ -102,9 +102,10 @@ def make_frames(n_cams, width, height, channels=3, seed=0):
     return [texture(height, width, channels, seed=seed * 131 + k) for k in range(n_cams)]
 
 
-def world_frames(C, width, height, channels=3, seed=0):
+def world_frames(C, width, height, channels=3, seed=0, world_fn=None):
     """Camera frames rendered from ONE shared world texture through the camera models C (so
-    overlaps agree up to interpolation, as with a real rig); float bilinear, numpy."""
+    overlaps agree up to interpolation, as with a real rig); float bilinear, numpy.  world_fn(h,
+    w, channels, seed) -> u8 image replaces the default procedural texture."""
     corners = np.array([[0, 0, 1], [width - 1, 0, 1], [0, height - 1, 1],
                         [width - 1, height - 1, 1]], np.float64).T
     pts = []
@@ -114,7 +115,8 @@ def world_frames(C, width, height, channels=3, seed=0):
     pts = np.concatenate(pts, axis=1)
     x0, y0 = np.floor(pts.min(axis=1)) - 2
     x1, y1 = np.ceil(pts.max(axis=1)) + 2
-    world = texture(int(y1 - y0) + 1, int(x1 - x0) + 1, channels, seed=seed).astype(np.float64)
+    make = world_fn or texture
+    world = make(int(y1 - y0) + 1, int(x1 - x0) + 1, channels, seed=seed).astype(np.float64)
     if world.ndim == 2:
         world = world[..., None]
     v, u = np.mgrid[0:height, 0:width].astype(np.float64)

@@ -1,0 +1,138 @@
+#!/usr/bin/env python3
+"""C3 benchmark (BASELINE.json configs[2]): per rig capture, the homographies re-estimated on
+the GPU -- ORB (nfeatures 2000, 8 levels x 1.2, FAST 20) on each of the 4 1920x1080 BGR camera
+frames, BF Hamming kNN-2 + Lowe ratio 0.75 + RANSAC (3.0 px, 2000 hypotheses) for each adjacent
+camera pair -- and the CPU restatement (oracle/, the checker) of the same chain beside it.
+
+The frames are rendered from one shared world (rectangles of random grey levels, seed 0) through
+the C2 rig's camera models, so overlaps agree and the true pair homographies are known; the
+estimates are checked against them (max reprojection error over the pair's overlap).  Host
+frames in, homographies out: the PCIe upload of each frame is inside the timed region.
+
+One JSON line: rig estimations/s, ms per capture and per stage, matches / inliers, errors.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def world(h, w, channels, seed):
+    from multicamera_stitching_amd import rig
+    g = rig.corner_texture(h, w, seed=seed).astype(np.int32)
+    tint = np.array([0, 7, -9][:channels], np.int32)
+    return np.clip(g[..., None] + tint, 1, 255).astype(np.uint8)
+
+
+def pair_error(H, Ht, w, h):
+    """max |H p - Ht p| over a grid of the query camera's left quarter (the overlap)."""
+    u, v = np.meshgrid(np.linspace(0, w * 0.2, 8), np.linspace(0, h - 1, 8))
+    g = np.stack([u.ravel(), v.ravel(), np.ones(u.size)], axis=1)
+    p, q = g @ H.T, g @ Ht.T
+    return float(np.abs(p[:, :2] / p[:, 2:] - q[:, :2] / q[:, 2:]).max())
+
+
+def estimate_gpu(frames, args):
+    from multicamera_stitching_amd import _capi
+    from multicamera_stitching_amd.features import ratio_matches
+    t = {"orb": 0.0, "match": 0.0, "ransac": 0.0}
+    t0 = time.perf_counter()
+    feats = [_capi.orb_detect(f, args.nfeatures, 8, 1.2, 20) for f in frames]
+    t1 = time.perf_counter()
+    t["orb"] = t1 - t0
+    out = []
+    for k in range(1, len(frames)):
+        ta = time.perf_counter()
+        idx, dist = _capi.match_hamming_knn2(feats[k]["desc"], feats[k - 1]["desc"])
+        m = ratio_matches(idx, dist)
+        tb = time.perf_counter()
+        src = np.float32([feats[k]["xy"][q] for (_, q) in m]).reshape(-1, 2)
+        dst = np.float32([feats[k - 1]["xy"][tr] for (tr, _) in m]).reshape(-1, 2)
+        H, mask = _capi.ransac_homography(src, dst, 3.0, 2000, 0)
+        tc = time.perf_counter()
+        t["match"] += tb - ta
+        t["ransac"] += tc - tb
+        out.append((H, len(m), int(mask.sum()), [len(f["xy"]) for f in feats]))
+    return out, t
+
+
+def estimate_cpu(frames, args):
+    from oracle import oracle
+    from multicamera_stitching_amd.features import ratio_matches
+    feats = []
+    for f in frames:
+        g = ((f[..., 0].astype(np.int32) * 1868 + f[..., 1].astype(np.int32) * 9617 +
+              f[..., 2].astype(np.int32) * 4899 + 8192) >> 14).astype(np.uint8)
+        feats.append(oracle.orb_detect(g, args.nfeatures, 8, 1.2, 20))
+    out = []
+    for k in range(1, len(frames)):
+        idx, dist = oracle.hamming_knn2(feats[k]["desc"], feats[k - 1]["desc"])
+        m = ratio_matches(idx, dist)
+        src = np.float32([feats[k]["xy"][q] for (_, q) in m]).reshape(-1, 2)
+        dst = np.float32([feats[k - 1]["xy"][tr] for (tr, _) in m]).reshape(-1, 2)
+        H, mask, _, _ = oracle.ransac_homography(src, dst, 3.0, 2000, 0)
+        out.append(H)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--nfeatures", type=int, default=2000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+    from multicamera_stitching_amd import rig
+    W, Hh, N = 1920, 1080, 4
+    C = rig.camera_models(N, W, Hh, seed=0)
+    frames = rig.world_frames(C, W, Hh, 3, seed=0, world_fn=world)
+    truth = [np.linalg.inv(C[k - 1]) @ C[k] for k in range(1, N)]
+    truth = [T / T[2, 2] for T in truth]
+    for _ in range(args.warmup):
+        estimate_gpu(frames, args)
+    tot = {"orb": 0.0, "match": 0.0, "ransac": 0.0}
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res, t = estimate_gpu(frames, args)
+        for key in tot:
+            tot[key] += t[key]
+    elapsed = time.perf_counter() - t0
+    errs = [pair_error(h, T, W, Hh) if h is not None else None for (h, *_), T in zip(res, truth)]
+    line = {
+        "metric": "rig homography estimations/sec (C3: 4-cam 1080p, ORB + BF Hamming kNN-2 + "
+                  "RANSAC per capture)",
+        "value": round(args.steps / elapsed, 2), "unit": "captures/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+        "dtype": "u8 / int popcount / f64", "data": "synthetic (shared-world rig, seed 0)",
+        "config": {"workload": "BASELINE configs[2]: ORB nfeatures %d, 8 levels x 1.2, FAST 20; "
+                               "Hamming kNN-2, ratio 0.75; RANSAC 3.0 px, 2000 hypotheses; 3 "
+                               "adjacent pairs" % args.nfeatures,
+                   "host_frames": True},
+        "stage_ms_per_capture": {k: round(v / args.steps * 1e3, 3) for k, v in tot.items()},
+        "keypoints": res[0][3], "matches": [r[1] for r in res], "inliers": [r[2] for r in res],
+        "max_reproj_err_px_vs_truth": errs,
+    }
+    if not args.no_cpu_baseline:
+        from oracle import oracle
+        tc = time.perf_counter()
+        cpu = estimate_cpu(frames, args)
+        dt = time.perf_counter() - tc
+        diff = [pair_error(a, b, W, Hh) if a is not None and b is not None else None
+                for a, b in zip([r[0] for r in res], cpu)]
+        line["cpu_baseline"] = {"value": round(1.0 / dt, 3), "unit": "captures/s",
+                                "cores": oracle.num_threads(), "kind": "port",
+                                "sample": "1 capture through the C restatement (orc_orb.c, "
+                                          "orc_match.c, orc_ransac.c), %.1f s" % dt}
+        line["max_abs_H_reproj_diff_gpu_vs_cpu_px"] = diff
+    print(json.dumps(line))
+
+
+if __name__ == "__main__":
+    main()
