@@ -83,3 +83,22 @@ def test_dropin_calibrates_with_gpu_orb_backend(monkeypatch):
         crop = crop[..., 0]
     err = np.abs(crop[:, 700:1300] - ref[:, 700:1300])
     assert np.median(err) <= 2
+
+
+def test_orb_match_ransac_concurrent_threads_match_serial():
+    """The per-frame entry points from several host threads at once (each thread has its own
+    stream and device workspace in libmcs) give the serial results, call after call."""
+    from concurrent.futures import ThreadPoolExecutor
+    from multicamera_stitching_amd import _capi
+    imgs = [rig.corner_texture(540, 960, seed=s) for s in range(4)]
+    want = [_capi.orb_detect(im, 800) for im in imgs]
+    want_m = [_capi.match_hamming_knn2(want[k]["desc"], want[k - 1]["desc"]) for k in (1, 2, 3)]
+    with ThreadPoolExecutor(4) as ex:
+        for _ in range(3):
+            got = list(ex.map(lambda im: _capi.orb_detect(im, 800), imgs))
+            for g, w in zip(got, want):
+                assert np.array_equal(g["xy"], w["xy"]) and np.array_equal(g["desc"], w["desc"])
+            got_m = list(ex.map(lambda k: _capi.match_hamming_knn2(got[k]["desc"],
+                                                                   got[k - 1]["desc"]), (1, 2, 3)))
+            for (gi, gd), (wi, wd) in zip(got_m, want_m):
+                assert np.array_equal(gi, wi) and np.array_equal(gd, wd)
