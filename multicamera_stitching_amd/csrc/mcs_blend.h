@@ -7,7 +7,7 @@
 // camera farthest from its own image edge); then only the tiles where blending changes pixels
 // are recomputed here, 32 x 32 output pixels per block:
 //   feather   -- tiles with a pixel covered by two cameras at positive edge distance;
-//   multiband -- tiles whose 64 x 64 neighbourhood (the 3-level pyramid's reach, 16 px halo)
+//   multiband -- tiles whose neighbourhood (the 3-level pyramid's reach, 16 px halo)
 //                holds two owners (the seam band).  Per tile: the owners' warped images over the
 //                neighbourhood (replicate border) -> integer Gaussian/Laplacian pyramids in LDS
 //                -> mask-weighted blend per level (double) -> collapse -> bytes.
@@ -167,10 +167,10 @@ __device__ __forceinline__ void blend_owner_tile(const KParams &P, uint8_t *owne
     __shared__ uint32_t s_own, s_feather;
     if (threadIdx.x == 0) s_own = s_feather = 0;
     __syncthreads();
-    const int X0 = blockIdx.x * kBlendTile, Y0 = blockIdx.y * kBlendTile;
+    const int X0 = blockIdx.x * kBlendTileW, Y0 = blockIdx.y * kBlendTileH;
     uint32_t own = 0, fea = 0;
-    for (int i = threadIdx.x; i < kBlendTile * kBlendTile; i += blockDim.x) {
-        const int x = X0 + (i % kBlendTile), y = Y0 + i / kBlendTile;
+    for (int i = threadIdx.x; i < kMbTilePx; i += blockDim.x) {
+        const int x = X0 + (i % kBlendTileW), y = Y0 + i / kBlendTileW;
         if (x >= P.out_w || y >= P.out_h) continue;
         uint32_t pm;
         const int o = blend_owner<INTERP>(P, x, y, &pm);
@@ -197,7 +197,7 @@ __device__ __forceinline__ void blend_classify(const KParams &P, int mode, const
                                                const uint32_t *info, int *list, int *overflow)
 {
     __shared__ uint32_t s_mask;
-    const int gx = (P.out_w + kBlendTile - 1) / kBlendTile;
+    const int gx = (P.out_w + kBlendTileW - 1) / kBlendTileW;
     const int t = blockIdx.x, tx = t % gx, ty = t / gx;
     uint32_t mask;
     if (mode == MCS_BLEND_FEATHER) {
@@ -205,10 +205,10 @@ __device__ __forceinline__ void blend_classify(const KParams &P, int mode, const
     } else {
         if (threadIdx.x == 0) s_mask = 0;
         __syncthreads();
-        const int x0 = max(tx * kBlendTile - kBlendHalo, 0);
-        const int x1 = min(tx * kBlendTile + kBlendTile + kBlendHalo, P.out_w);
-        const int y0 = max(ty * kBlendTile - kBlendHalo, 0);
-        const int y1 = min(ty * kBlendTile + kBlendTile + kBlendHalo, P.out_h);
+        const int x0 = max(tx * kBlendTileW - kBlendHalo, 0);
+        const int x1 = min(tx * kBlendTileW + kBlendTileW + kBlendHalo, P.out_w);
+        const int y0 = max(ty * kBlendTileH - kBlendHalo, 0);
+        const int y1 = min(ty * kBlendTileH + kBlendTileH + kBlendHalo, P.out_h);
         const int rw = x1 - x0, n = rw * (y1 - y0);
         uint32_t m = 0;
         for (int i = threadIdx.x; i < n; i += blockDim.x) {
@@ -235,12 +235,12 @@ template <int CN, int INTERP>
 __device__ __forceinline__ void feather_tile(const KBlendArgs &a)
 {
     const KParams &P = a.P;
-    const int gx = (P.out_w + kBlendTile - 1) / kBlendTile;
+    const int gx = (P.out_w + kBlendTileW - 1) / kBlendTileW;
     const int t = a.list[1 + 2 * blockIdx.x];
     const uint32_t mask = (uint32_t)a.list[2 + 2 * blockIdx.x];
-    const int X0 = (t % gx) * kBlendTile, Y0 = (t / gx) * kBlendTile, f = blockIdx.y;
-    for (int i = threadIdx.x; i < kBlendTile * kBlendTile; i += blockDim.x) {
-        const int x = X0 + (i % kBlendTile), y = Y0 + i / kBlendTile;
+    const int X0 = (t % gx) * kBlendTileW, Y0 = (t / gx) * kBlendTileH, f = blockIdx.y;
+    for (int i = threadIdx.x; i < kMbTilePx; i += blockDim.x) {
+        const int x = X0 + (i % kBlendTileW), y = Y0 + i / kBlendTileW;
         if (x >= P.out_w || y >= P.out_h) continue;
         int den = 0, num[CN];
 #pragma unroll
@@ -282,17 +282,14 @@ __device__ __forceinline__ void feather_tile(const KBlendArgs &a)
 //                       kernel already wrote (equal to the replicate-border sample wherever the
 //                       owner covers the pixel, which it always does).
 // Long launches run in chunks of captures so the scratch stays a few tens of MB.
-constexpr int kMbR0 = kBlendTile + 2 * kBlendHalo;   // 64
-constexpr int kMbN1 = 27, kMbO1 = 6;                  // level 1: [X0/2 - 6, X0/2 + 20]
-constexpr int kMbN2 = kMbN2Px, kMbO2 = 2;             // level 2: [X0/4 - 2, X0/4 + 9]
-constexpr int kMbNR = kMbNRPx, kMbOR = 1;             // R1:      [X0/2 - 1, X0/2 + 16]
-constexpr int kMbFirst = 2, kMbUsed = kMbUsedPx;      // level-0 offsets the pyramid reads
-constexpr int kMbU = kMbUsed * kMbUsed;               // level-0 samples per owner
+constexpr int kMbO1 = 6, kMbO2 = 2, kMbOR = 1;       // array origins: O/2 - 6, O/4 - 2, O/2 - 1
+constexpr int kMbFirst = 2;                           // level-0 origin: O - 16 + 2
+constexpr int kMbU = kMbUsedX * kMbUsedY;             // level-0 samples per owner
 #ifndef MCS_MB_FOOT_BYTES
-#define MCS_MB_FOOT_BYTES 24576
+#define MCS_MB_FOOT_BYTES 28672
 #endif
 #ifndef MCS_MB_FOOT_BUFS
-#define MCS_MB_FOOT_BUFS 2
+#define MCS_MB_FOOT_BUFS 1
 #endif
 #ifndef MCS_MB_STAGE
 #define MCS_MB_STAGE 1      // 0: no LDS footprints (global window loads; a 31 KiB levels block)
@@ -330,13 +327,14 @@ __device__ __forceinline__ MbGeo mb_geo(const KParams &P, int t)
     G.W = P.out_w;
     G.H = P.out_h;
     G.w1 = (G.W + 1) / 2, G.h1 = (G.H + 1) / 2, G.w2 = (G.w1 + 1) / 2, G.h2 = (G.h1 + 1) / 2;
-    const int gx = (G.W + kBlendTile - 1) / kBlendTile;
-    G.X0 = (t % gx) * kBlendTile, G.Y0 = (t / gx) * kBlendTile;
+    const int gx = (G.W + kBlendTileW - 1) / kBlendTileW;
+    G.X0 = (t % gx) * kBlendTileW, G.Y0 = (t / gx) * kBlendTileH;
     G.RX = G.X0 - kBlendHalo, G.RY = G.Y0 - kBlendHalo;         // level-0 origin
     G.X1 = G.X0 / 2 - kMbO1, G.Y1 = G.Y0 / 2 - kMbO1;             // level-1 origin
     G.X2 = G.X0 / 4 - kMbO2, G.Y2 = G.Y0 / 4 - kMbO2;             // level-2 origin
     G.XR = G.X0 / 2 - kMbOR, G.YR = G.Y0 / 2 - kMbOR;             // R1 origin
-    G.interior = G.RX >= 0 && G.RY >= 0 && G.RX + kMbR0 <= G.W && G.RY + kMbR0 <= G.H;
+    G.interior = G.RX >= 0 && G.RY >= 0 && G.RX + kBlendTileW + 2 * kBlendHalo <= G.W &&
+                 G.RY + kBlendTileH + 2 * kBlendHalo <= G.H;
     return G;
 }
 
@@ -456,7 +454,7 @@ __device__ __forceinline__ int div_small(int e)
 __device__ __forceinline__ int mb_sample_index(int e, int a0, int w0)
 {
     const int r = e / w0;
-    return r * kMbUsed + a0 + (e - r * w0);
+    return r * kMbUsedX + a0 + (e - r * w0);
 }
 
 // Local slot j (0 .. popc(mask) - 1) -> plan slot: the j-th set bit of mask.
@@ -471,8 +469,8 @@ template <int CN, int INTERP>
 __device__ __forceinline__ void mb_prep(const KMbArgs &a)
 {
     __shared__ uint8_t own[kMbU];
-    __shared__ int32_t m1[kBlendSlots][kMbN1 * kMbN1];
-    __shared__ int32_t m2[kBlendSlots][kMbN2 * kMbN2];
+    __shared__ int32_t m1[kBlendSlots][kMbN1X * kMbN1Y];
+    __shared__ int32_t m2[kBlendSlots][kMbN2X * kMbN2Y];
     const KParams &P = a.P;
     const int bt = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
     const uint32_t mask = (uint32_t)a.list[2 + 2 * bt];
@@ -481,23 +479,23 @@ __device__ __forceinline__ void mb_prep(const KMbArgs &a)
     const int w5[5] = {1, 4, 6, 4, 1};
     // owner map of the used neighbourhood as local slot indices (bit rank in `mask`)
     for (int i = tid; i < kMbU; i += nt) {
-        const int cx = refl(G.RX + kMbFirst + i % kMbUsed, G.W);
-        const int cy = refl(G.RY + kMbFirst + i / kMbUsed, G.H);
+        const int cx = refl(G.RX + kMbFirst + i % kMbUsedX, G.W);
+        const int cy = refl(G.RY + kMbFirst + i / kMbUsedX, G.H);
         const int o = a.owner[(int64_t)cy * G.W + cx];
         own[i] = (uint8_t)((o != kBlendNone && ((mask >> o) & 1u))
                                ? __popc(mask & ((1u << o) - 1u)) : kBlendNone);
     }
     const int RX2 = G.RX + kMbFirst, RY2 = G.RY + kMbFirst;
     // m1 = reduce(owner == slot) over the level-1 array (25-tap form with reflection)
-    for (int i = tid; i < kMbN1 * kMbN1 * ns; i += nt) {
-        const int j = i / (kMbN1 * kMbN1), e = i % (kMbN1 * kMbN1);
-        const int qx = refl(G.X1 + e % kMbN1, G.w1), qy = refl(G.Y1 + e / kMbN1, G.h1);
+    for (int i = tid; i < kMbN1X * kMbN1Y * ns; i += nt) {
+        const int j = i / (kMbN1X * kMbN1Y), e = i % (kMbN1X * kMbN1Y);
+        const int qx = refl(G.X1 + e % kMbN1X, G.w1), qy = refl(G.Y1 + e / kMbN1X, G.h1);
         int macc = 0;
         for (int u = 0; u < 5; u++) {
             const int cy = refl(2 * qy + u - 2, G.H);
             for (int v = 0; v < 5; v++) {
                 const int cx = refl(2 * qx + v - 2, G.W);
-                const int p = ix2<false>(cy, RY2, kMbUsed) * kMbUsed + ix2<false>(cx, RX2, kMbUsed);
+                const int p = ix2<false>(cy, RY2, kMbUsedY) * kMbUsedX + ix2<false>(cx, RX2, kMbUsedX);
                 macc += own[p] == j ? w5[u] * w5[v] : 0;
             }
         }
@@ -505,15 +503,15 @@ __device__ __forceinline__ void mb_prep(const KMbArgs &a)
     }
     __syncthreads();
     // m2 = reduce(m1)
-    for (int i = tid; i < kMbN2 * kMbN2 * ns; i += nt) {
-        const int j = i / (kMbN2 * kMbN2), e = i % (kMbN2 * kMbN2);
-        const int zx = refl(G.X2 + e % kMbN2, G.w2), zy = refl(G.Y2 + e / kMbN2, G.h2);
+    for (int i = tid; i < kMbN2X * kMbN2Y * ns; i += nt) {
+        const int j = i / (kMbN2X * kMbN2Y), e = i % (kMbN2X * kMbN2Y);
+        const int zx = refl(G.X2 + e % kMbN2X, G.w2), zy = refl(G.Y2 + e / kMbN2X, G.h2);
         int macc = 0;
         for (int u = 0; u < 5; u++) {
             const int qy = refl(2 * zy + u - 2, G.h1);
             for (int v = 0; v < 5; v++) {
                 const int qx = refl(2 * zx + v - 2, G.w1);
-                const int p = ix2<false>(qy, G.Y1, kMbN1) * kMbN1 + ix2<false>(qx, G.X1, kMbN1);
+                const int p = ix2<false>(qy, G.Y1, kMbN1Y) * kMbN1X + ix2<false>(qx, G.X1, kMbN1X);
                 macc += w5[u] * w5[v] * m1[j][p];
             }
         }
@@ -522,23 +520,23 @@ __device__ __forceinline__ void mb_prep(const KMbArgs &a)
     __syncthreads();
     // table: m1 (R1 region) [slots], m2 [slots], d1 (R1 region), d2
     int32_t *tab = a.tab + (int64_t)bt * mb_tab_words(a.slots);
-    int32_t *t_m1 = tab, *t_m2 = tab + a.slots * kMbNR * kMbNR;
-    int32_t *t_d1 = t_m2 + a.slots * kMbN2 * kMbN2, *t_d2 = t_d1 + kMbNR * kMbNR;
-    for (int e = tid; e < kMbNR * kMbNR; e += nt) {
-        const int p = (e / kMbNR + kMbRS) * kMbN1 + e % kMbNR + kMbRS;
+    int32_t *t_m1 = tab, *t_m2 = tab + a.slots * kMbNRX * kMbNRY;
+    int32_t *t_d1 = t_m2 + a.slots * kMbN2X * kMbN2Y, *t_d2 = t_d1 + kMbNRX * kMbNRY;
+    for (int e = tid; e < kMbNRX * kMbNRY; e += nt) {
+        const int p = (e / kMbNRX + kMbRS) * kMbN1X + e % kMbNRX + kMbRS;
         int d = 0;
         for (int j = 0; j < a.slots; j++) {
             const int v = j < ns ? m1[j][p] : 0;
-            t_m1[j * kMbNR * kMbNR + e] = v;
+            t_m1[j * kMbNRX * kMbNRY + e] = v;
             d += v;
         }
         t_d1[e] = d;
     }
-    for (int e = tid; e < kMbN2 * kMbN2; e += nt) {
+    for (int e = tid; e < kMbN2X * kMbN2Y; e += nt) {
         int d = 0;
         for (int j = 0; j < a.slots; j++) {
             const int v = j < ns ? m2[j][e] : 0;
-            t_m2[j * kMbN2 * kMbN2 + e] = v;
+            t_m2[j * kMbN2X * kMbN2Y + e] = v;
             d += v;
         }
         t_d2[e] = d;
@@ -549,16 +547,16 @@ __device__ __forceinline__ void mb_prep(const KMbArgs &a)
     // g1 / 256 and R0 = g0 exactly (all dyadic, no rounding).  The stitch kernel has written that
     // sample (or the border 0 where no camera covers the pixel), so the blend kernel computes only
     // the other ("mixed") pixels and the R1 entries they read.
-    __shared__ int need_r1[kMbNR * kMbNR];
+    __shared__ int need_r1[kMbNRX * kMbNRY];
     __shared__ int n_px, n_r1;
-    int32_t *t_cnt = t_d2 + kMbN2 * kMbN2;
+    int32_t *t_cnt = t_d2 + kMbN2X * kMbN2Y;
     uint16_t *t_px = reinterpret_cast<uint16_t *>(t_cnt + kMbTabCounts);
-    uint16_t *t_r1 = t_px + kBlendTile * kBlendTile;
-    for (int e = tid; e < kMbNR * kMbNR; e += nt) need_r1[e] = 0;
+    uint16_t *t_r1 = t_px + kMbTilePx;
+    for (int e = tid; e < kMbNRX * kMbNRY; e += nt) need_r1[e] = 0;
     if (tid == 0) n_px = n_r1 = 0;
     __syncthreads();
-    for (int i = tid; i < kBlendTile * kBlendTile; i += nt) {
-        const int x = G.X0 + i % kBlendTile, y = G.Y0 + i / kBlendTile;
+    for (int i = tid; i < kMbTilePx; i += nt) {
+        const int x = G.X0 + i % kBlendTileW, y = G.Y0 + i / kBlendTileW;
         if (x >= G.W || y >= G.H) continue;
         const int o = a.owner[(int64_t)y * G.W + x];
         if (o == kBlendNone) continue;
@@ -574,8 +572,8 @@ __device__ __forceinline__ void mb_prep(const KMbArgs &a)
                 exp_taps<false>(ix[v], G.w2, zx, ux);
                 for (int b = 0; b < 3; b++)
                     for (int c = 0; c < 3; c++) {
-                        const int e2 = ix2<false>(zy[b], G.Y2, kMbN2) * kMbN2 +
-                                       ix2<false>(zx[c], G.X2, kMbN2);
+                        const int e2 = ix2<false>(zy[b], G.Y2, kMbN2Y) * kMbN2X +
+                                       ix2<false>(zx[c], G.X2, kMbN2X);
                         for (int j = 0; j < ns; j++)
                             mixed = mixed || (j != s && m2[j][e2] > 0);
                     }
@@ -584,26 +582,27 @@ __device__ __forceinline__ void mb_prep(const KMbArgs &a)
         t_px[atomicAdd(&n_px, 1)] = (uint16_t)i;
         for (int u = 0; u < 3; u++)
             for (int v = 0; v < 3; v++)
-                need_r1[ix2<false>(iy[u], G.YR, kMbNR) * kMbNR + ix2<false>(ix[v], G.XR, kMbNR)] = 1;
+                need_r1[ix2<false>(iy[u], G.YR, kMbNRY) * kMbNRX + ix2<false>(ix[v], G.XR, kMbNRX)] =
+                    1;
     }
     __syncthreads();
-    for (int e = tid; e < kMbNR * kMbNR; e += nt)
+    for (int e = tid; e < kMbNRX * kMbNRY; e += nt)
         if (need_r1[e]) t_r1[atomicAdd(&n_r1, 1)] = (uint16_t)e;
     __syncthreads();
     // Column ranges of the level arrays the mixed pixels depend on (interior tiles; mosaic-border
     // tiles keep the full arrays): R1 entries -> their level-2 taps -> the level-1 entries the R1
     // region and those taps reduce from -> the level-0 samples.  mb_levels computes only these.
     __shared__ int r1lo, r1hi, rng[6];
-    if (tid == 0) r1lo = kMbNR, r1hi = -1;
+    if (tid == 0) r1lo = kMbNRX, r1hi = -1;
     __syncthreads();
-    for (int e = tid; e < kMbNR * kMbNR; e += nt)
+    for (int e = tid; e < kMbNRX * kMbNRY; e += nt)
         if (need_r1[e]) {
-            atomicMin(&r1lo, e % kMbNR);
-            atomicMax(&r1hi, e % kMbNR);
+            atomicMin(&r1lo, e % kMbNRX);
+            atomicMax(&r1hi, e % kMbNRX);
         }
     __syncthreads();
     if (tid == 0) {
-        int a0_ = 0, b0_ = kMbUsed - 1, a1_ = 0, b1_ = kMbN1 - 1, a2_ = 0, b2_ = kMbN2 - 1;
+        int a0_ = 0, b0_ = kMbUsedX - 1, a1_ = 0, b1_ = kMbN1X - 1, a2_ = 0, b2_ = kMbN2X - 1;
         if (n_px == 0) {
             a0_ = a1_ = a2_ = 0;
             b0_ = b1_ = b2_ = -1;
@@ -616,11 +615,11 @@ __device__ __forceinline__ void mb_prep(const KMbArgs &a)
                 zhi = max(zhi, max(zi[1], zi[2]));
             }
             a2_ = max(zlo - G.X2, 0);
-            b2_ = min(zhi - G.X2, kMbN2 - 1);
+            b2_ = min(zhi - G.X2, kMbN2X - 1);
             a1_ = max(min(G.XR + r1lo, 2 * zlo - 2) - G.X1, 0);
-            b1_ = min(max(G.XR + r1hi, 2 * zhi + 2) - G.X1, kMbN1 - 1);
+            b1_ = min(max(G.XR + r1hi, 2 * zhi + 2) - G.X1, kMbN1X - 1);
             a0_ = max(2 * (a1_ + G.X1) - 2 - (G.RX + kMbFirst), 0);
-            b0_ = min(2 * (b1_ + G.X1) + 2 - (G.RX + kMbFirst), kMbUsed - 1);
+            b0_ = min(2 * (b1_ + G.X1) + 2 - (G.RX + kMbFirst), kMbUsedX - 1);
         }
         rng[0] = a0_, rng[1] = b0_, rng[2] = a1_, rng[3] = b1_, rng[4] = a2_, rng[5] = b2_;
         t_cnt[0] = n_px;
@@ -628,7 +627,7 @@ __device__ __forceinline__ void mb_prep(const KMbArgs &a)
         for (int q = 0; q < 6; q++) t_cnt[2 + q] = rng[q];
     }
     __syncthreads();
-    const int a0 = rng[0], w0 = rng[1] - rng[0] + 1, n_s = kMbUsed * w0;
+    const int a0 = rng[0], w0 = rng[1] - rng[0] + 1, n_s = kMbUsedY * w0;
     // every owner's source footprint (bounding box of its taps) ...
     __shared__ int f_rmin[kBlendSlots], f_rmax[kBlendSlots], f_bmin[kBlendSlots],
         f_bmax[kBlendSlots];
@@ -641,8 +640,8 @@ __device__ __forceinline__ void mb_prep(const KMbArgs &a)
     for (int i = tid; i < n_s * ns; i += nt) {
         const int j = i / n_s, e = i % n_s;
         const int g = mb_sample_index(e, a0, w0);
-        const int cx = refl(G.RX + kMbFirst + g % kMbUsed, G.W);
-        const int cy = refl(G.RY + kMbFirst + g / kMbUsed, G.H);
+        const int cx = refl(G.RX + kMbFirst + g % kMbUsedX, G.W);
+        const int cy = refl(G.RY + kMbFirst + g / kMbUsedX, G.H);
         const MbSrc q = mb_src<INTERP>(P, mb_slot(mask, j), cx, cy);
         atomicMin(&f_rmin[j], q.ya);
         atomicMax(&f_rmax[j], q.yb);
@@ -677,8 +676,8 @@ __device__ __forceinline__ void mb_prep(const KMbArgs &a)
     for (int i = tid; i < n_s * ns; i += nt) {
         const int j = i / n_s, e = i % n_s;
         const int g = mb_sample_index(e, a0, w0);
-        const int cx = refl(G.RX + kMbFirst + g % kMbUsed, G.W);
-        const int cy = refl(G.RY + kMbFirst + g / kMbUsed, G.H);
+        const int cx = refl(G.RX + kMbFirst + g % kMbUsedX, G.W);
+        const int cy = refl(G.RY + kMbFirst + g / kMbUsedX, G.H);
         const int sj = mb_slot(mask, j);
         const MbSrc q = mb_src<INTERP>(P, sj, cx, cy);
         int cam, w, h;
@@ -701,10 +700,10 @@ template <int CN>
 struct MbLvLds {
     uint8_t foot[MCS_MB_STAGE ? kMbFootBufs : 0][kMbFoot] __attribute__((aligned(16)));   // source footprints
     uint32_t g0[kMbU];                 // level 0: channel k in byte k
-    uint2 g1[kMbN1 * kMbN1];           // 256 G1 <= 65280 as u16 lanes: x = (c0, c2), y = (c1, c3)
+    uint2 g1[kMbN1X * kMbN1Y];         // 256 G1 <= 65280 as u16 lanes: x = (c0, c2), y = (c1, c3)
     union {
-        uint2 hs[kMbUsed * kMbN1];     // horizontal pass of level 1 (<= 4080), lanes as g1
-        int4 hs2[kMbN1 * kMbN2];       // horizontal pass of level 2, one int per channel
+        uint2 hs[kMbUsedY * kMbN1X];   // horizontal pass of level 1 (<= 4080), lanes as g1
+        int4 hs2[kMbN1Y * kMbN2X];     // horizontal pass of level 2, one int per channel
     };
 };
 
@@ -726,10 +725,11 @@ __device__ __forceinline__ void mb_levels(const KMbArgs &a, MbLvLds<CN> &L)
     // the column ranges the tile's mixed pixels depend on (mb_prep): level 0 [a0, a0 + w0),
     // level 1 [a1, a1 + w1), level 2 [a2, a2 + w2); all rows
     const int32_t *rg = a.tab + (int64_t)bt * mb_tab_words(a.slots) +
-                        a.slots * (kMbNR * kMbNR + kMbN2 * kMbN2) + kMbNR * kMbNR + kMbN2 * kMbN2 + 2;
+                        a.slots * (kMbNRX * kMbNRY + kMbN2X * kMbN2Y) + kMbNRX * kMbNRY +
+                        kMbN2X * kMbN2Y + 2;
     const int w0 = rg[1] - rg[0] + 1, a1 = rg[2], w1 = rg[3] - rg[2] + 1;
     const int a2 = rg[4], w2 = rg[5] - rg[4] + 1;
-    const int n_s = kMbUsed * w0;                    // level-0 samples (compacted columns)
+    const int n_s = kMbUsedY * w0;                   // level-0 samples (compacted columns)
     if (n_s <= 0) return;                            // no mixed pixel: nothing to do (uniform)
     const unsigned d1m = (65536u + w1 - 1) / w1, d2m = (65536u + w2 - 1) / w2;   // / w1, / w2
     int cam, w, h;
@@ -792,7 +792,7 @@ __device__ __forceinline__ void mb_levels(const KMbArgs &a, MbLvLds<CN> &L)
             }
 #pragma unroll
             for (int kk = 0; kk < KJ; kk++)
-                if (tid + kk * NT < n_s) L.g0[(dmeta[kk] >> 16) & 0xfffu] = px[kk];
+                if (tid + kk * NT < n_s) L.g0[(dmeta[kk] >> 16) & 0x1fffu] = px[kk];
         } else if (shifted) {
             struct __attribute__((packed)) U2 {
                 uint32_t x, y;
@@ -818,7 +818,7 @@ __device__ __forceinline__ void mb_levels(const KMbArgs &a, MbLvLds<CN> &L)
             }
 #pragma unroll
             for (int kk = 0; kk < KJ; kk++)
-                if (tid + kk * NT < n_s) L.g0[(dmeta[kk] >> 16) & 0xfffu] = px[kk];
+                if (tid + kk * NT < n_s) L.g0[(dmeta[kk] >> 16) & 0x1fffu] = px[kk];
         } else {
             for (int i = tid; i < n_s; i += NT) {
                 const uint64_t v = dsc[i];
@@ -829,15 +829,15 @@ __device__ __forceinline__ void mb_levels(const KMbArgs &a, MbLvLds<CN> &L)
                 mb_weights((uint32_t)(v >> 32), wa, wb);
 #pragma unroll
                 for (int k = 0; k < CN; k++) px |= mb_tap<CN>(r0, r1, wa, wb, k, 0u) << (8 * k);
-                L.g0[(uint32_t)(v >> 48) & 0xfffu] = px;
+                L.g0[(uint32_t)(v >> 48) & 0x1fffu] = px;
             }
         }
         __syncthreads();
         // single buffer: the next capture's footprint streams in during this one's reduces
         if (kMbFootBufs == 1 && staged && fl + 1 < fl1) stage(fl + 1, 0);
         const int64_t job = ((int64_t)bt * a.slots + j) * a.chunk + fl;
-        uint2 *og1 = reinterpret_cast<uint2 *>(a.g1) + job * (kMbNR * kMbNR);
-        int32_t *og2 = a.g2 + job * (kMbN2 * kMbN2 * CN);
+        uint2 *og1 = reinterpret_cast<uint2 *>(a.g1) + job * (kMbNRX * kMbNRY);
+        int32_t *og2 = a.g2 + job * (kMbN2X * kMbN2Y * CN);
         if (G.interior) {
             // separable 5-tap reduces, all channels at once in 16-bit lanes up to level 1 (the
             // sums stay below 2^16: exact), then per channel.  Level-1 entry e reads level-0
@@ -845,15 +845,15 @@ __device__ __forceinline__ void mb_levels(const KMbArgs &a, MbLvLds<CN> &L)
             // (each thread's items are computed before any is stored, so that their LDS reads
             // are not ordered behind the stores; only the needed columns, all rows)
             {
-                constexpr int IT = (kMbUsed * kMbN1 + NT - 1) / NT;
-                const int n = kMbUsed * w1;
+                constexpr int IT = (kMbUsedY * kMbN1X + NT - 1) / NT;
+                const int n = kMbUsedY * w1;
                 uint2 res[IT];
 #pragma unroll
                 for (int q = 0; q < IT; q++) {
                     const int i = min(tid + q * NT, n - 1);
                     const int r = (int)(__umul24((unsigned)i, d1m) >> 16);
                     const int e = a1 + i - (int)__umul24((unsigned)r, (unsigned)w1);
-                    const uint32_t *g = &L.g0[r * kMbUsed + 2 * e];
+                    const uint32_t *g = &L.g0[r * kMbUsedX + 2 * e];
                     uint32_t lo = 0, hi = 0;
 #pragma unroll
                     for (int v = 0; v < 5; v++) {
@@ -868,14 +868,14 @@ __device__ __forceinline__ void mb_levels(const KMbArgs &a, MbLvLds<CN> &L)
                     const int i = tid + q * NT;
                     if (i < n) {
                         const int r = (int)(__umul24((unsigned)i, d1m) >> 16);
-                        L.hs[r * kMbN1 + a1 + i - (int)__umul24((unsigned)r, (unsigned)w1)] = res[q];
+                        L.hs[r * kMbN1X + a1 + i - (int)__umul24((unsigned)r, (unsigned)w1)] = res[q];
                     }
                 }
             }
             __syncthreads();
             {
-                constexpr int IT = (kMbN1 * kMbN1 + NT - 1) / NT;
-                const int n = kMbN1 * w1;
+                constexpr int IT = (kMbN1Y * kMbN1X + NT - 1) / NT;
+                const int n = kMbN1Y * w1;
                 uint2 res[IT];
 #pragma unroll
                 for (int q = 0; q < IT; q++) {
@@ -885,7 +885,7 @@ __device__ __forceinline__ void mb_levels(const KMbArgs &a, MbLvLds<CN> &L)
                     uint32_t lo = 0, hi = 0;
 #pragma unroll
                     for (int u = 0; u < 5; u++) {
-                        const uint2 t = L.hs[(2 * ey + u) * kMbN1 + ex];
+                        const uint2 t = L.hs[(2 * ey + u) * kMbN1X + ex];
                         lo += (uint32_t)w5[u] * t.x;
                         hi += (uint32_t)w5[u] * t.y;
                     }
@@ -896,51 +896,52 @@ __device__ __forceinline__ void mb_levels(const KMbArgs &a, MbLvLds<CN> &L)
                     const int i = tid + q * NT;
                     if (i < n) {
                         const int ey = (int)(__umul24((unsigned)i, d1m) >> 16);
-                        L.g1[ey * kMbN1 + a1 + i - (int)__umul24((unsigned)ey, (unsigned)w1)] = res[q];
+                        L.g1[ey * kMbN1X + a1 + i - (int)__umul24((unsigned)ey, (unsigned)w1)] =
+                            res[q];
                     }
                 }
             }
             __syncthreads();
-            for (int i = tid; i < kMbN1 * w2; i += NT) {
+            for (int i = tid; i < kMbN1Y * w2; i += NT) {
                 const int r = (int)(__umul24((unsigned)i, d2m) >> 16);
                 const int e = a2 + i - (int)__umul24((unsigned)r, (unsigned)w2);
                 int acc[4] = {0, 0, 0, 0};
 #pragma unroll
                 for (int v = 0; v < 5; v++) {
-                    const uint2 t = L.g1[r * kMbN1 + 2 * e + v];
+                    const uint2 t = L.g1[r * kMbN1X + 2 * e + v];
 #pragma unroll
                     for (int k = 0; k < CN; k++) acc[k] += w5[v] * ch16(t, k);
                 }
-                L.hs2[r * kMbN2 + e] = make_int4(acc[0], acc[1], acc[2], acc[3]);
+                L.hs2[r * kMbN2X + e] = make_int4(acc[0], acc[1], acc[2], acc[3]);
             }
             __syncthreads();
-            for (int i = tid; i < kMbN2 * w2; i += NT) {
+            for (int i = tid; i < kMbN2Y * w2; i += NT) {
                 const int ey = (int)(__umul24((unsigned)i, d2m) >> 16);
                 const int ex = a2 + i - (int)__umul24((unsigned)ey, (unsigned)w2);
                 int acc[4] = {0, 0, 0, 0};
 #pragma unroll
                 for (int u = 0; u < 5; u++) {
-                    const int4 t = L.hs2[(2 * ey + u) * kMbN2 + ex];
+                    const int4 t = L.hs2[(2 * ey + u) * kMbN2X + ex];
                     acc[0] += w5[u] * t.x;
                     acc[1] += w5[u] * t.y;
                     acc[2] += w5[u] * t.z;
                     acc[3] += w5[u] * t.w;
                 }
 #pragma unroll
-                for (int k = 0; k < CN; k++) og2[k * (kMbN2 * kMbN2) + ey * kMbN2 + ex] = acc[k];
+                for (int k = 0; k < CN; k++) og2[k * (kMbN2X * kMbN2Y) + ey * kMbN2X + ex] = acc[k];
             }
         } else {
             // mosaic-border tiles: 25-tap form with reflection at every level
             const int RX2 = G.RX + kMbFirst, RY2 = G.RY + kMbFirst;
-            for (int e = tid; e < kMbN1 * kMbN1; e += NT) {
-                const int qx = refl(G.X1 + e % kMbN1, G.w1), qy = refl(G.Y1 + e / kMbN1, G.h1);
+            for (int e = tid; e < kMbN1X * kMbN1Y; e += NT) {
+                const int qx = refl(G.X1 + e % kMbN1X, G.w1), qy = refl(G.Y1 + e / kMbN1X, G.h1);
                 uint32_t lo = 0, hi = 0;
                 for (int u = 0; u < 5; u++) {
-                    const int cy = ix2<false>(refl(2 * qy + u - 2, G.H), RY2, kMbUsed);
+                    const int cy = ix2<false>(refl(2 * qy + u - 2, G.H), RY2, kMbUsedY);
 #pragma unroll
                     for (int v = 0; v < 5; v++) {
-                        const int cx = ix2<false>(refl(2 * qx + v - 2, G.W), RX2, kMbUsed);
-                        const uint32_t t = L.g0[cy * kMbUsed + cx], wt = w5[u] * w5[v];
+                        const int cx = ix2<false>(refl(2 * qx + v - 2, G.W), RX2, kMbUsedX);
+                        const uint32_t t = L.g0[cy * kMbUsedX + cx], wt = w5[u] * w5[v];
                         lo += wt * (t & 0x00ff00ffu);
                         hi += wt * ((t >> 8) & 0x00ff00ffu);
                     }
@@ -948,41 +949,41 @@ __device__ __forceinline__ void mb_levels(const KMbArgs &a, MbLvLds<CN> &L)
                 L.g1[e] = make_uint2(lo, hi);
             }
             __syncthreads();
-            for (int e = tid; e < kMbN2 * kMbN2; e += NT) {
-                const int zx = refl(G.X2 + e % kMbN2, G.w2), zy = refl(G.Y2 + e / kMbN2, G.h2);
+            for (int e = tid; e < kMbN2X * kMbN2Y; e += NT) {
+                const int zx = refl(G.X2 + e % kMbN2X, G.w2), zy = refl(G.Y2 + e / kMbN2X, G.h2);
                 int acc[4] = {0, 0, 0, 0};
                 for (int u = 0; u < 5; u++) {
-                    const int qy = ix2<false>(refl(2 * zy + u - 2, G.h1), G.Y1, kMbN1);
+                    const int qy = ix2<false>(refl(2 * zy + u - 2, G.h1), G.Y1, kMbN1Y);
 #pragma unroll
                     for (int v = 0; v < 5; v++) {
-                        const int qx = ix2<false>(refl(2 * zx + v - 2, G.w1), G.X1, kMbN1);
-                        const uint2 t = L.g1[qy * kMbN1 + qx];
+                        const int qx = ix2<false>(refl(2 * zx + v - 2, G.w1), G.X1, kMbN1X);
+                        const uint2 t = L.g1[qy * kMbN1X + qx];
                         const int wt = w5[u] * w5[v];
 #pragma unroll
                         for (int k = 0; k < CN; k++) acc[k] += wt * ch16(t, k);
                     }
                 }
 #pragma unroll
-                for (int k = 0; k < CN; k++) og2[k * (kMbN2 * kMbN2) + e] = acc[k];
+                for (int k = 0; k < CN; k++) og2[k * (kMbN2X * kMbN2Y) + e] = acc[k];
             }
         }
-        // the R1 region of g1 (level-1 entries [kMbRS, kMbRS + 18) of the 27-entry array)
-        for (int e = tid; e < kMbNR * kMbNR; e += NT)
-            og1[e] = L.g1[(e / kMbNR + kMbRS) * kMbN1 + e % kMbNR + kMbRS];
+        // the R1 region of g1 (level-1 entries from kMbRS on, both axes)
+        for (int e = tid; e < kMbNRX * kMbNRY; e += NT)
+            og1[e] = L.g1[(e / kMbNRX + kMbRS) * kMbN1X + e % kMbNRX + kMbRS];
         __syncthreads();   // the next capture overwrites level 0 and the pass arrays
     }
 }
 
 // ---- blend: grid (listed tiles, nf), block kMbBlThreads ------------------------------------------
-template <int CN>
+template <int CN, int S>
 struct MbBlLds {
-    uint2 g1[kBlendSlots][kMbNR * kMbNR];   // packed as in mb_levels
-    int32_t g2[kBlendSlots][CN][kMbN2 * kMbN2];   // channel-planar: indices need no * CN
-    double b2[CN][kMbN2 * kMbN2];
-    double r1[CN][kMbNR * kMbNR];
+    uint2 g1[S][kMbNRX * kMbNRY];      // packed as in mb_levels
+    int32_t g2[S][CN][kMbN2X * kMbN2Y];   // channel-planar: indices need no * CN
+    double b2[CN][kMbN2X * kMbN2Y];
+    double r1[CN][kMbNRX * kMbNRY];
 };
 
-constexpr int kMbPQ = kBlendTile * kBlendTile / kMbBlThreads;   // tile pixels per thread
+constexpr int kMbPQ = kMbTilePx / kMbBlThreads;   // tile pixels per thread
 template <int CN>
 struct MbPix {
     int i[kMbPQ];            // the thread's mixed pixels (tile index, -1: none)
@@ -990,30 +991,30 @@ struct MbPix {
     uint32_t v[kMbPQ];       // its owner sample (the stitch kernel's output), channel k in byte k
 };
 
-template <int CN, bool IN>
-__device__ __forceinline__ void mb_blend_tile(const KMbArgs &a, const MbGeo &G, MbBlLds<CN> &L,
+template <int CN, int S, bool IN>
+__device__ __forceinline__ void mb_blend_tile(const KMbArgs &a, const MbGeo &G, MbBlLds<CN, S> &L,
                                               const MbPix<CN> &px, uint32_t mask, int ns, int f)
 {
     const KParams &P = a.P;
     const int tid = threadIdx.x, nt = blockDim.x;
     const int32_t *tab = a.tab + (int64_t)blockIdx.x * mb_tab_words(a.slots);
-    const int32_t *t_m1 = tab, *t_m2 = tab + a.slots * kMbNR * kMbNR;
-    const int32_t *t_d1 = t_m2 + a.slots * kMbN2 * kMbN2, *t_d2 = t_d1 + kMbNR * kMbNR;
+    const int32_t *t_m1 = tab, *t_m2 = tab + a.slots * kMbNRX * kMbNRY;
+    const int32_t *t_d1 = t_m2 + a.slots * kMbN2X * kMbN2Y, *t_d2 = t_d1 + kMbNRX * kMbNRY;
     // (24-bit multiplies: full-rate v_mul_u32_u24 instead of quarter-rate v_mul_lo_u32)
     auto i2 = [&](int cx, int cy) {
-        return (int)__umul24((unsigned)ix2<IN>(cy, G.Y2, kMbN2), kMbN2) + ix2<IN>(cx, G.X2, kMbN2);
+        return (int)__umul24((unsigned)ix2<IN>(cy, G.Y2, kMbN2Y), kMbN2X) + ix2<IN>(cx, G.X2, kMbN2X);
     };
     auto ir = [&](int cx, int cy) {   // the R1 region (g1, m1, d1, r1)
-        return (int)__umul24((unsigned)ix2<IN>(cy, G.YR, kMbNR), kMbNR) + ix2<IN>(cx, G.XR, kMbNR);
+        return (int)__umul24((unsigned)ix2<IN>(cy, G.YR, kMbNRY), kMbNRX) + ix2<IN>(cx, G.XR, kMbNRX);
     };
     // B2 = sum m2 g2 / (sum m2 * 65536)
-    for (int e = tid; e < kMbN2 * kMbN2; e += nt) {
+    for (int e = tid; e < kMbN2X * kMbN2Y; e += nt) {
         // (integer sums in double: every product < 2^41, every sum < 2^43 -- exact)
         double num[CN];
 #pragma unroll
         for (int k = 0; k < CN; k++) num[k] = 0.0;
         for (int j = 0; j < ns; j++) {
-            const double m = (double)t_m2[__umul24((unsigned)j, kMbN2 * kMbN2) + e];
+            const double m = (double)t_m2[__umul24((unsigned)j, kMbN2X * kMbN2Y) + e];
 #pragma unroll
             for (int k = 0; k < CN; k++) num[k] += m * (double)L.g2[j][k][e];
         }
@@ -1024,13 +1025,12 @@ __device__ __forceinline__ void mb_blend_tile(const KMbArgs &a, const MbGeo &G, 
     }
     __syncthreads();
     // R1 = B1 + up(B2), B1 = sum m1 (16384 g1 - E(g2)) / (sum m1 * 4194304)
-    const int n_r1 = t_d2[kMbN2 * kMbN2 + 1];
+    const int n_r1 = t_d2[kMbN2X * kMbN2Y + 1];
     const uint16_t *t_r1 =
-        reinterpret_cast<const uint16_t *>(t_d2 + kMbN2 * kMbN2 + kMbTabCounts) +
-        kBlendTile * kBlendTile;
+        reinterpret_cast<const uint16_t *>(t_d2 + kMbN2X * kMbN2Y + kMbTabCounts) + kMbTilePx;
     for (int l = tid; l < n_r1; l += nt) {
         const int e = t_r1[l];
-        const int ey = div_small<kMbNR>(e), ex = e - (int)__umul24((unsigned)ey, kMbNR);
+        const int ey = div_small<kMbNRX>(e), ex = e - (int)__umul24((unsigned)ey, kMbNRX);
         const int qx = rf<IN>(G.XR + ex, G.w1), qy = rf<IN>(G.YR + ey, G.h1);
         int iy[3], wy[3], ix[3], wx[3];
         exp_taps<IN>(qy, G.h2, iy, wy);
@@ -1058,7 +1058,7 @@ __device__ __forceinline__ void mb_blend_tile(const KMbArgs &a, const MbGeo &G, 
                 for (int k = 0; k < CN; k++)   // (tw <= 36, g2 < 2^24: a 24-bit multiply)
                     e2[k] += (int)__umul24((unsigned)tw[t], (unsigned)L.g2[j][k][tp[t]]);
             const uint2 g1 = L.g1[j][p1];
-            const double m = (double)t_m1[__umul24((unsigned)j, kMbNR * kMbNR) + p1];
+            const double m = (double)t_m1[__umul24((unsigned)j, kMbNRX * kMbNRY) + p1];
 #pragma unroll
             for (int k = 0; k < CN; k++) num[k] += m * (double)(16384 * ch16(g1, k) - e2[k]);
         }
@@ -1085,7 +1085,7 @@ __device__ __forceinline__ void mb_blend_tile(const KMbArgs &a, const MbGeo &G, 
     for (int q = 0; q < kMbPQ; q++) {
         const int i = px.i[q];
         if (i < 0) continue;
-        const int x = G.X0 + (i % kBlendTile), y = G.Y0 + i / kBlendTile;
+        const int x = G.X0 + (i % kBlendTileW), y = G.Y0 + i / kBlendTileW;
         // (global address space: the stores cannot alias the LDS arrays read by later pixels)
         typedef __attribute__((address_space(1))) uint8_t gu8;
         gu8 *po = (gu8 *)(P.out + (int64_t)f * P.out_fstride + (int64_t)y * P.out_pitch + x * CN);
@@ -1126,8 +1126,8 @@ __device__ __forceinline__ void mb_blend_tile(const KMbArgs &a, const MbGeo &G, 
     }
 }
 
-template <int CN>
-__device__ __forceinline__ void mb_blend(const KMbArgs &a, MbBlLds<CN> &L)
+template <int CN, int S>
+__device__ __forceinline__ void mb_blend(const KMbArgs &a, MbBlLds<CN, S> &L)
 {
     typedef __attribute__((address_space(1))) const uint8_t cgu8;
     typedef __attribute__((address_space(1))) const uint2 cgu2;
@@ -1143,8 +1143,8 @@ __device__ __forceinline__ void mb_blend(const KMbArgs &a, MbBlLds<CN> &L)
     int n_px;
     {
         const cgi32 *tc = (const cgi32 *)a.tab + (int64_t)bt * mb_tab_words(a.slots) +
-                          a.slots * (kMbNR * kMbNR + kMbN2 * kMbN2) + kMbNR * kMbNR +
-                          kMbN2 * kMbN2;
+                          a.slots * (kMbNRX * kMbNRY + kMbN2X * kMbN2Y) + kMbNRX * kMbNRY +
+                          kMbN2X * kMbN2Y;
         typedef __attribute__((address_space(1))) const uint16_t cgu16;
         n_px = tc[0];
         const cgu16 *lp = (const cgu16 *)(tc + kMbTabCounts);
@@ -1158,7 +1158,7 @@ __device__ __forceinline__ void mb_blend(const KMbArgs &a, MbBlLds<CN> &L)
 #pragma unroll
     for (int q = 0; q < kMbPQ; q++) {
         const int i = px.i[q];
-        const int x = G.X0 + (i % kBlendTile), y = G.Y0 + i / kBlendTile;
+        const int x = G.X0 + (i % kBlendTileW), y = G.Y0 + i / kBlendTileW;
         px.own[q] = kBlendNone;
         px.v[q] = 0;
         if (i >= 0) {
@@ -1169,37 +1169,37 @@ __device__ __forceinline__ void mb_blend(const KMbArgs &a, MbBlLds<CN> &L)
             for (int k = 0; k < CN; k++) px.v[q] |= (uint32_t)po[k] << (8 * k);
         }
     }
-    constexpr int N1 = (kMbNR * kMbNR + kMbBlThreads - 1) / kMbBlThreads;
-    constexpr int N2 = (kMbN2 * kMbN2 * CN + kMbBlThreads - 1) / kMbBlThreads;
-    uint2 r1[kBlendSlots][N1];
-    int32_t r2[kBlendSlots][N2];
+    constexpr int N1 = (kMbNRX * kMbNRY + kMbBlThreads - 1) / kMbBlThreads;
+    constexpr int N2 = (kMbN2X * kMbN2Y * CN + kMbBlThreads - 1) / kMbBlThreads;
+    uint2 r1[S][N1];
+    int32_t r2[S][N2];
 #pragma unroll
-    for (int j = 0; j < kBlendSlots; j++) {
+    for (int j = 0; j < S; j++) {
         if (j >= ns) break;
         const int64_t job = ((int64_t)bt * a.slots + j) * a.chunk + fl;
-        const cgu2 *s1 = (const cgu2 *)a.g1 + job * (kMbNR * kMbNR);
-        const cgi32 *s2 = (const cgi32 *)a.g2 + job * (kMbN2 * kMbN2 * CN);
+        const cgu2 *s1 = (const cgu2 *)a.g1 + job * (kMbNRX * kMbNRY);
+        const cgi32 *s2 = (const cgi32 *)a.g2 + job * (kMbN2X * kMbN2Y * CN);
 #pragma unroll
         for (int q = 0; q < N1; q++)
-            r1[j][q] = s1[min(tid + q * kMbBlThreads, kMbNR * kMbNR - 1)];
+            r1[j][q] = s1[min(tid + q * kMbBlThreads, kMbNRX * kMbNRY - 1)];
 #pragma unroll
         for (int q = 0; q < N2; q++)
-            r2[j][q] = s2[min(tid + q * kMbBlThreads, kMbN2 * kMbN2 * CN - 1)];
+            r2[j][q] = s2[min(tid + q * kMbBlThreads, kMbN2X * kMbN2Y * CN - 1)];
     }
 #pragma unroll
-    for (int j = 0; j < kBlendSlots; j++) {
+    for (int j = 0; j < S; j++) {
         if (j >= ns) break;
 #pragma unroll
         for (int q = 0; q < N1; q++)
-            if (tid + q * kMbBlThreads < kMbNR * kMbNR) L.g1[j][tid + q * kMbBlThreads] = r1[j][q];
+            if (tid + q * kMbBlThreads < kMbNRX * kMbNRY) L.g1[j][tid + q * kMbBlThreads] = r1[j][q];
 #pragma unroll
         for (int q = 0; q < N2; q++)
-            if (tid + q * kMbBlThreads < kMbN2 * kMbN2 * CN)
+            if (tid + q * kMbBlThreads < kMbN2X * kMbN2Y * CN)
                 (&L.g2[j][0][0])[tid + q * kMbBlThreads] = r2[j][q];
     }
     __syncthreads();
-    if (G.interior) mb_blend_tile<CN, true>(a, G, L, px, mask, ns, f);
-    else mb_blend_tile<CN, false>(a, G, L, px, mask, ns, f);
+    if (G.interior) mb_blend_tile<CN, S, true>(a, G, L, px, mask, ns, f);
+    else mb_blend_tile<CN, S, false>(a, G, L, px, mask, ns, f);
 }
 
 }  // namespace mcs

@@ -85,7 +85,7 @@ struct Kernels {
     hipFunction_t feather[5][2] = {};     // [channels][interp]
     hipFunction_t mb_prep[5][2] = {};     // [channels][interp]
     hipFunction_t mb_levels[5] = {};      // [channels]
-    hipFunction_t mb_blend[5] = {};       // [channels]
+    hipFunction_t mb_blend[5][2] = {};    // [channels][<= 2 owners : <= 4]
 };
 Kernels g_k[kMaxDevices];
 std::mutex g_k_mu;
@@ -109,8 +109,10 @@ int kernels(const Api *A, int device, const Kernels **out)
             if (rc == MCS_OK) rc = fn(name, &k.resize[c]);
             snprintf(name, sizeof(name), "mcs_mb_levels_c%d", c);
             if (rc == MCS_OK) rc = fn(name, &k.mb_levels[c]);
-            snprintf(name, sizeof(name), "mcs_mb_blend_c%d", c);
-            if (rc == MCS_OK) rc = fn(name, &k.mb_blend[c]);
+            snprintf(name, sizeof(name), "mcs_mb_blend_c%d_s2", c);
+            if (rc == MCS_OK) rc = fn(name, &k.mb_blend[c][0]);
+            snprintf(name, sizeof(name), "mcs_mb_blend_c%d_s4", c);
+            if (rc == MCS_OK) rc = fn(name, &k.mb_blend[c][1]);
             for (int i = 0; i < 2 && rc == MCS_OK; i++) {
                 snprintf(name, sizeof(name), "mcs_prepare_c%d_i%d", c, i);
                 rc = fn(name, &k.prepare[c][i]);
@@ -224,18 +226,18 @@ int prepare_multiband(const Api *A, mcs_plan *p, const Kernels *k, hipStream_t s
         if (w * h * C >= (int64_t(1) << 31))
             return mcs::fail(MCS_E_UNSUPPORTED, "multi-band: camera frames must be < 2 GiB");
     }
-    const int64_t per_f = (int64_t)n * S * (mcs::kMbNRPx * mcs::kMbNRPx * 8 +
-                                            mcs::kMbN2Px * mcs::kMbN2Px * C * 4);
+    const int64_t per_f = (int64_t)n * S * (mcs::kMbNRX * mcs::kMbNRY * 8 +
+                                            mcs::kMbN2X * mcs::kMbN2Y * C * 4);
     int chunk = (int)std::max<int64_t>(1, std::min<int64_t>(64, mcs::kMbScratchBytes / per_f));
     if (chunk > mcs::kMbLvFrames) chunk -= chunk % mcs::kMbLvFrames;
-    const int64_t samples = (int64_t)mcs::kMbUsedPx * mcs::kMbUsedPx;
+    const int64_t samples = (int64_t)mcs::kMbUsedX * mcs::kMbUsedY;
     HIP_TRY(A->hipMalloc((void **)&p->d_mbdesc, (size_t)(n * S * samples) * sizeof(uint64_t)));
     HIP_TRY(A->hipMalloc((void **)&p->d_mbtab, (size_t)n * mcs::mb_tab_words(S) * sizeof(int32_t)));
     HIP_TRY(A->hipMalloc((void **)&p->d_mbfoot, (size_t)n * S * 8 * sizeof(int32_t)));
     HIP_TRY(A->hipMalloc((void **)&p->d_mbg1,
-                         (size_t)n * S * chunk * mcs::kMbNRPx * mcs::kMbNRPx * 8));
+                         (size_t)n * S * chunk * mcs::kMbNRX * mcs::kMbNRY * 8));
     HIP_TRY(A->hipMalloc((void **)&p->d_mbg2,
-                         (size_t)n * S * chunk * mcs::kMbN2Px * mcs::kMbN2Px * C * 4));
+                         (size_t)n * S * chunk * mcs::kMbN2X * mcs::kMbN2Y * C * 4));
     p->mb_chunk = chunk;
     mcs::KMbArgs a;
     mb_args(p, p->kp, a);
@@ -247,8 +249,8 @@ int prepare_multiband(const Api *A, mcs_plan *p, const Kernels *k, hipStream_t s
 int prepare_blend(const Api *A, mcs_plan *p, const Kernels *k, hipStream_t s)
 {
     const int W = p->fd.out_w, H = p->fd.out_h;
-    const int bx = (W + mcs::kBlendTile - 1) / mcs::kBlendTile;
-    const int by = (H + mcs::kBlendTile - 1) / mcs::kBlendTile;
+    const int bx = (W + mcs::kBlendTileW - 1) / mcs::kBlendTileW;
+    const int by = (H + mcs::kBlendTileH - 1) / mcs::kBlendTileH;
     const size_t nt = (size_t)bx * by;
     HIP_TRY(A->hipMalloc((void **)&p->d_owner, (size_t)W * H));
     HIP_TRY(A->hipMalloc((void **)&p->d_binfo, nt * 2 * sizeof(uint32_t)));
@@ -468,7 +470,8 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
                 m.f0 = f0;
                 m.nf = nf;
                 if (rc == MCS_OK)
-                    rc = launch_args(A, k->mb_blend[p->fd.channels], (unsigned)p->n_blend,
+                    rc = launch_args(A, k->mb_blend[p->fd.channels][p->mb_slots <= 2 ? 0 : 1],
+                                     (unsigned)p->n_blend,
                                      (unsigned)nf, mcs::kMbBlThreads, 1, &m, sizeof(m), s);
             }
         }

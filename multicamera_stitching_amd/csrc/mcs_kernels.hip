@@ -970,16 +970,23 @@ extern "C" __global__ __launch_bounds__(256) void mcs_blend_classify(const mcs::
 #define MCS_MB_WAVES 4
 #endif
 #define MCS_MB_ENTRY(CN)                                                                       \
-    extern "C" __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(MCS_MB_WAVES))) \
+    extern "C" __global__ __launch_bounds__(MCS_MB_LV_THREADS) __attribute__((amdgpu_waves_per_eu(MCS_MB_WAVES))) \
     void mcs_mb_levels_c##CN(const mcs::KMbArgs a)                                             \
     {                                                                                          \
         __shared__ mcs::MbLvLds<CN> lds;                                                       \
         mcs::mb_levels<CN>(a, lds);                                                            \
     }                                                                                          \
-    extern "C" __global__ __launch_bounds__(256) void mcs_mb_blend_c##CN(const mcs::KMbArgs a)  \
+    extern "C" __global__ __launch_bounds__(256) void mcs_mb_blend_c##CN##_s2(                \
+        const mcs::KMbArgs a)                                                                  \
     {                                                                                          \
-        __shared__ mcs::MbBlLds<CN> lds;                                                       \
-        mcs::mb_blend<CN>(a, lds);                                                             \
+        __shared__ mcs::MbBlLds<CN, 2> lds;                                                    \
+        mcs::mb_blend<CN, 2>(a, lds);                                                          \
+    }                                                                                          \
+    extern "C" __global__ __launch_bounds__(256) void mcs_mb_blend_c##CN##_s4(                \
+        const mcs::KMbArgs a)                                                                  \
+    {                                                                                          \
+        __shared__ mcs::MbBlLds<CN, 4> lds;                                                    \
+        mcs::mb_blend<CN, 4>(a, lds);                                                          \
     }
 MCS_MB_ENTRY(1)
 MCS_MB_ENTRY(2)

@@ -130,30 +130,43 @@ struct KResizeArgs {
 };
 constexpr int kResizeBlock = 256;
 
-// Blended modes (mcs_blend.h): 32 x 32 output tiles, 16-px pyramid halo, <= 4 owners per
+// Blended modes (mcs_blend.h): 32 x 64 output tiles (tall: the seams of a horizontal rig run
+// vertically, so a tall tile shares its pyramid rows), 16-px pyramid halo, <= 4 owners per
 // multi-band neighbourhood, owner map byte 255 = no camera.
-constexpr int kBlendTile = 32;
+#ifndef MCS_BLEND_TILE_H
+#define MCS_BLEND_TILE_H 64
+#endif
+constexpr int kBlendTileW = 32;
+constexpr int kBlendTileH = MCS_BLEND_TILE_H;
 constexpr int kBlendHalo = 16;
 constexpr int kBlendSlots = 4;
 constexpr int kBlendNone = 255;
 // multi-band kernels (mcs_blend.h): prep once per plan, then per chunk of captures levels + blend
 constexpr int kMbPrepThreads = 256;
-constexpr int kMbLvThreads = 512;
+#ifndef MCS_MB_LV_THREADS
+#define MCS_MB_LV_THREADS 512
+#endif
+constexpr int kMbLvThreads = MCS_MB_LV_THREADS;
 constexpr int kMbLvFrames = 8;      // captures per levels block (sample windows held in registers)
 constexpr int kMbBlThreads = 256;
 constexpr int64_t kMbScratchBytes = 1ll << 30;    // level scratch budget per plan (<= 64 captures)
-constexpr int kMbUsedPx = 57;       // level-0 neighbourhood side a tile's pyramid reads
-constexpr int kMbNRPx = 18;         // R1 region side (level 1)
-constexpr int kMbN2Px = 12;         // level-2 side
+// The pyramid arrays a tile holds, per axis (tile side T): level 0 [O - 14, O + T + 10]
+// (T + 25), level 1 [O/2 - 6, O/2 + T/2 + 4] (T/2 + 11), level 2 [O/4 - 2, O/4 + T/4 + 1]
+// (T/4 + 4), the collapsed level 1 ("R1 region") [O/2 - 1, O/2 + T/2] (T/2 + 2).
+constexpr int kMbUsedX = kBlendTileW + 25, kMbUsedY = kBlendTileH + 25;
+constexpr int kMbN1X = kBlendTileW / 2 + 11, kMbN1Y = kBlendTileH / 2 + 11;
+constexpr int kMbN2X = kBlendTileW / 4 + 4, kMbN2Y = kBlendTileH / 4 + 4;
+constexpr int kMbNRX = kBlendTileW / 2 + 2, kMbNRY = kBlendTileH / 2 + 2;
+constexpr int kMbTilePx = kBlendTileW * kBlendTileH;
 // per-tile table (int32 words): m1 (R1 region) [slots], m2 [slots], d1 (R1 region), d2, then
 // the work lists: n_px, n_r1, the level-0 / level-1 / level-2 column ranges (first, last) the
-// mixed pixels depend on, the tile pixels to blend (u16, 1024 slots) and the R1 entries they
-// read (u16, 18 * 18 slots)
+// mixed pixels depend on, the tile pixels to blend (u16, one per tile pixel) and the R1 entries
+// they read (u16, one per R1 entry)
 constexpr int kMbTabCounts = 8;
-constexpr int kMbTabLists = kMbTabCounts + 32 * 32 / 2 + kMbNRPx * kMbNRPx / 2;
+constexpr int kMbTabLists = kMbTabCounts + kMbTilePx / 2 + (kMbNRX * kMbNRY + 1) / 2;
 constexpr int mb_tab_words(int slots)
 {
-    return slots * (kMbNRPx * kMbNRPx + kMbN2Px * kMbN2Px) + kMbNRPx * kMbNRPx + kMbN2Px * kMbN2Px +
+    return slots * (kMbNRX * kMbNRY + kMbN2X * kMbN2Y) + kMbNRX * kMbNRY + kMbN2X * kMbN2Y +
            kMbTabLists;
 }
 struct KBlendPrepArgs {
@@ -168,11 +181,11 @@ struct KMbArgs {
     KParams P;
     const uint8_t *owner;          // owner map of the mosaic
     const int *list;               // blend tile list: list[1 + 2i] = tile, list[2 + 2i] = mask
-    uint64_t *desc;                // [tiles][slots][57 * 57] level-0 sample windows (prep)
+    uint64_t *desc;                // [tiles][slots][kMbUsedX * kMbUsedY] level-0 samples (prep)
     int32_t *tab;                  // [tiles][mb_tab_words(slots)] masks + denominators (prep)
     int32_t *foot;                 // [tiles][slots][8] source footprint per owner (prep)
-    uint16_t *g1;                  // scratch [tiles][slots][chunk][18 * 18][4] (u16 lanes)
-    int32_t *g2;                   // scratch [tiles][slots][chunk][12 * 12 * CN]
+    uint16_t *g1;                  // scratch [tiles][slots][chunk][R1 region][4] (u16 lanes)
+    int32_t *g2;                   // scratch [tiles][slots][chunk][CN][level 2]
     int slots;                     // owners per tile (the tables' slot dimension)
     int chunk;                     // scratch capture stride
     int f0, nf;                    // captures [f0, f0 + nf) of this launch
