@@ -249,7 +249,7 @@ def main():
             "plan": {"prepare_ms_once": round(prep_ms, 3), "tiles": plan_stats["tiles"],
                      "lds_tiles": plan_stats["lds_tiles"],
                      "direct_tiles": plan_stats["direct_tiles"],
-                     "blend_tiles_32px": plan_stats["blend_tiles"],
+                     "blend_tiles_32x64": plan_stats["blend_tiles"],
                      "table_mb": round(plan_stats["table_bytes"] / 1e6, 2)},
             "kernels": {"launch_ms": round(launch_ms, 4),
                         "paste_only_launch_ms": None if paste_ms is None else round(paste_ms, 4)},
