@@ -404,7 +404,13 @@ extern "C" __global__ __launch_bounds__(256) void mcs_orb_nms(const mcs::KOrbLev
             if (dx || dy) keep = keep && c > s[dy * a.w + dx];
     if (!keep) return;
     const double r = mcs::orb_harris(a.img + (int64_t)y * a.w + x, a.w);
-    const int i = atomicAdd(a.ncand, 1);
+    // one atomic per wave: the surviving lanes (the active ones here) take consecutive slots
+    // (their order is irrelevant: the host ranks each level's candidates)
+    const unsigned long long act = __ballot(1);
+    const int lane = __lane_id(), leader = __ffsll((long long)act) - 1;
+    int base = 0;
+    if (lane == leader) base = atomicAdd(a.ncand, __popcll(act));
+    const int i = __shfl(base, leader) + __popcll(act & ((1ull << lane) - 1ull));
     if (i < a.cap) {
         a.cand[i].x = x;
         a.cand[i].y = y;
