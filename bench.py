@@ -266,6 +266,12 @@ def main():
                 "traffic": traffic,
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 "kernel_ms_per_launch": round(launch_ms, 4),
+                # the HBM-bound streaming kernel alone (the paste-only launch: the same gather
+                # over every tile without the blend passes), same algorithmic bytes
+                "stream_kernel": None if paste_ms is None else {
+                    "achieved": round(bytes_per_launch / (paste_ms * 1e-3) / 1e9, 1),
+                    "frac": round(bytes_per_launch / (paste_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                    "ms_per_launch": round(paste_ms, 4)},
             },
             "cpu_baseline": cpu,
         }
