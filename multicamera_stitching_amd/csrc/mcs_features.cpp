@@ -501,7 +501,10 @@ int mcs_orb_detect_host(const uint8_t *image, int w, int h, int channels, int nf
     rc = workspace(A, device, o, &buf, &s);
     if (rc) return rc;
     std::vector<int> counts(nlevels);
-    std::vector<mcs::OrbCand> cand(cap_total);
+    // host copy of the candidates: per thread, grown on demand, never cleared (only the
+    // entries the counts cover are copied and read)
+    static thread_local std::vector<mcs::OrbCand> cand;
+    if (cand.size() < cap_total) cand.resize(cap_total);
     std::vector<int> kp;
     std::vector<double> orient, resp;
     uint8_t *lvl0 = buf + o_lvl;
@@ -542,9 +545,16 @@ int mcs_orb_detect_host(const uint8_t *image, int w, int h, int channels, int nf
     if (e == hipSuccess && rc == MCS_OK)
         e = A->hipMemcpyAsync(counts.data(), buf + o_cnt, nlevels * sizeof(int),
                               hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess && rc == MCS_OK)
-        e = A->hipMemcpyAsync(cand.data(), buf + o_cand, cap_total * sizeof(mcs::OrbCand),
-                              hipMemcpyDeviceToHost, s);
+    // counts first, then only the candidates each level found (a small fraction of the
+    // capacity): the copy-back is sized by the image's corners, not by its area
+    if (e == hipSuccess && rc == MCS_OK) e = A->hipStreamSynchronize(s);
+    for (int l = 0; l < nlevels && e == hipSuccess && rc == MCS_OK; l++) {
+        const int c = std::min(std::max(counts[l], 0), (int)cap[l]);
+        if (c > 0)
+            e = A->hipMemcpyAsync(cand.data() + coff[l],
+                                  buf + o_cand + coff[l] * sizeof(mcs::OrbCand),
+                                  (size_t)c * sizeof(mcs::OrbCand), hipMemcpyDeviceToHost, s);
+    }
     if (e == hipSuccess && rc == MCS_OK) e = A->hipStreamSynchronize(s);
     int n = 0;
     if (e == hipSuccess && rc == MCS_OK) {
