@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstring>
 #include <mutex>
 
 #include <vector>
@@ -526,27 +527,35 @@ int mcs_orb_detect_host(const uint8_t *image, int w, int h, int channels, int nf
         rc = mcs_resize_linear_device(buf + o_lvl + off[l - 1], lw[l - 1], lh[l - 1], lw[l - 1],
                                       0, buf + o_lvl + off[l], lw[l], lh[l], lw[l], 0, 1, 1,
                                       device, s);
-    for (int l = 0; l < nlevels && e == hipSuccess && rc == MCS_OK; l++) {
-        mcs::KOrbLevelArgs la;
-        la.img = buf + o_lvl + off[l];
-        la.hblur = reinterpret_cast<uint16_t *>(buf + o_h16) + off[l];
-        la.blur = buf + o_blur + off[l];
-        la.score = buf + o_score + off[l];
-        la.cand = reinterpret_cast<mcs::OrbCand *>(buf + o_cand) + coff[l];
-        la.ncand = reinterpret_cast<int *>(buf + o_cnt) + l;
-        la.w = lw[l];
-        la.h = lh[l];
-        la.threshold = fast_threshold;
-        la.cap = (int)cap[l];
-        const unsigned gx = (unsigned)(lw[l] + 255) / 256;
+    if (e == hipSuccess && rc == MCS_OK) {
+        // blur, FAST and NMS of every level: one launch each
+        mcs::KOrbPyrArgs pa;
+        std::memset(&pa, 0, sizeof(pa));
+        pa.img = buf + o_lvl;
+        pa.hblur = reinterpret_cast<uint16_t *>(buf + o_h16);
+        pa.blur = buf + o_blur;
+        pa.score = buf + o_score;
+        pa.cand = reinterpret_cast<mcs::OrbCand *>(buf + o_cand);
+        pa.ncand = reinterpret_cast<int *>(buf + o_cnt);
+        pa.nlevels = nlevels;
+        pa.threshold = fast_threshold;
+        for (int l = 0; l < nlevels; l++) {
+            pa.off[l] = (int64_t)off[l];
+            pa.coff[l] = (int)coff[l];
+            pa.w[l] = lw[l];
+            pa.h[l] = lh[l];
+            pa.cap[l] = (int)cap[l];
+            pa.bstart[l + 1] = pa.bstart[l] + (lw[l] + 255) / 256 * lh[l];
+        }
         for (hipFunction_t f : {k->orb_blur_h, k->orb_blur_v, k->orb_fast, k->orb_nms})
-            if (rc == MCS_OK) rc = launch(A, f, gx, lh[l], 256, &la, sizeof(la), s);
+            if (rc == MCS_OK)
+                rc = launch(A, f, (unsigned)pa.bstart[nlevels], 1, 256, &pa, sizeof(pa), s);
     }
+    // counts first, then only the candidates each level found (a small fraction of the
+    // capacity): the copy-back is sized by the image's corners, not by its area
     if (e == hipSuccess && rc == MCS_OK)
         e = A->hipMemcpyAsync(counts.data(), buf + o_cnt, nlevels * sizeof(int),
                               hipMemcpyDeviceToHost, s);
-    // counts first, then only the candidates each level found (a small fraction of the
-    // capacity): the copy-back is sized by the image's corners, not by its area
     if (e == hipSuccess && rc == MCS_OK) e = A->hipStreamSynchronize(s);
     for (int l = 0; l < nlevels && e == hipSuccess && rc == MCS_OK; l++) {
         const int c = std::min(std::max(counts[l], 0), (int)cap[l]);

@@ -348,10 +348,9 @@ __device__ __forceinline__ int orb_refl(int i, int n)
     return i < 0 ? -i : (i >= n ? 2 * n - 2 - i : i);
 }
 
-// grid (ceil(w / 256), h): horizontal 7-tap pass (u16, exact).
-extern "C" __global__ __launch_bounds__(256) void mcs_orb_blur_h(const mcs::KOrbLevelArgs a)
+// horizontal 7-tap pass (u16, exact).
+__device__ __forceinline__ void orb_blur_h(const mcs::KOrbLevelArgs a, const int x, const int y)
 {
-    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
     if (x >= a.w) return;
     const uint8_t *r = a.img + (int64_t)y * a.w;
     int s = 0;
@@ -360,10 +359,9 @@ extern "C" __global__ __launch_bounds__(256) void mcs_orb_blur_h(const mcs::KOrb
     a.hblur[(int64_t)y * a.w + x] = (uint16_t)s;
 }
 
-// grid (ceil(w / 256), h): vertical pass, one rounding.
-extern "C" __global__ __launch_bounds__(256) void mcs_orb_blur_v(const mcs::KOrbLevelArgs a)
+// vertical pass, one rounding.
+__device__ __forceinline__ void orb_blur_v(const mcs::KOrbLevelArgs a, const int x, const int y)
 {
-    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
     if (x >= a.w) return;
     int s = 0;
 #pragma unroll
@@ -372,11 +370,10 @@ extern "C" __global__ __launch_bounds__(256) void mcs_orb_blur_v(const mcs::KOrb
     a.blur[(int64_t)y * a.w + x] = (uint8_t)((s + 32768) >> 16);
 }
 
-// grid (ceil(w / 256), h): FAST scores of corners (score > threshold) where the NMS of a
+// FAST scores of corners (score > threshold) where the NMS of a
 // keypoint candidate can look (one pixel around the keypoint region), 0 elsewhere.
-extern "C" __global__ __launch_bounds__(256) void mcs_orb_fast(const mcs::KOrbLevelArgs a)
+__device__ __forceinline__ void orb_fast(const mcs::KOrbLevelArgs a, const int x, const int y)
 {
-    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
     if (x >= a.w) return;
     const int lo = mcs::kOrbEdge - 1;
     uint8_t v = 0;
@@ -387,36 +384,87 @@ extern "C" __global__ __launch_bounds__(256) void mcs_orb_fast(const mcs::KOrbLe
     a.score[(int64_t)y * a.w + x] = v;
 }
 
-// grid (ceil(w / 256), h): 3x3 non-maximum suppression + Harris response; survivors appended.
-extern "C" __global__ __launch_bounds__(256) void mcs_orb_nms(const mcs::KOrbLevelArgs a)
+// 3x3 non-maximum suppression + Harris response; survivors appended.
+// The block first gathers its row segment's survivors in LDS, so the Harris sums run on the
+// first ceil(n / 64) waves only, every lane busy, instead of on every wave holding a survivor.
+__device__ __forceinline__ void orb_nms(const mcs::KOrbLevelArgs a, const int x, const int y)
 {
-    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
+    __shared__ int sx[256];
+    __shared__ int ns;
     const int e = mcs::kOrbEdge;
-    if (x < e || y < e || x >= a.w - e || y >= a.h - e) return;
-    const uint8_t *s = a.score + (int64_t)y * a.w + x;
-    const int c = s[0];
-    if (c == 0) return;
-    bool keep = true;
+    if (threadIdx.x == 0) ns = 0;
+    __syncthreads();
+    bool keep = x >= e && y >= e && x < a.w - e && y < a.h - e;
+    if (keep) {
+        const uint8_t *s = a.score + (int64_t)y * a.w + x;
+        const int c = s[0];
+        keep = c != 0;
 #pragma unroll
-    for (int dy = -1; dy <= 1; dy++)
+        for (int dy = -1; dy <= 1; dy++)
 #pragma unroll
-        for (int dx = -1; dx <= 1; dx++)
-            if (dx || dy) keep = keep && c > s[dy * a.w + dx];
-    if (!keep) return;
-    const double r = mcs::orb_harris(a.img + (int64_t)y * a.w + x, a.w);
-    // one atomic per wave: the surviving lanes (the active ones here) take consecutive slots
-    // (their order is irrelevant: the host ranks each level's candidates)
+            for (int dx = -1; dx <= 1; dx++)
+                if (dx || dy) keep = keep && c > s[dy * a.w + dx];
+    }
+    if (keep) {
+        const unsigned long long act = __ballot(1);
+        const int lane = __lane_id(), leader = __ffsll((long long)act) - 1;
+        int base = 0;
+        if (lane == leader) base = atomicAdd(&ns, __popcll(act));
+        sx[__shfl(base, leader) + __popcll(act & ((1ull << lane) - 1ull))] = x;
+    }
+    __syncthreads();
+    const int n = ns;
+    if ((int)threadIdx.x >= n) return;
+    const int xs = sx[threadIdx.x];
+    const double r = mcs::orb_harris(a.img + (int64_t)y * a.w + xs, a.w);
+    // one atomic per wave: the lanes take consecutive slots (their order is irrelevant: the
+    // host ranks each level's candidates)
     const unsigned long long act = __ballot(1);
     const int lane = __lane_id(), leader = __ffsll((long long)act) - 1;
     int base = 0;
     if (lane == leader) base = atomicAdd(a.ncand, __popcll(act));
     const int i = __shfl(base, leader) + __popcll(act & ((1ull << lane) - 1ull));
     if (i < a.cap) {
-        a.cand[i].x = x;
+        a.cand[i].x = xs;
         a.cand[i].y = y;
         a.cand[i].response = r;
     }
 }
+
+// Level of this block (KOrbPyrArgs), its pixel (x, y) and its per-level view.
+__device__ __forceinline__ mcs::KOrbLevelArgs orb_level(const mcs::KOrbPyrArgs &p, int &x, int &y)
+{
+    const int b = blockIdx.x;
+    int l = 0;
+    for (int k = 1; k < p.nlevels; k++) l += b >= p.bstart[k] ? 1 : 0;
+    const int bx = (p.w[l] + 255) >> 8, loc = b - p.bstart[l];
+    y = loc / bx;
+    x = (loc - y * bx) * 256 + (int)threadIdx.x;
+    mcs::KOrbLevelArgs a;
+    a.img = p.img + p.off[l];
+    a.hblur = p.hblur + p.off[l];
+    a.blur = p.blur + p.off[l];
+    a.score = p.score + p.off[l];
+    a.cand = p.cand + p.coff[l];
+    a.ncand = p.ncand + l;
+    a.w = p.w[l];
+    a.h = p.h[l];
+    a.threshold = p.threshold;
+    a.cap = p.cap[l];
+    return a;
+}
+
+#define MCS_ORB_PYR_KERNEL(NAME)                                                               \
+    extern "C" __global__ __launch_bounds__(256) void mcs_orb_##NAME(const mcs::KOrbPyrArgs p) \
+    {                                                                                          \
+        int x, y;                                                                              \
+        const mcs::KOrbLevelArgs a = orb_level(p, x, y);                                       \
+        orb_##NAME(a, x, y);                                                                   \
+    }
+MCS_ORB_PYR_KERNEL(blur_h)
+MCS_ORB_PYR_KERNEL(blur_v)
+MCS_ORB_PYR_KERNEL(fast)
+MCS_ORB_PYR_KERNEL(nms)
 
 // grid (n), block 64: one wave per keypoint -- orientation moments (lane v sums row v of the
 // disk, wave reduction), then 4 rBRIEF pairs per lane packed into the 32 descriptor bytes.

@@ -77,6 +77,20 @@ struct KOrbLevelArgs {
     int *ncand;
     int w, h, threshold, cap;
 };
+// All levels of one frame in one launch: grid (bstart[nlevels]) blocks of 256 threads, level l
+// owning blocks [bstart[l], bstart[l + 1]), one block per 256-pixel row segment.  Level buffers
+// are the bases + off[l] (pixels) and cand + coff[l] (candidates).
+struct KOrbPyrArgs {
+    const uint8_t *img;
+    uint16_t *hblur;
+    uint8_t *blur;
+    uint8_t *score;
+    OrbCand *cand;
+    int *ncand;                 // [nlevels]
+    int64_t off[12];
+    int coff[12], w[12], h[12], cap[12], bstart[13];
+    int nlevels, threshold;
+};
 struct KOrbDescArgs {
     const uint8_t *img[12], *blur[12];
     int w[12];

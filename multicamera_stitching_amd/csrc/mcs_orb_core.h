@@ -74,19 +74,21 @@ MCS_ORB_HD void orb_sobel(const uint8_t *p, int step, int &ix, int &iy)
          ((int)p[-step - 1] + 2 * p[-step] + p[-step + 1]);
 }
 
+// |Ix|, |Iy| <= 4 * 255, so each of the 49-term sums stays below 49 * 1020^2 < 2^31: 32-bit
+// accumulators are exact (the products of the final combination need 64 bits).
 MCS_ORB_HD double orb_harris(const uint8_t *p, int step)
 {
-    int64_t a = 0, b = 0, c = 0;
+    int32_t a = 0, b = 0, c = 0;
     for (int v = -3; v <= 3; v++)
         for (int u = -3; u <= 3; u++) {
             int ix, iy;
             orb_sobel(p + v * step + u, step, ix, iy);
-            a += (int64_t)ix * ix;
-            b += (int64_t)iy * iy;
-            c += (int64_t)ix * iy;
+            a += ix * ix;
+            b += iy * iy;
+            c += ix * iy;
         }
-    const double t = (double)(a + b);
-    return (double)(a * b - c * c) - 0.04 * (t * t);
+    const double t = (double)((int64_t)a + b);
+    return (double)((int64_t)a * b - (int64_t)c * c) - 0.04 * (t * t);
 }
 
 // (cos, sin) of the intensity-centroid orientation at p (level image, unblurred).
