@@ -571,11 +571,16 @@ int mcs_orb_detect_host(const uint8_t *image, int w, int h, int channels, int nf
         for (int l = 0; l < nlevels; l++) {
             const int c = std::min(counts[l], (int)cap[l]);
             mcs::OrbCand *b = cand.data() + coff[l];
-            std::sort(b, b + c, [](const mcs::OrbCand &p, const mcs::OrbCand &q) {
+            // a strict total order (positions are unique), so selecting the quota first and
+            // sorting only it gives the full sort's prefix
+            auto rank = [](const mcs::OrbCand &p, const mcs::OrbCand &q) {
                 if (p.response != q.response) return p.response > q.response;
                 return p.y != q.y ? p.y < q.y : p.x < q.x;
-            });
-            for (int i = 0; i < std::min(c, quota[l]); i++) {
+            };
+            const int keep = std::min(c, quota[l]);
+            if (keep < c) std::nth_element(b, b + keep, b + c, rank);
+            std::sort(b, b + keep, rank);
+            for (int i = 0; i < keep; i++) {
                 kp.push_back(l);
                 kp.push_back(b[i].x);
                 kp.push_back(b[i].y);

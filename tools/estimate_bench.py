@@ -91,17 +91,28 @@ def estimate_cpu(frames, args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--nfeatures", type=int, default=2000)
     ap.add_argument("--threads", type=int, default=4,
                     help="host threads issuing the per-camera / per-pair calls (1: serial)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pinned", action="store_true",
+                    help="camera frames in pinned host buffers (default: pageable numpy arrays, "
+                         "as the reference's capture loop holds them)")
     args = ap.parse_args()
     from multicamera_stitching_amd import rig
     W, Hh, N = 1920, 1080, 4
     C = rig.camera_models(N, W, Hh, seed=0)
     frames = rig.world_frames(C, W, Hh, 3, seed=0, world_fn=world)
+    if args.pinned:
+        import torch
+        pinned = []
+        for f in frames:
+            t = torch.empty(f.shape, dtype=torch.uint8, pin_memory=True)
+            t.numpy()[...] = f
+            pinned.append(t)
+        frames = [t.numpy() for t in pinned]
     truth = [np.linalg.inv(C[k - 1]) @ C[k] for k in range(1, N)]
     truth = [T / T[2, 2] for T in truth]
     for _ in range(args.warmup):
@@ -124,7 +135,8 @@ def main():
         "config": {"workload": "BASELINE configs[2]: ORB nfeatures %d, 8 levels x 1.2, FAST 20; "
                                "Hamming kNN-2, ratio 0.75; RANSAC 3.0 px, 2000 hypotheses; 3 "
                                "adjacent pairs" % args.nfeatures,
-                   "host_frames": True, "host_threads": args.threads},
+                   "host_frames": "pinned" if args.pinned else "pageable",
+                   "host_threads": args.threads},
         "stage_ms_per_capture": {k: round(v / args.steps * 1e3, 3) for k, v in tot.items()},
         "keypoints": res[0][3], "matches": [r[1] for r in res], "inliers": [r[2] for r in res],
         "max_reproj_err_px_vs_truth": errs,
