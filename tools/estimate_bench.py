@@ -91,8 +91,8 @@ def estimate_cpu(frames, args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--nfeatures", type=int, default=2000)
     ap.add_argument("--threads", type=int, default=4,
                     help="host threads issuing the per-camera / per-pair calls (1: serial)")
