@@ -699,10 +699,11 @@ __device__ __forceinline__ void mb_prep(const KMbArgs &a)
 template <int CN>
 struct MbLvLds {
     uint8_t foot[MCS_MB_STAGE ? kMbFootBufs : 0][kMbFoot] __attribute__((aligned(16)));   // source footprints
-    uint32_t g0[kMbU];                 // level 0: channel k in byte k
-    uint2 g1[kMbN1X * kMbN1Y];         // 256 G1 <= 65280 as u16 lanes: x = (c0, c2), y = (c1, c3)
+    // (one spare entry past each array: the branch-free stores of out-of-range items land there)
+    uint32_t g0[kMbU + 1];             // level 0: channel k in byte k
+    uint2 g1[kMbN1X * kMbN1Y + 1];     // 256 G1 <= 65280 as u16 lanes: x = (c0, c2), y = (c1, c3)
     union {
-        uint2 hs[kMbUsedY * kMbN1X];   // horizontal pass of level 1 (<= 4080), lanes as g1
+        uint2 hs[kMbUsedY * kMbN1X + 1];   // horizontal pass of level 1 (<= 4080), lanes as g1
         int4 hs2[kMbN1Y * kMbN2X];     // horizontal pass of level 2, one int per channel
     };
 };
@@ -792,7 +793,7 @@ __device__ __forceinline__ void mb_levels(const KMbArgs &a, MbLvLds<CN> &L)
             }
 #pragma unroll
             for (int kk = 0; kk < KJ; kk++)
-                if (tid + kk * NT < n_s) L.g0[(dmeta[kk] >> 16) & 0x1fffu] = px[kk];
+                L.g0[tid + kk * NT < n_s ? (dmeta[kk] >> 16) & 0x1fffu : (uint32_t)kMbU] = px[kk];
         } else if (shifted) {
             struct __attribute__((packed)) U2 {
                 uint32_t x, y;
@@ -818,7 +819,7 @@ __device__ __forceinline__ void mb_levels(const KMbArgs &a, MbLvLds<CN> &L)
             }
 #pragma unroll
             for (int kk = 0; kk < KJ; kk++)
-                if (tid + kk * NT < n_s) L.g0[(dmeta[kk] >> 16) & 0x1fffu] = px[kk];
+                L.g0[tid + kk * NT < n_s ? (dmeta[kk] >> 16) & 0x1fffu : (uint32_t)kMbU] = px[kk];
         } else {
             for (int i = tid; i < n_s; i += NT) {
                 const uint64_t v = dsc[i];
@@ -866,10 +867,9 @@ __device__ __forceinline__ void mb_levels(const KMbArgs &a, MbLvLds<CN> &L)
 #pragma unroll
                 for (int q = 0; q < IT; q++) {
                     const int i = tid + q * NT;
-                    if (i < n) {
-                        const int r = (int)(__umul24((unsigned)i, d1m) >> 16);
-                        L.hs[r * kMbN1X + a1 + i - (int)__umul24((unsigned)r, (unsigned)w1)] = res[q];
-                    }
+                    const int r = (int)(__umul24((unsigned)i, d1m) >> 16);
+                    L.hs[i < n ? r * kMbN1X + a1 + i - (int)__umul24((unsigned)r, (unsigned)w1)
+                               : kMbUsedY * kMbN1X] = res[q];
                 }
             }
             __syncthreads();
@@ -894,11 +894,9 @@ __device__ __forceinline__ void mb_levels(const KMbArgs &a, MbLvLds<CN> &L)
 #pragma unroll
                 for (int q = 0; q < IT; q++) {
                     const int i = tid + q * NT;
-                    if (i < n) {
-                        const int ey = (int)(__umul24((unsigned)i, d1m) >> 16);
-                        L.g1[ey * kMbN1X + a1 + i - (int)__umul24((unsigned)ey, (unsigned)w1)] =
-                            res[q];
-                    }
+                    const int ey = (int)(__umul24((unsigned)i, d1m) >> 16);
+                    L.g1[i < n ? ey * kMbN1X + a1 + i - (int)__umul24((unsigned)ey, (unsigned)w1)
+                               : kMbN1X * kMbN1Y] = res[q];
                 }
             }
             __syncthreads();
