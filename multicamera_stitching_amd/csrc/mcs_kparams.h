@@ -147,7 +147,11 @@ constexpr int kMbPrepThreads = 256;
 #define MCS_MB_LV_THREADS 512
 #endif
 constexpr int kMbLvThreads = MCS_MB_LV_THREADS;
-constexpr int kMbLvFrames = 8;      // captures per levels block (sample windows held in registers)
+#ifndef MCS_MB_LV_FRAMES
+#define MCS_MB_LV_FRAMES 8
+#endif
+constexpr int kMbLvFrames = MCS_MB_LV_FRAMES;   // captures per levels block (sample windows held
+                                                // in registers)
 constexpr int kMbBlThreads = 256;
 constexpr int64_t kMbScratchBytes = 1ll << 30;    // level scratch budget per plan (<= 64 captures)
 // The pyramid arrays a tile holds, per axis (tile side T): level 0 [O - 14, O + T + 10]
