@@ -257,7 +257,8 @@ int mcs_match_hamming_knn2_host(const uint8_t *query, int n_query, const uint8_t
  * with OpenCV's per-level quota of nfeatures, intensity-centroid orientation, rBRIEF (OpenCV's
  * 31x31 pattern).  Specified in csrc/mcs_orb_core.h.  Outputs (capacity nfeatures): kp_xy
  * (level-0 pixels), kp_response, kp_angle (degrees), kp_level (may be NULL), desc (32 B each),
- * *n_out.  Synchronous. */
+ * *n_out.  w, h <= 65535.  Synchronous: one upload, one copy back (levels ranked on the device;
+ * a level with more than 4096 candidates is ranked on the host, same result). */
 int mcs_orb_detect_host(const uint8_t *image, int w, int h, int channels, int nfeatures,
                         int nlevels, float scale_factor, int fast_threshold, float *kp_xy,
                         float *kp_response, float *kp_angle, int *kp_level, uint8_t *desc,

@@ -24,6 +24,7 @@ struct FeatureKernels {
     hipFunction_t ransac_score = nullptr, ransac_mask = nullptr;
     hipFunction_t orb_gray = nullptr, orb_blur_h = nullptr, orb_blur_v = nullptr;
     hipFunction_t orb_fast = nullptr, orb_nms = nullptr, orb_describe = nullptr;
+    hipFunction_t orb_select = nullptr;
     hipFunction_t l2_prep = nullptr, l2_i8 = nullptr, l2_f32 = nullptr, l2_finalize = nullptr;
 };
 FeatureKernels g_fk[mcs::kMaxDevices];
@@ -83,6 +84,7 @@ int feature_kernels(const Api *A, int device, const FeatureKernels **out)
         } orb[] = {{"mcs_orb_gray", &k.orb_gray},     {"mcs_orb_blur_h", &k.orb_blur_h},
                    {"mcs_orb_blur_v", &k.orb_blur_v}, {"mcs_orb_fast", &k.orb_fast},
                    {"mcs_orb_nms", &k.orb_nms},       {"mcs_orb_describe", &k.orb_describe},
+                   {"mcs_orb_select", &k.orb_select},
                    {"mcs_l2_prep", &k.l2_prep},       {"mcs_l2_knn2_i8", &k.l2_i8},
                    {"mcs_l2_knn2_f32", &k.l2_f32},    {"mcs_l2_knn2_finalize", &k.l2_finalize}};
         for (const auto &o : orb)
@@ -437,7 +439,9 @@ int mcs_orb_detect_host(const uint8_t *image, int w, int h, int channels, int nf
 {
     mcs::clear_error();
     if (!image || !kp_xy || !desc || !n_out) return mcs::fail(MCS_E_INVALID, "NULL buffer");
-    if (w <= 0 || h <= 0 || (channels != 1 && channels != 3) || nfeatures < 0 ||
+    // (w, h < 2^16: the device ranking packs a keypoint's position as y << 16 | x)
+    if (w <= 0 || h <= 0 || w > 65535 || h > 65535 || (channels != 1 && channels != 3) ||
+        nfeatures < 0 ||
         nlevels < 1 || nlevels > mcs::kOrbMaxLevels || !(scale_factor > 1.0f) ||
         fast_threshold < 0 || fast_threshold > 255)
         return mcs::fail(MCS_E_INVALID, "w=%d h=%d channels=%d nfeatures=%d nlevels=%d "
@@ -498,6 +502,9 @@ int mcs_orb_detect_host(const uint8_t *image, int w, int h, int channels, int nf
     const size_t o_kp = take((size_t)std::max(nfeatures, 1) * 3 * sizeof(int));
     const size_t o_desc = take((size_t)std::max(nfeatures, 1) * 32);
     const size_t o_or = take((size_t)std::max(nfeatures, 1) * 2 * sizeof(double));
+    const size_t o_resp = take((size_t)std::max(nfeatures, 1) * sizeof(double));
+    const size_t o_sel = take(2 * sizeof(int));
+    const size_t o_end = o;   // [o_cnt, o_end): everything the device ranking path copies back
     uint8_t *buf = nullptr;
     hipStream_t s = nullptr;
     rc = workspace(A, device, o, &buf, &s);
@@ -552,59 +559,99 @@ int mcs_orb_detect_host(const uint8_t *image, int w, int h, int channels, int nf
             if (rc == MCS_OK)
                 rc = launch(A, f, (unsigned)pa.bstart[nlevels], 1, 256, &pa, sizeof(pa), s);
     }
-    // counts first, then only the candidates each level found (a small fraction of the
-    // capacity): the copy-back is sized by the image's corners, not by its area
-    if (e == hipSuccess && rc == MCS_OK)
-        e = A->hipMemcpyAsync(counts.data(), buf + o_cnt, nlevels * sizeof(int),
-                              hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess && rc == MCS_OK) e = A->hipStreamSynchronize(s);
-    for (int l = 0; l < nlevels && e == hipSuccess && rc == MCS_OK; l++) {
-        const int c = std::min(std::max(counts[l], 0), (int)cap[l]);
-        if (c > 0)
-            e = A->hipMemcpyAsync(cand.data() + coff[l],
-                                  buf + o_cand + coff[l] * sizeof(mcs::OrbCand),
-                                  (size_t)c * sizeof(mcs::OrbCand), hipMemcpyDeviceToHost, s);
+    // Device ranking (mcs_orb_select) and description, then ONE copy back of counts,
+    // keypoints, descriptors, orientations and responses.  A level with more than kOrbSelMax
+    // candidates sets the overflow flag instead; the host then ranks (below).
+    static thread_local std::vector<uint8_t> blob;
+    if (blob.size() < o_end - o_cnt) blob.resize(o_end - o_cnt);
+    auto at = [&](size_t off) { return blob.data() + (off - o_cnt); };
+    mcs::KOrbDescArgs da;
+    std::memset(&da, 0, sizeof(da));
+    for (int l = 0; l < mcs::kOrbMaxLevels; l++) {
+        const int ll = l < nlevels ? l : 0;
+        da.img[l] = buf + o_lvl + off[ll];
+        da.blur[l] = buf + o_blur + off[ll];
+        da.w[l] = lw[ll];
     }
+    da.kp = reinterpret_cast<const int *>(buf + o_kp);
+    da.desc = buf + o_desc;
+    da.orient = reinterpret_cast<double *>(buf + o_or);
+    int n_bound = 0;
+    for (int l = 0; l < nlevels; l++) n_bound += quota[l];
+    if (e == hipSuccess && rc == MCS_OK) {
+        mcs::KOrbSelArgs sa;
+        std::memset(&sa, 0, sizeof(sa));
+        sa.cand = reinterpret_cast<const mcs::OrbCand *>(buf + o_cand);
+        sa.ncand = reinterpret_cast<const int *>(buf + o_cnt);
+        sa.kp = reinterpret_cast<int *>(buf + o_kp);
+        sa.resp = reinterpret_cast<double *>(buf + o_resp);
+        sa.sel = reinterpret_cast<int *>(buf + o_sel);
+        for (int l = 0; l < nlevels; l++) {
+            sa.coff[l] = (int)coff[l];
+            sa.cap[l] = (int)cap[l];
+            sa.quota[l] = quota[l];
+        }
+        sa.nlevels = nlevels;
+        rc = launch(A, k->orb_select, (unsigned)nlevels, 1, mcs::kOrbSelThreads, &sa, sizeof(sa), s);
+        da.sel = sa.sel;
+        da.n = n_bound;
+        if (rc == MCS_OK && n_bound > 0)
+            rc = launch(A, k->orb_describe, (unsigned)n_bound, 1, 64, &da, sizeof(da), s);
+    }
+    if (e == hipSuccess && rc == MCS_OK)
+        e = A->hipMemcpyAsync(blob.data(), buf + o_cnt, o_end - o_cnt, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess && rc == MCS_OK) e = A->hipStreamSynchronize(s);
     int n = 0;
-    if (e == hipSuccess && rc == MCS_OK) {
-        // per level: rank by response (desc), then y, then x; keep the level's quota
-        for (int l = 0; l < nlevels; l++) {
-            const int c = std::min(counts[l], (int)cap[l]);
-            mcs::OrbCand *b = cand.data() + coff[l];
-            // a strict total order (positions are unique), so selecting the quota first and
-            // sorting only it gives the full sort's prefix
-            auto rank = [](const mcs::OrbCand &p, const mcs::OrbCand &q) {
-                if (p.response != q.response) return p.response > q.response;
-                return p.y != q.y ? p.y < q.y : p.x < q.x;
-            };
-            const int keep = std::min(c, quota[l]);
-            if (keep < c) std::nth_element(b, b + keep, b + c, rank);
-            std::sort(b, b + keep, rank);
-            for (int i = 0; i < keep; i++) {
-                kp.push_back(l);
-                kp.push_back(b[i].x);
-                kp.push_back(b[i].y);
-                resp.push_back(b[i].response);
-            }
+    const int *sel = reinterpret_cast<const int *>(at(o_sel));
+    const int *kpd = reinterpret_cast<const int *>(at(o_kp));
+    const double *respd = reinterpret_cast<const double *>(at(o_resp));
+    const double *ord = reinterpret_cast<const double *>(at(o_or));
+    if (e == hipSuccess && rc == MCS_OK && !sel[1]) {
+        n = sel[0];
+        kp.assign(kpd, kpd + 3 * (size_t)n);
+        resp.assign(respd, respd + n);
+        orient.assign(ord, ord + 2 * (size_t)n);
+        std::memcpy(desc, at(o_desc), (size_t)n * 32);
+    } else if (e == hipSuccess && rc == MCS_OK) {
+        // host ranking: only the candidates each level found come back
+        std::memcpy(counts.data(), at(o_cnt), nlevels * sizeof(int));
+        for (int l = 0; l < nlevels && e == hipSuccess; l++) {
+            const int c = std::min(std::max(counts[l], 0), (int)cap[l]);
+            if (c > 0)
+                e = A->hipMemcpyAsync(cand.data() + coff[l],
+                                      buf + o_cand + coff[l] * sizeof(mcs::OrbCand),
+                                      (size_t)c * sizeof(mcs::OrbCand), hipMemcpyDeviceToHost, s);
         }
-        n = (int)kp.size() / 3;
-        orient.resize(2 * (size_t)std::max(n, 1));
-        if (n > 0) {
+        if (e == hipSuccess) e = A->hipStreamSynchronize(s);
+        if (e == hipSuccess) {
+            // per level: rank by response (desc), then y, then x; keep the level's quota (a
+            // strict total order -- positions are unique -- so selecting the quota first and
+            // sorting only it gives the full sort's prefix)
+            for (int l = 0; l < nlevels; l++) {
+                const int c = std::min(counts[l], (int)cap[l]);
+                mcs::OrbCand *b = cand.data() + coff[l];
+                auto rank = [](const mcs::OrbCand &p, const mcs::OrbCand &q) {
+                    if (p.response != q.response) return p.response > q.response;
+                    return p.y != q.y ? p.y < q.y : p.x < q.x;
+                };
+                const int keep = std::min(c, quota[l]);
+                if (keep < c) std::nth_element(b, b + keep, b + c, rank);
+                std::sort(b, b + keep, rank);
+                for (int i = 0; i < keep; i++) {
+                    kp.push_back(l);
+                    kp.push_back(b[i].x);
+                    kp.push_back(b[i].y);
+                    resp.push_back(b[i].response);
+                }
+            }
+            n = (int)kp.size() / 3;
+            orient.resize(2 * (size_t)std::max(n, 1));
+        }
+        if (e == hipSuccess && n > 0) {
             e = A->hipMemcpyAsync(buf + o_kp, kp.data(), kp.size() * sizeof(int),
                                   hipMemcpyHostToDevice, s);
-            mcs::KOrbDescArgs da;
-            for (int l = 0; l < mcs::kOrbMaxLevels; l++) {
-                const int ll = l < nlevels ? l : 0;
-                da.img[l] = buf + o_lvl + off[ll];
-                da.blur[l] = buf + o_blur + off[ll];
-                da.w[l] = lw[ll];
-            }
-            da.kp = reinterpret_cast<const int *>(buf + o_kp);
-            da.desc = buf + o_desc;
-            da.orient = reinterpret_cast<double *>(buf + o_or);
+            da.sel = nullptr;
             da.n = n;
-            da.pad_ = 0;
             if (e == hipSuccess) rc = launch(A, k->orb_describe, n, 1, 64, &da, sizeof(da), s);
             if (e == hipSuccess && rc == MCS_OK)
                 e = A->hipMemcpyAsync(desc, buf + o_desc, (size_t)n * 32, hipMemcpyDeviceToHost, s);

@@ -466,12 +466,69 @@ MCS_ORB_PYR_KERNEL(blur_v)
 MCS_ORB_PYR_KERNEL(fast)
 MCS_ORB_PYR_KERNEL(nms)
 
+// grid (nlevels), block kOrbSelThreads: the level's candidates ranked in LDS by a bitonic sort
+// (response descending, then y, then x: the host ranking's total order; (y, x) packed as
+// y << 16 | x), then its quota written at the level's offset (the kept counts of the levels
+// before it).  More than kOrbSelMax candidates on any level: overflow, the host ranks instead.
+extern "C" __global__ __launch_bounds__(1024) void mcs_orb_select(const mcs::KOrbSelArgs a)
+{
+    using namespace mcs;
+    __shared__ double rs[kOrbSelMax];
+    __shared__ uint32_t ks[kOrbSelMax];
+    const int l = blockIdx.x, tid = threadIdx.x;
+    auto kept = [&](int i) { return min(min(a.ncand[i], a.cap[i]), a.quota[i]); };
+    int base = 0, total = 0;
+    for (int i = 0; i < a.nlevels; i++) {
+        if (i < l) base += kept(i);
+        total += kept(i);
+    }
+    bool over = false;
+    for (int i = 0; i < a.nlevels; i++) over = over || min(a.ncand[i], a.cap[i]) > kOrbSelMax;
+    if (l == 0 && tid == 0) {
+        a.sel[0] = total;
+        a.sel[1] = over ? 1 : 0;
+    }
+    if (over) return;   // uniform
+    const int c = min(a.ncand[l], a.cap[l]), q = kept(l);
+    int n = 64;
+    while (n < c) n <<= 1;
+    const OrbCand *cd = a.cand + a.coff[l];
+    for (int i = tid; i < n; i += kOrbSelThreads) {
+        const bool v = i < c;
+        rs[i] = v ? cd[i].response : -__builtin_inf();
+        ks[i] = v ? ((uint32_t)cd[i].y << 16) | (uint32_t)cd[i].x : 0xffffffffu;
+    }
+    __syncthreads();
+    for (int size = 2; size <= n; size <<= 1)
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int t = tid; t < n / 2; t += kOrbSelThreads) {
+                const int lo = 2 * t - (t & (stride - 1)), hi = lo + stride;
+                const double rl = rs[lo], rh = rs[hi];
+                const uint32_t kl = ks[lo], kh = ks[hi];
+                const bool hi_first = rh > rl || (rh == rl && kh < kl);
+                if (hi_first == ((lo & size) == 0)) {
+                    rs[lo] = rh, rs[hi] = rl;
+                    ks[lo] = kh, ks[hi] = kl;
+                }
+            }
+            __syncthreads();
+        }
+    for (int i = tid; i < q; i += kOrbSelThreads) {
+        const int o = base + i;
+        a.kp[3 * o] = l;
+        a.kp[3 * o + 1] = (int)(ks[i] & 0xffffu);
+        a.kp[3 * o + 2] = (int)(ks[i] >> 16);
+        a.resp[o] = rs[i];
+    }
+}
+
 // grid (n), block 64: one wave per keypoint -- orientation moments (lane v sums row v of the
 // disk, wave reduction), then 4 rBRIEF pairs per lane packed into the 32 descriptor bytes.
 extern "C" __global__ __launch_bounds__(64) void mcs_orb_describe(const mcs::KOrbDescArgs a)
 {
     using namespace mcs;
     const int k = blockIdx.x, lane = threadIdx.x;
+    if (a.sel && (k >= a.sel[0] || a.sel[1])) return;   // past the device ranking's count
     const int lvl = a.kp[3 * k], x = a.kp[3 * k + 1], y = a.kp[3 * k + 2];
     const int w = a.w[lvl];
     const uint8_t *p = a.img[lvl] + (int64_t)y * w + x;

@@ -97,7 +97,22 @@ struct KOrbDescArgs {
     const int *kp;         // n x 3: level, x, y
     uint8_t *desc;         // n x 32
     double *orient;        // n x 2: cos, sin
+    const int *sel;        // mcs_orb_select's [n, overflow] (grid = the n bound), or NULL: n
     int n, pad_;
+};
+// Per-level ranking on the device (mcs_orb_select): one block per level sorts the level's
+// candidates (<= kOrbSelMax, else the host ranks every level) and writes its quota's
+// keypoints, levels in order.  sel[0] = total keypoints, sel[1] = overflow flag.
+constexpr int kOrbSelMax = 4096;
+constexpr int kOrbSelThreads = 1024;
+struct KOrbSelArgs {
+    const OrbCand *cand;
+    const int *ncand;      // [nlevels]
+    int *kp;               // n x 3: level, x, y
+    double *resp;          // n
+    int *sel;              // [2]: n, overflow
+    int coff[12], cap[12], quota[12];
+    int nlevels, pad_;
 };
 struct KGrayArgs {
     const uint8_t *bgr;

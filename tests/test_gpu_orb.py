@@ -26,6 +26,27 @@ def test_orb_vs_oracle(h, w, nf, nl):
     assert np.allclose(got["angle"], ang, atol=1e-3)
 
 
+@pytest.mark.parametrize("kind", ["noise", "blocks4", "blocks8"])
+def test_orb_dense_candidates_vs_oracle(kind):
+    """Many candidates per level: pixel noise puts more than kOrbSelMax (4096) on level 0 (the
+    host ranks every level), blocky noise a few thousand (the device's bitonic ranking, with
+    ties in response broken by position)."""
+    from multicamera_stitching_amd import _capi
+    rng = np.random.default_rng(7)
+    if kind == "noise":
+        img = rng.integers(0, 256, (480, 640), dtype=np.uint8)
+    else:
+        b = int(kind[-1])
+        img = np.kron(rng.integers(0, 256, (480 // b, 640 // b)), np.ones((b, b))).astype(np.uint8)
+    got = _capi.orb_detect(img, nfeatures=1500, nlevels=8)
+    want = oracle.orb_detect(img, nfeatures=1500, nlevels=8)
+    assert len(got["xy"]) == len(want["xy"]) > 0
+    assert np.array_equal(got["level"], want["level"])
+    assert np.array_equal(got["xy"], want["xy"])
+    assert np.array_equal(got["response"], want["response"].astype(np.float32))
+    assert np.array_equal(got["desc"], want["desc"])
+
+
 def test_orb_bgr_input_uses_opencv_gray():
     from multicamera_stitching_amd import _capi
     rng = np.random.default_rng(3)
