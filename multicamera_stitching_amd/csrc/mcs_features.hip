@@ -499,6 +499,8 @@ extern "C" __global__ __launch_bounds__(1024) void mcs_orb_select(const mcs::KOr
         ks[i] = v ? ((uint32_t)cd[i].y << 16) | (uint32_t)cd[i].x : 0xffffffffu;
     }
     __syncthreads();
+    // (a stage of stride <= 64 pairs elements inside each wave's own 128-element segments: the
+    // wave's LDS accesses stay in issue order, so only strides >= 128 need the block barrier)
     for (int size = 2; size <= n; size <<= 1)
         for (int stride = size >> 1; stride > 0; stride >>= 1) {
             for (int t = tid; t < n / 2; t += kOrbSelThreads) {
@@ -511,7 +513,12 @@ extern "C" __global__ __launch_bounds__(1024) void mcs_orb_select(const mcs::KOr
                     ks[lo] = kh, ks[hi] = kl;
                 }
             }
-            __syncthreads();
+            if (stride >= 128 || (stride == 1 && size * 2 > 128) || size == n) {
+                __syncthreads();
+            } else {
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+            }
         }
     for (int i = tid; i < q; i += kOrbSelThreads) {
         const int o = base + i;
