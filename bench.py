@@ -57,8 +57,13 @@ def parse():
                     default="multiband",
                     help="multiband = BASELINE configs[1]; none = the reference's paste")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--gather", action="store_true",
-                    help="after timing, gather one mosaic per rank onto rank 0 (RCCL)")
+    ap.add_argument("--gather", choices=["after", "timed", "none"], default="after",
+                    help="N > 1: deliver every rank's F mosaics to rank 0 (RCCL point-to-point "
+                         "over xGMI) after the timed region ('after', reported as 'gather'), "
+                         "or additionally as part of every timed step ('timed')")
+    ap.add_argument("--stub", action="store_true",
+                    help="CPU rehearsal of the multi-rank orchestration (gloo, a stub step): "
+                         "no GPU, no libmcs; tests/test_bench_dist.py")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-paste-ref", action="store_true",
                     help="skip the paste-only reference launch (PMC passes: one plan's dispatches)")
@@ -66,14 +71,42 @@ def parse():
     return ap.parse_args()
 
 
+def spawn_ranks(args) -> int:
+    """--gpus N > 1 without a torch.distributed launcher around us: start N rank processes (one
+    per GPU) under torch.distributed.run as CHILDREN and return their exit code.  This parent
+    never touches the GPU (nothing above imports torch.cuda)."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def world_from_env(args):
+    """(world, rank, local_rank).  Exits non-zero when the launcher's WORLD_SIZE disagrees with
+    --gpus (a line must never report a GPU count it did not run)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench: WORLD_SIZE={world} but --gpus {args.gpus}: launch one rank per "
+                         f"GPU (python bench.py --gpus N spawns them itself)")
+    return world, int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args))
+    world, rank, local = world_from_env(args)
+    if args.stub:
+        return stub_main(args, world, rank)
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -135,41 +168,36 @@ def main():
     prep_ms = (time.perf_counter() - t_prep) * 1e3
     plan_stats = plan.stats()
 
-    def step():
+    def stitch():
         plan.stitch_device([t.data_ptr() for t in d_cams], [t[0].numel() for t in d_cams],
                            d_out.data_ptr(), pitch, d_out[0].numel(), F, stream.cuda_stream)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+    step = stitch
+    if world > 1 and args.gather == "timed":
+        # every step also delivers the F mosaics of every rank to rank 0 (RCCL send/recv)
+        bufs = [torch.empty_like(d_out) for _ in range(world - 1)] if rank == 0 else None
+
+        def step():
+            stream.wait_stream(torch.cuda.current_stream())   # previous sends done with d_out
+            stitch()
+            torch.cuda.current_stream().wait_stream(stream)
+            shard.gather_mosaics(d_out, dst=0, bufs=bufs)
+
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps)]
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        ev[i][0].record(stream)
-        step()
-        ev[i][1].record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+
+    def record(i, what):
+        ev[i][0 if what == "start" else 1].record(stream)
+
+    elapsed = shard.timed_loop(step, args.steps, args.warmup, torch.cuda.synchronize, record)
     launch_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     elapsed, launch_ms = shard.max_over_ranks([elapsed, launch_ms], device=dev)
-    gather_ms = None
-    if args.gather and world > 1:
-        # optional: deliver every rank's first mosaic to rank 0 (RCCL point-to-point over xGMI)
-        torch.cuda.synchronize()
-        tg = time.perf_counter()
-        shard.gather_mosaics(d_out[0], dst=0)
-        torch.cuda.synchronize()
-        gather_ms = shard.max_over_ranks([(time.perf_counter() - tg) * 1e3], device=dev)[0]
+    gather = None
+    if world > 1 and args.gather != "none":
+        gather = gather_all(d_out, args, shard, torch, dev)
 
     mpix_per_launch = F * out_w * out_h / 1e6
-    value = world * mpix_per_launch * args.steps / elapsed
+    value = shard.job_rate(mpix_per_launch, args.steps, elapsed, world)
     frame0 = d_out[0, :, :out_w * C].reshape(out_h, out_w, C).cpu().numpy() if rank == 0 else None
 
     # the same launch with the reference's paste (cylinder: the hard seam) and no blend pass:
@@ -208,10 +236,14 @@ def main():
                 f"super{int(args.super_mode)}-F{F}-{args.blend}")
     if cyl:
         workload = f"cyl-f{args.focal:g}-" + workload
+    traffic_src = None
     try:
         pm = json.load(open(args.pmc_json))
-        if pm.get("workload") == workload:
+        # counters count only for the kernels they were taken on: same workload AND same build
+        # of the embedded code objects (mcs_build_id), else traffic stays null
+        if pm.get("workload") == workload and pm.get("build_id") == _capi.build_id():
             traffic = pm.get("hbm_bytes_per_launch")
+            traffic_src = os.path.relpath(args.pmc_json, ROOT)
     except (OSError, ValueError):
         pass
 
@@ -245,7 +277,7 @@ def main():
                 "parallelism": f"captures sharded over {world} GPU(s), no data-path collective",
             },
             "max_abs_diff": max_abs,
-            "gather_ms": gather_ms,
+            "gather": gather,
             "plan": {"prepare_ms_once": round(prep_ms, 3), "tiles": plan_stats["tiles"],
                      "lds_tiles": plan_stats["lds_tiles"],
                      "direct_tiles": plan_stats["direct_tiles"],
@@ -264,6 +296,8 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
+                "traffic_source": traffic_src,
+                "build_id": _capi.build_id(),
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 "kernel_ms_per_launch": round(launch_ms, 4),
                 # the HBM-bound streaming kernel alone (the paste-only launch: the same gather
@@ -275,6 +309,73 @@ def main():
             },
             "cpu_baseline": cpu,
         }
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return result
+
+
+def gather_all(d_out, args, shard, torch, dev, reps: int = 3):
+    """Deliver every rank's F finished mosaics (the whole output batch) to rank 0 over RCCL
+    point-to-point (xGMI, one link per peer), outside the timed region; verified by a checksum
+    of checksums.  Reported separately: best-of-`reps` time, max over ranks."""
+    import torch.distributed as dist
+    world, rank = dist.get_world_size(), dist.get_rank()
+    bufs = [torch.empty_like(d_out) for _ in range(world - 1)] if rank == 0 else None
+    ok_all, best = True, None
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        dist.barrier()
+        t = time.perf_counter()
+        shard.gather_mosaics(d_out, dst=0, bufs=bufs)
+        torch.cuda.synchronize()
+        dt = shard.max_over_ranks([time.perf_counter() - t], device=dev)[0]
+        best = dt if best is None else min(best, dt)
+    _, ok_all = shard.gather_and_verify(d_out, dst=0, bufs=bufs, device=dev)
+    moved = (world - 1) * d_out.numel()
+    return {"what": f"all {d_out.shape[0]} mosaics of every rank -> rank 0 (RCCL send/recv)",
+            "bytes_into_rank0": moved, "ms": round(best * 1e3, 3),
+            "GBps_into_rank0": round(moved / best / 1e9, 1), "verified": ok_all,
+            "in_timed_region": args.gather == "timed"}
+
+
+def stub_main(args, world, rank):
+    """CPU rehearsal of the multi-rank bench orchestration (gloo): the same spawn, world check,
+    timed region, max over ranks, job rate and verified gather as the GPU path, around a stub
+    step (a small host copy standing in for one stitch launch)."""
+    import torch
+    import torch.distributed as dist
+    from multicamera_stitching_amd import shard
+    if world > 1:
+        dist.init_process_group("gloo")
+    dev = torch.device("cpu")
+    F, out_h, out_w, C = 4, 32, 48, 3
+    src = torch.arange(F * out_h * out_w * C, dtype=torch.int64).remainder(251).to(torch.uint8)
+    d_out = torch.empty((F, out_h, out_w * C), dtype=torch.uint8)
+
+    def step():
+        d_out.view(-1).copy_(src.roll(rank + 1))
+        time.sleep(0.002 * (rank + 1))          # ranks of different speed: max over ranks
+
+    elapsed = shard.timed_loop(step, args.steps, args.warmup, lambda: None)
+    mine = elapsed
+    elapsed = shard.max_over_ranks([elapsed], device=dev)[0]
+    mpix = F * out_w * out_h / 1e6
+    gather = None
+    if world > 1 and args.gather != "none":
+        got, ok = shard.gather_and_verify(d_out, dst=0, device=dev)
+        gather = {"verified": ok, "ranks": None if got is None else len(got),
+                  "bytes_into_rank0": (world - 1) * d_out.numel()}
+    result = None
+    if rank == 0:
+        result = {"metric": "stub (orchestration rehearsal, no GPU)",
+                  "value": round(shard.job_rate(mpix, args.steps, elapsed, world), 6),
+                  "unit": "MPix/s", "n_gpus": world, "steps": args.steps,
+                  "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+                  "rank0_seconds": mine, "max_seconds": elapsed,
+                  "mpix_per_step_per_rank": mpix, "higher_is_better": True, "scaling": "weak",
+                  "gather": gather, "config": {"workload": "stub"}}
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.barrier()

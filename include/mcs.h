@@ -89,6 +89,10 @@ typedef struct mcs_plan mcs_plan;
 /* Library / device info. */
 const char *mcs_version(void);
 int mcs_abi_version(void);
+/* Identity of the kernels this library runs: the first 16 hex digits of the SHA-256 of its
+ * embedded gfx950 code objects (profiles/ PMC summaries record it, and bench.py reports their
+ * HBM traffic only for the same build). */
+const char *mcs_build_id(void);
 const char *mcs_last_error(void);
 int mcs_device_count(int *n);
 /* The HIP runtime libmcs bound to (it links none: it uses the process's, e.g. PyTorch's). */
@@ -217,12 +221,17 @@ int mcs_plan_footprint(mcs_plan *plan, int64_t *touched_px, int n_cams);
  * place) are uploaded on a copy stream, stitched on a compute stream (one hipGraph per slot when
  * use_graphs), and the mosaic downloaded on a second copy stream -- so consecutive captures
  * overlap upload, stitch and download.  wait: blocks for that slot's mosaic and copies it to
- * `out` (out_h x out_w x C, dense); a slot must be collected before it is reused.  The plan
- * (blend mode included) is fixed for the stream's lifetime; the stream is bound to the device
- * current at creation. */
+ * `out` (out_h x out_w x C, dense; NULL: no copy, read mcs_stream_output instead); a slot must
+ * be collected before it is reused.  The plan (blend mode included) is fixed for the stream's
+ * lifetime; the stream lives on the plan's device.  Zero-copy use: the producer writes the next
+ * slot's frames into mcs_stream_input(mcs_stream_next_slot()) and submits NULL, the consumer
+ * reads mcs_stream_output(slot) after mcs_stream_wait(slot, NULL) until that slot's next
+ * submit -- the pipeline then moves bytes only over PCIe. */
 typedef struct mcs_stream mcs_stream;
 int mcs_stream_create(mcs_plan *plan, int depth, int use_graphs, mcs_stream **out);
 uint8_t *mcs_stream_input(mcs_stream *stream, int slot, int cam);
+/* The pinned host mosaic of `slot` (out_h x out_w x C, dense), NULL for a bad slot. */
+const uint8_t *mcs_stream_output(const mcs_stream *stream, int slot);
 int mcs_stream_next_slot(const mcs_stream *stream);
 int mcs_stream_submit(mcs_stream *stream, const uint8_t *const *cams, int *slot);
 /* mcs_stream_submit with a row pitch (bytes) per camera: camera c is cam_h rows of
@@ -279,15 +288,22 @@ int mcs_match_l2_knn2_host(const float *query, int n_query, const float *train, 
 
 /* ---- Homography estimation ----------------------------------------------
  * RANSAC homography of n correspondences src_xy[i] -> dst_xy[i] (float x, y pairs), the role of
- * cv2.findHomography(ptsA, ptsB, cv2.RANSAC, reprojThresh) at StitcherClass.py:440-441.  `iters`
+ * cv2.findHomography(ptsA, ptsB, cv2.RANSAC, reprojThresh) at StitcherClass.py:443-444.  `iters`
  * hypotheses (4-point DLT, FP64) are scored in parallel on the GPU (one workgroup each); the
- * most-supported one (ties: lowest index) gives the inlier mask, and a least-squares refit over
- * its inliers gives H (row-major 3x3, H[8] = 1).  Deterministic for a given seed; algorithm
- * specified in csrc/mcs_ransac_core.h.  *n_inliers = 0 and H = 0 when no model (n < 4 or no
+ * most-supported one (ties: lowest index) gives the inlier mask; then, as findHomography does
+ * after its RANSAC loop (n > 4), the model is re-estimated on its inliers (Hartley-normalised
+ * DLT, Jacobi eigenvector) and refined by 10 Levenberg-Marquardt iterations
+ * (mcs_homography_refine_host).  H: row-major 3x3.  Deterministic for a given seed; hypothesis
+ * algorithm specified in csrc/mcs_ransac_core.h, refinement in csrc/mcs_refine.cpp.  *n_inliers = 0 and H = 0 when no model (n < 4 or no
  * hypothesis with >= 4 inliers), like the reference's H = None.  mask may be NULL. */
 int mcs_ransac_homography_host(const float *src_xy, const float *dst_xy, int n, double thresh,
                                int iters, uint32_t seed, double *H, uint8_t *mask,
                                int *n_inliers, int device);
+/* findHomography's post-RANSAC stage alone (host FP64, no GPU): H (9 doubles) holds the RANSAC
+ * model on entry and the refined one on return; mask[i] != 0 marks the inliers.  n <= 4 or no
+ * inlier: H unchanged. */
+int mcs_homography_refine_host(const float *src_xy, const float *dst_xy, int n,
+                               const uint8_t *mask, double *H);
 
 #ifdef __cplusplus
 }

@@ -47,6 +47,17 @@ def _env_interp() -> int:
     return INTERP.get(os.environ.get("MCS_INTERP", "linear").lower(), _capi.MCS_INTER_LINEAR)
 
 
+BLEND = {"none": _capi.MCS_BLEND_NONE, "paste": _capi.MCS_BLEND_NONE,
+         "feather": _capi.MCS_BLEND_FEATHER, "multiband": _capi.MCS_BLEND_MULTIBAND,
+         "seam": _capi.MCS_BLEND_SEAM}
+
+
+def _env_blend() -> int:
+    """MCS_BLEND (extension, default "none" = the reference's overwrite paste, :240-241):
+    "feather" / "multiband" blend the seams, "seam" = owner only."""
+    return BLEND.get(os.environ.get("MCS_BLEND", "none").lower(), _capi.MCS_BLEND_NONE)
+
+
 def is_cv3(or_better=False):
     """Reference helper (StitcherClass.py:30-39); False when OpenCV is absent."""
     major = get_opencv_major_version()
@@ -97,8 +108,10 @@ class _PlanCache(object):
 
     def get(self, key, make):
         if key != self.key or self.plan is None:
-            if self.plan is not None:
-                self.plan.close()
+            # drop the cache's reference only: a plan handed out by Stitcher.plan() (e.g. to a
+            # live StreamPipeline, whose native stream and captured graphs use its tables) stays
+            # alive until its last holder lets go (Plan.__del__ -> mcs_plan_destroy)
+            self.plan = None
             self.plan = make()
             self.key = key
         return self.plan
@@ -154,8 +167,9 @@ class Stitcher(_Transient, Debugger):
 
         homographies (extension, default None = feature matching like the reference): a list
         with one A->B 3x3 matrix (or None) per stage, or a callable
-        ``f(stage_index, stitcher_base, imageB, imageA) -> H or None``, for rigs whose
-        homographies are known in advance (north-star config 2, synthetic rigs, tests).
+        ``f(stage_index, stitcher_base, imageB, imageA) -> H or None`` (imageB: the mosaic of
+        the earlier stages, stitched as the reference does), for rigs whose homographies are
+        known in advance (north-star config 2, synthetic rigs, tests).
         """
         if homographies is None and not _features_available():
             self.debugger(DEBUG_LEVEL_0, "No feature backend for calibration (OpenCV contrib "
@@ -173,10 +187,12 @@ class Stitcher(_Transient, Debugger):
             self.stitchers[idx].calibrate(images=images, ratio=0.75, reprojThresh=3.0,
                                           xoffset=0, yoffset=0, homography=H,
                                           use_features=homographies is None)
-            if homographies is None:
+            if homographies is None or callable(homographies):
+                # the next stage's B is the real mosaic so far: the reference's features, or a
+                # callable that may estimate its H from imageB's pixels, see it
                 img_result = self.stitchers[idx].stitch(images=images)
             else:
-                # only the next stage's B shape is needed: no pixels, no device work
+                # a list of matrices needs only the next stage's B shape: no pixels, no GPU work
                 img_result = _shape_only(_stage_out_shape(self.stitchers[idx], images[0]))
         for stitcher in self.stitchers:
             self.debugger(DEBUG_LEVEL_0, "[STITCHER]: {}".format(stitcher),
@@ -370,11 +386,17 @@ class StitcherBase(_Transient, Debugger):
 def _get_plan(owner, chain, cam0_shape, channels, interp=None, device=None):
     interp = _env_interp() if interp is None else interp
     device = _env_device() if device is None else device
+    blend = _env_blend()
     descs = [_stage_desc(sb) for sb in chain]
-    key = _plan_key(descs, cam0_shape, channels, interp, device)
+    key = _plan_key(descs, cam0_shape, channels, interp, device) + (blend,)
     cache = owner._cache()
-    return cache.get(key, lambda: _capi.Plan(descs, cam0_shape[1], cam0_shape[0], channels,
-                                             interp, device))
+
+    def make():
+        plan = _capi.Plan(descs, cam0_shape[1], cam0_shape[0], channels, interp, device)
+        if blend != _capi.MCS_BLEND_NONE:
+            plan.set_blend(blend)
+        return plan
+    return cache.get(key, make)
 
 
 def _conform_cameras(owner, chain, cams):

@@ -44,7 +44,7 @@ EXPORTS = (
     "mcs_plan_create_cylindrical", "mcs_plan_find_seams", "mcs_plan_seam_labels",
     "mcs_seam_graphcut_host", "mcs_plan_create_warp", "mcs_plan_create_undistort",
     "mcs_undistort_map_host", "mcs_match_l2_knn2", "mcs_match_l2_knn2_host",
-    "mcs_stream_submit_strided",
+    "mcs_stream_submit_strided", "mcs_build_id", "mcs_homography_refine_host", "mcs_stream_output",
 )
 
 
@@ -150,6 +150,8 @@ def load() -> ctypes.CDLL:
         L.mcs_version.argtypes = []
         L.mcs_abi_version.restype = I
         L.mcs_abi_version.argtypes = []
+        L.mcs_build_id.restype = ctypes.c_char_p
+        L.mcs_build_id.argtypes = []
         L.mcs_hip_runtime.restype = ctypes.c_char_p
         L.mcs_hip_runtime.argtypes = []
         L.mcs_last_error.restype = ctypes.c_char_p
@@ -177,10 +179,14 @@ def load() -> ctypes.CDLL:
         L.mcs_ransac_homography_host.argtypes = [P, P, I, ctypes.c_double, I, ctypes.c_uint32,
                                                  P, P, ctypes.POINTER(I), I]
         L.mcs_ransac_homography_host.restype = I
+        L.mcs_homography_refine_host.argtypes = [P, P, I, P, P]
+        L.mcs_homography_refine_host.restype = I
         L.mcs_stream_create.argtypes = [P, I, I, ctypes.POINTER(P)]
         L.mcs_stream_create.restype = I
         L.mcs_stream_input.argtypes = [P, I, I]
         L.mcs_stream_input.restype = P
+        L.mcs_stream_output.argtypes = [P, I]
+        L.mcs_stream_output.restype = P
         L.mcs_stream_next_slot.argtypes = [P]
         L.mcs_stream_next_slot.restype = I
         L.mcs_stream_submit.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(I)]
@@ -241,6 +247,11 @@ def check(rc: int):
     if rc != MCS_OK:
         msg = load().mcs_last_error()
         raise McsError(rc, msg.decode() if msg else "")
+
+
+def build_id() -> str:
+    """SHA-256 prefix of the embedded gfx950 code objects (mcs_build_id)."""
+    return load().mcs_build_id().decode()
 
 
 def hip_runtime() -> str:
@@ -478,6 +489,19 @@ def match_hamming_knn2_device(q_ptr: int, nq: int, t_ptr: int, nt: int, idx_ptr:
                                         stream or None))
 
 
+def homography_refine(src, dst, mask, H):
+    """findHomography's post-RANSAC refinement (mcs_homography_refine_host, host FP64):
+    normalised DLT on the inliers + 10 Levenberg-Marquardt iterations from the model H."""
+    L = load()
+    src = np.ascontiguousarray(src, np.float32).reshape(-1, 2)
+    dst = np.ascontiguousarray(dst, np.float32).reshape(-1, 2)
+    m = np.ascontiguousarray(np.asarray(mask).reshape(-1), np.uint8)
+    h = np.ascontiguousarray(np.asarray(H, np.float64).reshape(9)).copy()
+    check(L.mcs_homography_refine_host(src.ctypes.data, dst.ctypes.data, src.shape[0],
+                                       m.ctypes.data, h.ctypes.data))
+    return h.reshape(3, 3)
+
+
 def ransac_homography(src, dst, thresh: float, iters: int = 2000, seed: int = 0,
                       device: int = 0):
     """RANSAC homography on the GPU (mcs.h): (H 3x3 or None, status mask (n, 1) uint8), the
@@ -508,8 +532,27 @@ class StreamPipeline:
                                           ctypes.byref(h)))
         self._h = h
 
+    def _check_frames(self, cams):
+        """The pipeline copies cam_w * C * cam_h bytes per camera from each frame: refuse
+        anything that is not exactly the plan's camera (count, (h, w[, C]), uint8).  Frames off
+        their calibrated size go through Stitcher.stitch, which resizes them like the reference
+        (StitcherClass.py:226-233)."""
+        C = self.plan.channels
+        if len(cams) != self.plan.n_cams:
+            raise ValueError(f"{len(cams)} frames for a plan of {self.plan.n_cams} cameras")
+        out = []
+        for i, (c, (h, w)) in enumerate(zip(cams, self.plan.cam_shapes)):
+            c = np.asarray(c)
+            if c.dtype != np.uint8:
+                raise ValueError(f"camera {i}: dtype {c.dtype}, expected uint8")
+            want = (h, w) if C == 1 and c.ndim == 2 else (h, w, C)
+            if tuple(c.shape) != want:
+                raise ValueError(f"camera {i}: frame shape {c.shape}, the plan expects {want}")
+            out.append(np.ascontiguousarray(c))
+        return out
+
     def submit(self, cams) -> int:
-        cams = [np.ascontiguousarray(c, dtype=np.uint8) for c in cams]
+        cams = self._check_frames(cams)
         ptrs = (ctypes.c_void_p * len(cams))(*[c.ctypes.data for c in cams])
         slot = ctypes.c_int(-1)
         check(self._lib.mcs_stream_submit(self._h, ptrs, ctypes.byref(slot)))
@@ -520,10 +563,14 @@ class StreamPipeline:
         (np.concatenate(images, axis=1), video_mapping_node.py:140), in the plan's camera
         order; gathered into the pinned slot without an intermediate copy per camera."""
         frame = np.asarray(frame)
-        if frame.dtype != np.uint8 or frame.strides[-1] != 1 or (
-                frame.ndim == 3 and frame.strides[1] != frame.shape[2]):
-            frame = np.ascontiguousarray(frame, dtype=np.uint8)
         C = self.plan.channels
+        if frame.dtype != np.uint8:
+            raise ValueError(f"bus frame dtype {frame.dtype}, expected uint8")
+        if (frame.ndim == 3 and frame.shape[2] != C) or (frame.ndim == 2 and C != 1) or \
+                frame.ndim not in (2, 3):
+            raise ValueError(f"bus frame shape {frame.shape} for a {C}-channel plan")
+        if frame.strides[-1] != 1 or (frame.ndim == 3 and frame.strides[1] != frame.shape[2]):
+            frame = np.ascontiguousarray(frame)
         pitch = frame.strides[0]
         ptrs, pitches, x = [], [], 0
         for (h, w) in self.plan.cam_shapes:
@@ -540,9 +587,53 @@ class StreamPipeline:
         check(self._lib.mcs_stream_submit_strided(self._h, pp, rp, ctypes.byref(slot)))
         return slot.value
 
-    def wait(self, slot: int, out=None) -> np.ndarray:
+    def next_slot(self) -> int:
+        """The slot the next submit fills (McsError if it has not been collected yet)."""
+        r = self._lib.mcs_stream_next_slot(self._h)
+        if r < 0:
+            check(r)
+        return r
+
+    def input_views(self, slot: int):
+        """Zero-copy producer side: numpy views of `slot`'s pinned input buffers, one per
+        camera ((h, w[, C]) uint8), to be filled in place before submit_inplace()."""
+        C = self.plan.channels
+        views = []
+        for i, (h, w) in enumerate(self.plan.cam_shapes):
+            p = self._lib.mcs_stream_input(self._h, int(slot), i)
+            if not p:
+                raise McsError(MCS_E_INVALID, f"no input buffer for slot {slot} camera {i}")
+            buf = (ctypes.c_uint8 * (h * w * C)).from_address(p)
+            views.append(np.frombuffer(buf, np.uint8).reshape((h, w) if C == 1 else (h, w, C)))
+        return views
+
+    def submit_inplace(self) -> int:
+        """Submit the next slot with the frames already written into its input_views()."""
+        slot = ctypes.c_int(-1)
+        check(self._lib.mcs_stream_submit(self._h, None, ctypes.byref(slot)))
+        return slot.value
+
+    def output_view(self, slot: int) -> np.ndarray:
+        """Zero-copy consumer side: the pinned mosaic of `slot` (valid after wait(slot,
+        copy=False) until the slot is submitted again)."""
+        p = self._lib.mcs_stream_output(self._h, int(slot))
+        if not p:
+            raise McsError(MCS_E_INVALID, f"no output buffer for slot {slot}")
+        shape = self.plan.out_shape()
+        buf = (ctypes.c_uint8 * int(np.prod(shape))).from_address(p)
+        return np.frombuffer(buf, np.uint8).reshape(shape)
+
+    def wait(self, slot: int, out=None, copy: bool = True) -> np.ndarray:
+        if not copy:
+            check(self._lib.mcs_stream_wait(self._h, slot, None))
+            return self.output_view(slot)
         if out is None:
             out = np.empty(self.plan.out_shape(), np.uint8)
+        elif not (isinstance(out, np.ndarray) and out.dtype == np.uint8 and
+                  out.flags.c_contiguous and out.flags.writeable and
+                  tuple(out.shape) == self.plan.out_shape()):
+            raise ValueError(f"out must be a writeable C-contiguous uint8 array of shape "
+                             f"{self.plan.out_shape()}")
         check(self._lib.mcs_stream_wait(self._h, slot, out.ctypes.data))
         return out
 

@@ -12,6 +12,7 @@ Usage: python -m multicamera_stitching_amd.build [--force]
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import subprocess
 import sys
@@ -28,7 +29,7 @@ ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.environ.get("HIPCC", os.path.join(ROCM, "bin", "hipcc"))
 CXX = os.environ.get("CXX", "g++")
 HOST_SRC = ["mcs_plan.cpp", "hip_rt.cpp", "mcs_runtime.cpp", "mcs_capi.cpp", "mcs_features.cpp",
-            "mcs_stream.cpp", "mcs_seam.cpp"]
+            "mcs_stream.cpp", "mcs_seam.cpp", "mcs_refine.cpp"]
 HEADERS = ["mcs_kparams.h", "mcs_fparams.h", "mcs_common.h", "hip_rt.h", "mcs_blend.h", "mcs_ransac_core.h",
            "mcs_orb_core.h", "mcs_orb_pattern.h"]
 INC = ["-I" + os.path.join(ROOT, "include"), "-I" + CSRC]
@@ -79,6 +80,11 @@ def _build_to(LIB: str, HSACO: str, defines, verbose: bool) -> str:
               os.path.join(CSRC, src)], verbose)
         os.replace(out + ".tmp", out)
         objs[name] = out
+    digest = hashlib.sha256()
+    for name in sorted(objs):
+        with open(objs[name], "rb") as f:
+            digest.update(f.read())
+    build_id = digest.hexdigest()[:16]
     blob = LIB + ".blob.S"
     with open(blob, "w") as f:
         f.write("    .section .rodata\n")
@@ -87,7 +93,8 @@ def _build_to(LIB: str, HSACO: str, defines, verbose: bool) -> str:
                     '    .incbin "%s"\n    .byte 0\n' % (name, name, path))
         f.write('    .section .note.GNU-stack,"",@progbits\n')
     try:
-        _run([CXX, *HOST_FLAGS, *["-D" + d for d in defines], *INC, "-o", LIB + ".tmp",
+        _run([CXX, *HOST_FLAGS, *["-D" + d for d in defines], f'-DMCS_BUILD_ID="{build_id}"',
+              *INC, "-o", LIB + ".tmp",
               *[os.path.join(CSRC, s) for s in HOST_SRC], blob, "-ldl", "-lpthread"], verbose)
     finally:
         os.remove(blob)

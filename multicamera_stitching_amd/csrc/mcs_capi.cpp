@@ -64,6 +64,8 @@ struct mcs_plan {
     int32_t *d_map = nullptr;
 };
 
+int mcs::plan_device(const mcs_plan *plan) { return plan ? plan->device : 0; }
+
 #define MCS_VERSION_STRING "mcs 0.1.0 (gfx950 code object, HIP module launch)"
 
 namespace {
@@ -568,6 +570,11 @@ extern "C" {
 const char *mcs_version(void) { return MCS_VERSION_STRING; }
 
 int mcs_abi_version(void) { return MCS_ABI_VERSION; }
+
+#ifndef MCS_BUILD_ID
+#define MCS_BUILD_ID "unknown"
+#endif
+const char *mcs_build_id(void) { return MCS_BUILD_ID; }
 
 const char *mcs_hip_runtime(void)
 {

@@ -37,6 +37,12 @@ enum Module { kModStitch = 0, kModFeatures = 1, kNumModules = 2 };
 constexpr int kMaxDevices = 64;
 // Loads module `m` on `device` once (the device must be current) and looks up `name`.
 int module_function(const rt::Api *A, int device, Module m, const char *name, hipFunction_t *out);
+// findHomography's post-RANSAC stage (mcs_refine.cpp): normalised DLT on the inliers of `mask`
+// + 10 Levenberg-Marquardt iterations; H (9 doubles) holds the RANSAC model on entry.
+void homography_refine(const float *src_xy, const float *dst_xy, int n, const uint8_t *mask,
+                       double *H);
+// The HIP device a plan was created for (its tables, buffers and side streams live there).
+int plan_device(const mcs_plan *plan);
 
 // Makes `dev` current for the duration of a call and restores the caller's device.
 struct DeviceGuard {

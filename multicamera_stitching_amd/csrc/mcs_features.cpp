@@ -412,20 +412,11 @@ int mcs_ransac_homography_host(const float *src_xy, const float *dst_xy, int n, 
     if (e != hipSuccess) return mcs::fail(MCS_E_HIP, "ransac: %s", A->hipGetErrorString(e));
     if (rc) return rc;
     if (best_score < 4) return MCS_OK;
-    // least-squares refit over the best hypothesis' inliers (8x8 normal equations, point order)
-    double M[8][9] = {};
-    for (int i = 0; i < n; i++) {
-        if (!m8[i]) continue;
-        double ru[9], rv[9];
-        mcs::rs_rows(pts[4 * i], pts[4 * i + 1], pts[4 * i + 2], pts[4 * i + 3], ru, rv);
-        for (const double *r : {ru, rv})
-            for (int p = 0; p < 8; p++)
-                for (int q = 0; q < 9; q++) M[p][q] = M[p][q] + r[p] * r[q];
-    }
-    double hr[8];
-    const bool ok = mcs::rs_solve8(M, hr);
-    for (int i = 0; i < 8; i++) H[i] = ok ? hr[i] : hb8[i];
+    // findHomography's refinement of the chosen model on its inliers (mcs_refine.cpp:
+    // normalised DLT re-estimate + Levenberg-Marquardt, StitcherClass.py:443-444)
+    for (int i = 0; i < 8; i++) H[i] = hb8[i];
     H[8] = 1.0;
+    mcs::homography_refine(src_xy, dst_xy, n, m8.data(), H);
     *n_inliers = best_score;
     if (mask)
         for (int i = 0; i < n; i++) mask[i] = m8[i];

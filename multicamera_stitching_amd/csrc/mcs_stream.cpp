@@ -121,10 +121,15 @@ int mcs_stream_create(mcs_plan *plan, int depth, int use_graphs, mcs_stream **ou
     if (fd.out_w <= 0 || fd.out_h <= 0) return mcs::fail(MCS_E_SHAPE, "empty mosaic");
     const Api *A = mcs::rt::api();
     if (!A) return MCS_E_HIP;
-    int dev = 0;
-    HIP_TRY(A->hipGetDevice(&dev));
+    // streams, pinned slots and device buffers live on the plan's device, whatever device the
+    // caller has current (the stitch itself switches to plan->device)
+    const int dev = mcs::plan_device(plan);
+    mcs::DeviceGuard g(A, dev);
+    if (g.err != hipSuccess)
+        return mcs::fail(MCS_E_HIP, "device %d: %s", dev, A->hipGetErrorString(g.err));
     mcs_stream *s = new (std::nothrow) mcs_stream();
     if (!s) return mcs::fail(MCS_E_NOMEM, "stream");
+    s->device = dev;
     s->plan = plan;
     s->depth = depth;
     s->graphs = use_graphs != 0;
@@ -145,7 +150,6 @@ int mcs_stream_create(mcs_plan *plan, int depth, int use_graphs, mcs_stream **ou
         delete s;
         return rc;
     }
-    s->device = dev;
     *out = s;
     return MCS_OK;
 }
@@ -154,6 +158,12 @@ uint8_t *mcs_stream_input(mcs_stream *s, int slot, int cam)
 {
     if (!s || slot < 0 || slot >= s->depth || cam < 0 || cam >= s->n_cams) return nullptr;
     return s->slot[slot].h_in + s->cam_off[cam];
+}
+
+const uint8_t *mcs_stream_output(const mcs_stream *s, int slot)
+{
+    if (!s || slot < 0 || slot >= s->depth) return nullptr;
+    return s->slot[slot].h_out;
 }
 
 int mcs_stream_next_slot(const mcs_stream *s)

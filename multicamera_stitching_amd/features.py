@@ -6,7 +6,8 @@ runs once per calibration (a keypress, video_mapping_node.py:187-188), not per f
 
 Backends (MCS_FEATURES = auto | sift | orb): "sift" is OpenCV contrib SIFT when cv2 is
 importable (the reference's own algorithm; its float L2 kNN-2 runs on the GPU unless
-MCS_L2_MATCHER=cv2, exact for SIFT's integer-valued descriptors); "orb" is the GPU path of
+MCS_L2_MATCHER=cv2, exact for SIFT's integer-valued descriptors, and so does findHomography's
+RANSAC + LM refinement unless MCS_HOMOGRAPHY=cv2); "orb" is the GPU path of
 SURVEY.md 8 NS-3..5 -- ORB (mcs_orb_detect_host), brute-force Hamming kNN-2
 (mcs_match_hamming_knn2_host), the same ratio test, RANSAC (mcs_ransac_homography_host).  "auto"
 prefers SIFT (reference behaviour) and falls back to ORB when a GPU is present.  With neither,
@@ -116,7 +117,13 @@ def match_keypoints(owner, kpsA, kpsB, featuresA, featuresB, ratio=0.75, reprojT
     if len(matches) > 4:
         ptsA = np.float32([kpsA[i] for (_, i) in matches])
         ptsB = np.float32([kpsB[i] for (i, _) in matches])
-        H, status = cv2.findHomography(ptsA, ptsB, cv2.RANSAC, reprojThresh)
+        if os.environ.get("MCS_HOMOGRAPHY", "gpu") == "cv2" and cv2 is not None:
+            H, status = cv2.findHomography(ptsA, ptsB, cv2.RANSAC, reprojThresh)
+        else:
+            # findHomography(RANSAC) on the GPU + its LM refinement (mcs_ransac_homography_host):
+            # calibration needs no cv2 once the descriptors exist
+            from . import _capi
+            H, status = _capi.ransac_homography(ptsA, ptsB, reprojThresh)
     return H, matches, status
 
 

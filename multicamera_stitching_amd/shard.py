@@ -9,6 +9,7 @@ buffer).
 """
 from __future__ import annotations
 
+import time
 from typing import List, Sequence
 
 
@@ -29,11 +30,13 @@ def max_over_ranks(values: Sequence[float], device=None) -> List[float]:
     return [float(v) for v in t.cpu()]
 
 
-def gather_mosaics(local, dst: int = 0):
+def gather_mosaics(local, dst: int = 0, bufs=None):
     """Collect every rank's finished mosaics (same shape on every rank) on rank `dst`.
 
     Returns the list of per-rank tensors on `dst` (rank order), None elsewhere.  Point-to-point
     sends to the consumer, not a ring collective: each peer's transfer uses its own xGMI link.
+    bufs (on `dst`): preallocated receive tensors, one per peer in rank order (reused across
+    calls); fresh ones otherwise.
     """
     import torch
     import torch.distributed as dist
@@ -41,10 +44,76 @@ def gather_mosaics(local, dst: int = 0):
         return [local]
     world, rank = dist.get_world_size(), dist.get_rank()
     if rank == dst:
-        out = [local if r == dst else torch.empty_like(local) for r in range(world)]
+        peers = iter(bufs) if bufs is not None else None
+        out = [local if r == dst else (next(peers) if peers else torch.empty_like(local))
+               for r in range(world)]
         reqs = [dist.irecv(out[r], src=r) for r in range(world) if r != dst]
         for q in reqs:
             q.wait()
         return out
     dist.send(local, dst=dst)
     return None
+
+
+def timed_loop(step, steps: int, warmup: int, sync, record=None) -> float:
+    """The bench contract's timed region on this rank: `warmup` untimed steps, then exactly
+    `steps` timed ones bracketed on both sides by (sync, barrier, sync); returns this rank's
+    wall seconds (reduce with max_over_ranks).  record(i, "start"|"end") brackets step i (HIP
+    events on the kernels' stream)."""
+    import torch.distributed as dist
+    multi = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    for _ in range(warmup):
+        step()
+    sync()
+    if multi:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        if record:
+            record(i, "start")
+        step()
+        if record:
+            record(i, "end")
+    sync()
+    if multi:
+        dist.barrier()
+    sync()
+    return time.perf_counter() - t0
+
+
+def job_rate(units_per_step_per_rank: float, steps: int, seconds_max: float, world: int) -> float:
+    """Whole-job throughput: the units every rank processed over the slowest rank's time."""
+    return world * units_per_step_per_rank * steps / seconds_max
+
+
+def checksum(t) -> int:
+    """Order-sensitive 63-bit checksum of a u8 tensor's bytes (position-weighted sum), computed
+    where the tensor lives; used to verify gathered mosaics against their producers."""
+    import torch
+    flat = t.reshape(-1).to(torch.int64)
+    w = torch.arange(1, flat.numel() + 1, device=flat.device, dtype=torch.int64) % 65521
+    return int((flat * w).sum().item()) & ((1 << 63) - 1)
+
+
+def gather_and_verify(local, dst: int = 0, bufs=None, device=None):
+    """gather_mosaics + a checksum-of-checksums check: every rank's checksum of what it sent is
+    all-gathered, and `dst` compares them with checksums of what it received.  Returns
+    (mosaics on dst or None, ok on every rank)."""
+    import torch
+    import torch.distributed as dist
+    got = gather_mosaics(local, dst, bufs)
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    mine = torch.tensor([checksum(local)], dtype=torch.int64, device=device)
+    sums = [torch.zeros_like(mine) for _ in range(world)]
+    if world > 1:
+        dist.all_gather(sums, mine)
+    else:
+        sums = [mine]
+    ok = True
+    if got is not None:
+        ok = all(checksum(g) == int(s.item()) for g, s in zip(got, sums))
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int64, device=device)
+    if world > 1:
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    return got, bool(flag.item())

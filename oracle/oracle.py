@@ -80,6 +80,8 @@ def lib():
         L.orc_ransac_homography.argtypes = [P, ctypes.c_int, ctypes.c_double, ctypes.c_int,
                                             ctypes.c_uint32, P, P, P]
         L.orc_ransac_homography.restype = ctypes.c_int
+        L.orc_homography_refine.argtypes = [P, ctypes.c_int, P, P]
+        L.orc_homography_refine.restype = None
         L.orc_orb_detect.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_float, ctypes.c_int, P, P, P, P, P, P]
         L.orc_orb_detect.restype = ctypes.c_int
@@ -362,6 +364,18 @@ def ransac_homography(src, dst, thresh, iters=2000, seed=0):
     best = lib().orc_ransac_homography(_p(pts), n, float(thresh), iters, seed & 0xffffffff,
                                        _p(scores), _p(mask), _p(H))
     return (None if best < 0 else H.reshape(3, 3)), mask, best, scores
+
+
+def homography_refine(src, dst, mask, H):
+    """findHomography's post-RANSAC refinement restated (orc_ransac.c orc_homography_refine):
+    normalised DLT on the inliers + 10 LM iterations, starting from the 3x3 model H."""
+    src = np.asarray(src, np.float32).reshape(-1, 2)
+    dst = np.asarray(dst, np.float32).reshape(-1, 2)
+    pts = np.ascontiguousarray(np.concatenate([src, dst], axis=1).astype(np.float64))
+    m = np.ascontiguousarray(np.asarray(mask).reshape(-1), np.uint8)
+    h = np.ascontiguousarray(np.asarray(H, np.float64).reshape(9)).copy()
+    lib().orc_homography_refine(_p(pts), pts.shape[0], _p(m), _p(h))
+    return h.reshape(3, 3)
 
 
 def orb_pattern() -> np.ndarray:

@@ -13,8 +13,8 @@
  *          magnitude >= 1e-12, FP64;
  *   score: w = (h6 x + h7 y) + 1, px = ((h0 x + h1 y) + h2) / w, ...; inlier iff w != 0 and
  *          (px - u)^2 + (py - v)^2 <= thresh^2;
- *   best:  most inliers, ties to the lowest k; needs >= 4; refit on its inliers by the 8x8
- *          normal equations accumulated in point order (u row, then v row).
+ *   best:  most inliers, ties to the lowest k; needs >= 4; then findHomography's own
+ *          refinement on its inliers (orc_homography_refine below).
  */
 #include <stdint.h>
 #include <string.h>
@@ -97,6 +97,8 @@ static int inlier(const double *h, const double *p, double t2)
     return ex * ex + ey * ey <= t2;
 }
 
+void orc_homography_refine(const double *pts, int n, const uint8_t *mask, double *H);
+
 /* pts: n x 4 (x, y, u, v).  scores[iters] (-1 = rejected), mask[n], H[9]; returns the best k or
  * -1 (no model). */
 int orc_ransac_homography(const double *pts, int n, double thresh, int iters, uint32_t seed,
@@ -135,21 +137,258 @@ int orc_ransac_homography(const double *pts, int n, double thresh, int iters, ui
         }
     }
     if (best_score < 4) return -1;
-    double M[8][9];
-    memset(M, 0, sizeof(M));
-    for (int i = 0; i < n; i++) {
-        mask[i] = (uint8_t)inlier(hbest, pts + 4 * i, t2);
-        if (!mask[i]) continue;
-        double ru[9], rv[9];
-        rows(pts[4 * i], pts[4 * i + 1], pts[4 * i + 2], pts[4 * i + 3], ru, rv);
-        for (int p = 0; p < 8; p++)
-            for (int q = 0; q < 9; q++) M[p][q] = M[p][q] + ru[p] * ru[q];
-        for (int p = 0; p < 8; p++)
-            for (int q = 0; q < 9; q++) M[p][q] = M[p][q] + rv[p] * rv[q];
-    }
-    double hr[8];
-    int ok = solve8(M, hr);
-    for (int i = 0; i < 8; i++) H[i] = ok ? hr[i] : hbest[i];
+    for (int i = 0; i < n; i++) mask[i] = (uint8_t)inlier(hbest, pts + 4 * i, t2);
+    for (int i = 0; i < 8; i++) H[i] = hbest[i];
     H[8] = 1.0;
+    orc_homography_refine(pts, n, mask, H);
     return best;
+}
+
+/* ---- findHomography's post-RANSAC stage (OpenCV 3.4 fundam.cpp / levmarq.cpp / lapack.cpp) ----
+ * Restated for the parity check of csrc/mcs_refine.cpp: the inliers (in point order) give a
+ * Hartley-normalised DLT (9x9 LtL, upper triangle summed then mirrored, Jacobi eigenvector of the
+ * smallest eigenvalue, invHnorm * H0 * Hnorm2, scaled by 1 / H33) that replaces the RANSAC model,
+ * then at most 10 Levenberg-Marquardt iterations refine h0..h7 (HomographyRefineCallback, h8 = 1
+ * in the residuals; steps by DECOMP_EIG solves of (JtJ + lambda diag JtJ) d = Jt r).  Reference
+ * call site: PostScripts/Stitcher/StitcherClass.py:443-444 (OpenCV itself is not vendored: the
+ * arithmetic is unpinned against a real cv2). */
+#include <float.h>
+#include <math.h>
+#include <stdlib.h>
+
+static double orc__hyp(double a, double b)
+{
+    a = fabs(a), b = fabs(b);
+    if (a > b) { b /= a; return a * sqrt(1 + b * b); }
+    if (b > 0) { a /= b; return b * sqrt(1 + a * a); }
+    return 0;
+}
+
+/* Jacobi eigen-decomposition of the symmetric n x n a (row-major, upper triangle used, destroyed):
+ * w descending, v rows = eigenvectors (cv::eigen, lapack.cpp JacobiImpl_). */
+static void orc__jacobi(double *a, int n, double *w, double *v)
+{
+    int ir[9], ic[9];
+    for (int i = 0; i < n * n; i++) v[i] = (i % (n + 1)) == 0 ? 1.0 : 0.0;
+#define ORC_ROWSCAN(k) do { int m_ = (k) + 1; double mv_ = fabs(a[(k) * n + m_]);           \
+        for (int i_ = (k) + 2; i_ < n; i_++) { double t_ = fabs(a[(k) * n + i_]);          \
+            if (mv_ < t_) mv_ = t_, m_ = i_; } ir[k] = m_; } while (0)
+#define ORC_COLSCAN(k) do { int m_ = 0; double mv_ = fabs(a[k]);                             \
+        for (int i_ = 1; i_ < (k); i_++) { double t_ = fabs(a[i_ * n + (k)]);             \
+            if (mv_ < t_) mv_ = t_, m_ = i_; } ic[k] = m_; } while (0)
+    for (int k = 0; k < n; k++) {
+        w[k] = a[k * n + k];
+        if (k < n - 1) ORC_ROWSCAN(k);
+        if (k > 0) ORC_COLSCAN(k);
+    }
+    for (int it = 0; it < n * n * 30; it++) {
+        int k = 0, l;
+        double mv = fabs(a[ir[0]]);
+        for (int i = 1; i < n - 1; i++)
+            if (mv < fabs(a[i * n + ir[i]])) mv = fabs(a[i * n + ir[i]]), k = i;
+        l = ir[k];
+        for (int i = 1; i < n; i++)
+            if (mv < fabs(a[ic[i] * n + i])) mv = fabs(a[ic[i] * n + i]), k = ic[i], l = i;
+        double p = a[k * n + l];
+        if (fabs(p) <= DBL_EPSILON) break;
+        double y = (w[l] - w[k]) * 0.5;
+        double t = fabs(y) + orc__hyp(p, y);
+        double s = orc__hyp(p, t);
+        double c = t / s;
+        s = p / s;
+        t = (p / t) * p;
+        if (y < 0) s = -s, t = -t;
+        a[k * n + l] = 0;
+        w[k] -= t;
+        w[l] += t;
+#define ORC_ROT(P0, P1) do { double a0_ = (P0), b0_ = (P1);                                   \
+        (P0) = a0_ * c - b0_ * s; (P1) = a0_ * s + b0_ * c; } while (0)
+        for (int i = 0; i < k; i++) ORC_ROT(a[i * n + k], a[i * n + l]);
+        for (int i = k + 1; i < l; i++) ORC_ROT(a[k * n + i], a[i * n + l]);
+        for (int i = l + 1; i < n; i++) ORC_ROT(a[k * n + i], a[l * n + i]);
+        for (int i = 0; i < n; i++) ORC_ROT(v[k * n + i], v[l * n + i]);
+        if (k < n - 1) ORC_ROWSCAN(k);
+        if (k > 0) ORC_COLSCAN(k);
+        if (l < n - 1) ORC_ROWSCAN(l);
+        if (l > 0) ORC_COLSCAN(l);
+#undef ORC_ROT
+    }
+#undef ORC_ROWSCAN
+#undef ORC_COLSCAN
+    for (int k = 0; k < n - 1; k++) {
+        int m = k;
+        for (int i = k + 1; i < n; i++)
+            if (w[m] < w[i]) m = i;
+        if (m == k) continue;
+        double t = w[m]; w[m] = w[k]; w[k] = t;
+        for (int i = 0; i < n; i++) { t = v[m * n + i]; v[m * n + i] = v[k * n + i]; v[k * n + i] = t; }
+    }
+}
+
+/* 1/w_i, or 0 for |w_i| <= 2 eps sum(w) (SVBkSb's threshold) */
+static void orc__eig8(const double *A, double *w, double *v, double *iw)
+{
+    double a[64], thr = 0;
+    memcpy(a, A, sizeof(a));
+    orc__jacobi(a, 8, w, v);
+    for (int i = 0; i < 8; i++) thr += w[i];
+    thr *= DBL_EPSILON * 2;
+    for (int i = 0; i < 8; i++) iw[i] = fabs(w[i]) <= thr ? 0.0 : 1 / w[i];
+}
+
+/* residuals r (2 per point) and Jacobian rows (8 per residual) of h at the m points */
+static void orc__lm_eval(const double *q, int m, const double *h, double *r, double *J)
+{
+    for (int i = 0; i < m; i++) {
+        double X = q[4 * i], Y = q[4 * i + 1];
+        double ww = h[6] * X + h[7] * Y + 1.;
+        ww = fabs(ww) > DBL_EPSILON ? 1. / ww : 0;
+        double xi = (h[0] * X + h[1] * Y + h[2]) * ww, yi = (h[3] * X + h[4] * Y + h[5]) * ww;
+        r[2 * i] = xi - q[4 * i + 2];
+        r[2 * i + 1] = yi - q[4 * i + 3];
+        if (!J) continue;
+        double *ju = J + 16 * i, *jv = ju + 8;
+        double u[8] = {X * ww, Y * ww, ww, 0., 0., 0., -X * ww * xi, -Y * ww * xi};
+        double vv[8] = {0., 0., 0., X * ww, Y * ww, ww, -X * ww * yi, -Y * ww * yi};
+        memcpy(ju, u, sizeof(u));
+        memcpy(jv, vv, sizeof(vv));
+    }
+}
+
+static void orc__jtj(const double *J, const double *r, int rows, double *A, double *g)
+{
+    for (int i = 0; i < 8; i++) {
+        for (int j = 0; j < 8; j++) {
+            double s = 0;
+            for (int q = 0; q < rows; q++) s += J[8 * q + i] * J[8 * q + j];
+            A[8 * i + j] = s;
+        }
+        double s = 0;
+        for (int q = 0; q < rows; q++) s += J[8 * q + i] * r[q];
+        g[i] = s;
+    }
+}
+
+static double orc__ss(const double *r, int rows)
+{
+    double s = 0;
+    for (int q = 0; q < rows; q++) s += r[q] * r[q];
+    return s;
+}
+
+/* pts: n x 4 doubles (x, y, u, v: float values), mask[n]; H[9] in: RANSAC model, out: refined. */
+void orc_homography_refine(const double *pts, int n, const uint8_t *mask, double *H)
+{
+    if (n <= 4) return;
+    int m = 0;
+    for (int i = 0; i < n; i++) m += mask[i] != 0;
+    if (m == 0) return;
+    double *q = (double *)malloc(sizeof(double) * 4 * (size_t)m);
+    for (int i = 0, k = 0; i < n; i++)
+        if (mask[i]) memcpy(q + 4 * k++, pts + 4 * i, 4 * sizeof(double));
+    /* runKernel on the inliers */
+    double cx = 0, cy = 0, cX = 0, cY = 0;
+    for (int i = 0; i < m; i++) cx += q[4 * i + 2], cy += q[4 * i + 3], cX += q[4 * i], cY += q[4 * i + 1];
+    cx /= m, cy /= m, cX /= m, cY /= m;
+    double sx = 0, sy = 0, sX = 0, sY = 0;
+    for (int i = 0; i < m; i++) {
+        sx += fabs(q[4 * i + 2] - cx), sy += fabs(q[4 * i + 3] - cy);
+        sX += fabs(q[4 * i] - cX), sY += fabs(q[4 * i + 1] - cY);
+    }
+    if (!(fabs(sx) < DBL_EPSILON || fabs(sy) < DBL_EPSILON || fabs(sX) < DBL_EPSILON ||
+          fabs(sY) < DBL_EPSILON)) {
+        sx = m / sx, sy = m / sy, sX = m / sX, sY = m / sY;
+        double L[81] = {0}, w9[9], v9[81];
+        for (int i = 0; i < m; i++) {
+            double x = (q[4 * i + 2] - cx) * sx, y = (q[4 * i + 3] - cy) * sy;
+            double X = (q[4 * i] - cX) * sX, Y = (q[4 * i + 1] - cY) * sY;
+            double lx[9] = {X, Y, 1, 0, 0, 0, -x * X, -x * Y, -x};
+            double ly[9] = {0, 0, 0, X, Y, 1, -y * X, -y * Y, -y};
+            for (int j = 0; j < 9; j++)
+                for (int k = j; k < 9; k++) L[9 * j + k] += lx[j] * lx[k] + ly[j] * ly[k];
+        }
+        for (int j = 1; j < 9; j++)
+            for (int k = 0; k < j; k++) L[9 * j + k] = L[9 * k + j];
+        orc__jacobi(L, 9, w9, v9);
+        const double *h0 = v9 + 72;
+        double ni[9] = {1. / sx, 0, cx, 0, 1. / sy, cy, 0, 0, 1};
+        double n2[9] = {sX, 0, -cX * sX, 0, sY, -cY * sY, 0, 0, 1};
+        double t[9], o[9];
+        for (int i = 0; i < 9; i++) {
+            int r = i / 3, c = i % 3;
+            t[i] = ni[3 * r] * h0[c] + ni[3 * r + 1] * h0[3 + c] + ni[3 * r + 2] * h0[6 + c];
+        }
+        for (int i = 0; i < 9; i++) {
+            int r = i / 3, c = i % 3;
+            o[i] = t[3 * r] * n2[c] + t[3 * r + 1] * n2[3 + c] + t[3 * r + 2] * n2[6 + c];
+        }
+        double sc = 1. / o[8];
+        for (int i = 0; i < 9; i++) H[i] = o[i] * sc;
+    }
+    /* LMSolver, 10 iterations */
+    const int rows = 2 * m;
+    double *r = (double *)malloc(sizeof(double) * (size_t)rows * 10);
+    double *rd = r + rows, *J = rd + rows;
+    double x[8], xd[8], A[64], g[8], D[8], lambda = 1, lc = 0.75;
+    memcpy(x, H, sizeof(x));
+    orc__lm_eval(q, m, x, r, J);
+    double S = orc__ss(r, rows);
+    orc__jtj(J, r, rows, A, g);
+    for (int i = 0; i < 8; i++) D[i] = A[9 * i];
+    for (int iter = 1;; iter++) {
+        double Ap[64], w[8], v[64], iw[8], d[8] = {0};
+        memcpy(Ap, A, sizeof(Ap));
+        for (int i = 0; i < 8; i++) Ap[9 * i] += lambda * D[i];
+        orc__eig8(Ap, w, v, iw);
+        for (int i = 0; i < 8; i++) {
+            if (iw[i] == 0.0) continue;
+            double s = 0;
+            for (int j = 0; j < 8; j++) s += v[8 * i + j] * g[j];
+            s *= iw[i];
+            for (int j = 0; j < 8; j++) d[j] = d[j] + s * v[8 * i + j];
+        }
+        for (int i = 0; i < 8; i++) xd[i] = x[i] - d[i];
+        orc__lm_eval(q, m, xd, rd, NULL);
+        double Sd = orc__ss(rd, rows), dS = 0;
+        for (int i = 0; i < 8; i++) {
+            double ad = 0;
+            for (int j = 0; j < 8; j++) ad += A[8 * i + j] * d[j];
+            dS += d[i] * (-ad + 2 * g[i]);
+        }
+        double R = (S - Sd) / (fabs(dS) > DBL_EPSILON ? dS : 1);
+        if (R > 0.75) {
+            lambda *= 0.5;
+            if (lambda < lc) lambda = 0;
+        } else if (R < 0.25) {
+            double t = 0;
+            for (int i = 0; i < 8; i++) t += d[i] * g[i];
+            double nu = (Sd - S) / (fabs(t) > DBL_EPSILON ? t : 1) + 2;
+            nu = nu < 2. ? 2. : (nu > 10. ? 10. : nu);
+            if (lambda == 0) {
+                double dg[8] = {0}, mx = DBL_EPSILON;
+                orc__eig8(A, w, v, iw);
+                for (int i = 0; i < 8; i++) {
+                    if (iw[i] == 0.0) continue;
+                    for (int j = 0; j < 8; j++) dg[j] = dg[j] + v[8 * i + j] * (v[8 * i + j] * iw[i]);
+                }
+                for (int i = 0; i < 8; i++) mx = fabs(dg[i]) > mx ? fabs(dg[i]) : mx;
+                lambda = lc = 1. / mx;
+                nu *= 0.5;
+            }
+            lambda *= nu;
+        }
+        if (Sd < S) {
+            S = Sd;
+            memcpy(x, xd, sizeof(x));
+            orc__lm_eval(q, m, x, r, J);
+            orc__jtj(J, r, rows, A, g);
+        }
+        double dm = 0, rm = 0;
+        for (int i = 0; i < 8; i++) dm = fabs(d[i]) > dm ? fabs(d[i]) : dm;
+        for (int i = 0; i < rows; i++) rm = fabs(r[i]) > rm ? fabs(r[i]) : rm;
+        if (!(iter < 10 && dm >= FLT_EPSILON && rm >= FLT_EPSILON)) break;
+    }
+    memcpy(H, x, sizeof(x));
+    free(r);
+    free(q);
 }

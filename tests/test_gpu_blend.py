@@ -94,3 +94,31 @@ def test_multiband_more_than_four_owners_is_refused():
     plan.set_blend(MODES["feather"])          # feather has no such limit
     want = oracle.blend_stitch(plan.describe(), cams, MODES["feather"])
     assert _diff(plan.stitch_host(cams).reshape(want.shape), want) == 0
+
+
+@pytest.mark.parametrize("interp", [0, 1])
+def test_c1_checker_feather_vs_oracle(interp, monkeypatch):
+    """BASELINE configs[0]: 2 x 640x480 checkerboard, H = translation(400, 0), nearest-neighbour
+    warp (and bilinear), linear feather blend -- through the drop-in Stitcher (MCS_BLEND=feather,
+    MCS_INTERP) on the GPU, bit-exact vs orc_blend.c; the 240-px overlap is a weighted mix."""
+    from multicamera_stitching_amd.StitcherClass import Stitcher
+    monkeypatch.setenv("MCS_BLEND", "feather")
+    monkeypatch.setenv("MCS_INTERP", "nearest" if interp == 0 else "linear")
+    yy, xx = np.mgrid[0:480, 0:640]
+    chk = np.where(((xx // 32) + (yy // 32)) % 2 == 0, 32, 224).astype(np.uint8)
+    a = np.stack([chk, chk // 2 + 10, 255 - chk], -1)
+    b = np.stack([255 - chk, chk, chk // 2 + 20], -1)
+    images = {"CAM1": a, "CAM2": b}
+    st = Stitcher(images)
+    st.calibrate_stitcher(images, save=False, homographies=[[[1, 0, 400], [0, 1, 0], [0, 0, 1]]])
+    got = st.stitch(images)
+    assert got.shape == (480, 1040, 3)
+    plan = st.plan(channels=3)
+    assert plan.stats()["blend"] == MODES["feather"] and plan.stats()["blend_tiles"] > 0
+    want = oracle.blend_stitch(plan.describe(), [a, b], MODES["feather"], interp)
+    assert _diff(got, want) == 0
+    # outside the overlap each camera alone; inside, every value between the two sources
+    assert np.array_equal(got[:, :400], a[:, :400]) and np.array_equal(got[:, 640:], b[:, 240:])
+    ov_a, ov_b, ov = a[:, 400:].astype(int), b[:, :240].astype(int), got[:, 400:640].astype(int)
+    assert ((ov >= np.minimum(ov_a, ov_b)) & (ov <= np.maximum(ov_a, ov_b))).all()
+    assert (ov != ov_a).any() and (ov != ov_b).any()

@@ -45,3 +45,97 @@ def test_stream_refuses_uncollected_slot():
         pipe.submit(cams)
     assert np.array_equal(pipe.wait(s), plan.stitch_host(cams))
     pipe.close()
+
+
+@pytest.fixture(scope="module")
+def rig4k():
+    """BASELINE configs[4]: 4 x 3840x2160 BGR rig, precomputed homographies (rig.py), and 4
+    distinct captures (the textures rolled by a different row count per capture)."""
+    from multicamera_stitching_amd import rig
+    from multicamera_stitching_amd.StitcherClass import _stage_desc
+    st, images, _ = rig.calibrated_stitcher(4, 3840, 2160, 3, seed=0)
+    cams0 = [images[label] for label in st.img_labels]
+    shots = [[np.roll(c, 37 * f + 5 * i, axis=0) for i, c in enumerate(cams0)] for f in range(4)]
+    stages = [dict(H=np.asarray(sb.cachedAH), canvas_w=sb.ABSize[0], canvas_h=sb.ABSize[1],
+                   bx=sb.Bpts[0][0], by=sb.Bpts[0][1], super_mode=sb.super_mode,
+                   x_limits=sb.x_limits, y_limits=sb.y_limits) for sb in st.stitchers]
+    return [_stage_desc(sb) for sb in st.stitchers], stages, shots
+
+
+@pytest.mark.parametrize("blend", [0, 2])
+def test_c5_4k_stream_vs_oracle(rig4k, blend):
+    """configs[4] at its stated size through the streaming pipeline (pinned staging, H2D / stitch
+    / D2H on three streams, one hipGraph per slot) at depths 2 and 3: every mosaic, in
+    submission order, equals the CPU restatement -- the reference's cascade (paste) or
+    orc_blend.c (3-level multi-band) -- not the library's own single-capture path."""
+    import os
+    from multicamera_stitching_amd import _capi
+    from oracle import oracle
+    descs, stages, shots = rig4k
+    oracle.set_threads(min(16, os.cpu_count() or 1))
+    plan = _capi.Plan(descs, 3840, 2160, 3, 1)
+    plan.set_blend(blend)
+    assert plan.out_w > 12000 and plan.out_h >= 2160
+    if blend == 0:
+        want = [oracle.cascade_stitch(stages, s) for s in shots]
+    else:
+        flat = plan.describe()
+        want = [oracle.blend_stitch(flat, s, oracle.BLEND_MULTIBAND) for s in shots]
+    for depth in (2, 3):
+        pipe = _capi.StreamPipeline(plan, depth=depth, use_graphs=True)
+        got, inflight = [], []
+        for f in range(len(shots) + depth):        # more captures than slots: slots are reused
+            if len(inflight) == depth:
+                got.append(pipe.wait(inflight.pop(0)))
+            inflight.append(pipe.submit(shots[f % len(shots)]))
+        while inflight:
+            got.append(pipe.wait(inflight.pop(0)))
+        pipe.close()
+        assert len(got) == len(shots) + depth
+        for f, g in enumerate(got):
+            w = want[f % len(shots)]
+            assert g.shape == w.shape
+            assert int(np.abs(g.astype(np.int16) - w.astype(np.int16)).max()) == 0, (depth, f)
+
+
+def test_stream_survives_recalibration():
+    """a pipeline built on Stitcher.plan() keeps working after the stitcher's plan
+    cache moves on (recalibration, other channel count): the cache drops its reference instead
+    of destroying a plan a live pipeline holds."""
+    from multicamera_stitching_amd import _capi, rig
+    st, images, _ = rig.calibrated_stitcher(3, 160, 96, 3, seed=21, rot_deg=2.0)
+    cams = [images[label] for label in st.img_labels]
+    plan = st.plan(channels=3)
+    want = plan.stitch_host(cams)
+    pipe = _capi.StreamPipeline(plan, depth=2)
+    del plan
+    st.plan(channels=1)                     # new key: the cache lets go of the 3-channel plan
+    st.calibrate_stitcher(images, save=False,
+                          homographies=[np.asarray(sb.cachedAH) for sb in st.stitchers])
+    st.stitch(images)                       # and builds another one
+    s = pipe.submit(cams)
+    assert np.array_equal(pipe.wait(s), want)
+    pipe.close()
+
+
+def test_stream_rejects_bad_frames():
+    """wrong camera count, frame size, channels or dtype, and a bad `out` buffer, are
+    refused before any byte is copied."""
+    from multicamera_stitching_amd import _capi, rig
+    from multicamera_stitching_amd.StitcherClass import _stage_desc
+    st, images, _ = rig.calibrated_stitcher(2, 64, 48, 3, seed=13)
+    cams = [images[label] for label in st.img_labels]
+    plan = _capi.Plan([_stage_desc(sb) for sb in st.stitchers], 64, 48, 3, 1)
+    pipe = _capi.StreamPipeline(plan, depth=1)
+    bad = [cams[:1], [cams[0], cams[1][:40]], [cams[0], cams[1][..., 0]],
+           [cams[0], cams[1].astype(np.float32)]]
+    for frames in bad:
+        with pytest.raises(ValueError):
+            pipe.submit(frames)
+    with pytest.raises(ValueError):
+        pipe.submit_concat(np.concatenate(cams, axis=1)[..., :2])
+    s = pipe.submit(cams)
+    with pytest.raises(ValueError):
+        pipe.wait(s, out=np.empty((3, 3), np.uint8))
+    assert np.array_equal(pipe.wait(s), plan.stitch_host(cams))
+    pipe.close()

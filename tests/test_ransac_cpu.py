@@ -52,3 +52,44 @@ def test_no_model():
     line = np.stack([np.arange(10), np.arange(10)], 1).astype(np.float32)
     H, _, best, scores = oracle.ransac_homography(line, line, 3.0, iters=50)
     assert H is None and (scores == -1).all()
+
+
+def _refine_case(seed, noise, outliers=0.25, perturb=2e-3):
+    src, dst, Ht, out = synthetic(n=500, outliers=outliers, noise=noise, seed=seed)
+    rng = np.random.default_rng(seed + 100)
+    H0 = Ht * (1 + rng.uniform(-perturb, perturb, (3, 3)))
+    H0 = H0 / H0[2, 2]
+    return src, dst, Ht, (~out).astype(np.uint8), H0
+
+
+def test_refine_product_equals_restatement():
+    """mcs_homography_refine_host (csrc/mcs_refine.cpp, host code of the product) is bit-exact
+    with the restatement orc_homography_refine, and both land on the true homography."""
+    from multicamera_stitching_amd import _capi
+    for seed, noise in ((0, 0.5), (1, 0.0), (2, 1.0), (3, 0.2)):
+        src, dst, Ht, mask, H0 = _refine_case(seed, noise)
+        got = _capi.homography_refine(src, dst, mask, H0)
+        want = oracle.homography_refine(src, dst, mask, H0)
+        assert np.array_equal(got, want), (seed, got - want)
+        assert max_reproj_diff(got, Ht) < (0.01 if noise == 0 else 0.5)
+        # the refinement is a least-squares fit: no worse than the starting model
+        assert max_reproj_diff(got, Ht) <= max_reproj_diff(H0, Ht)
+
+
+def test_refine_degenerate_inputs_keep_model():
+    """n <= 4 or no inliers: H unchanged (findHomography refines only for n > 4)."""
+    from multicamera_stitching_amd import _capi
+    src, dst, Ht, mask, H0 = _refine_case(4, 0.3)
+    for s, d, m in ((src[:4], dst[:4], mask[:4]), (src, dst, np.zeros_like(mask))):
+        assert np.array_equal(_capi.homography_refine(s, d, m, H0), H0)
+        assert np.array_equal(oracle.homography_refine(s, d, m, H0), H0)
+
+
+def test_ransac_model_is_refined():
+    """The RANSAC restatement's H is the refinement of its best hypothesis on its inliers."""
+    src, dst, Ht, out = synthetic(noise=0.8, seed=5)
+    H, mask, best, _ = oracle.ransac_homography(src, dst, 3.0)
+    assert max_reproj_diff(H, Ht) < 0.5
+    # refining again from the refined model moves it by far less than the noise
+    H2 = oracle.homography_refine(src, dst, mask, H)
+    assert max_reproj_diff(H2, H) < 0.05

@@ -63,7 +63,11 @@ def main(prefixes=("mcs_stream_c3",), workload=None, out=None):
     """Launches = the dispatches of the first family (one per stitch launch; the PMC runs use
     bench.py --no-paste-ref so only the measured plan dispatches); HBM bytes per launch = every
     family's FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE over its dispatches, / launches."""
-    res = {"kernels": list(prefixes), "workload": workload, "per_kernel": {}}
+    sys.path.insert(0, ROOT)
+    from multicamera_stitching_amd import _capi
+    # the kernels these counters belong to: bench.py reports "traffic" only for this build
+    res = {"kernels": list(prefixes), "workload": workload, "build_id": _capi.build_id(),
+           "per_kernel": {}}
     total = 0
     launches = None
     for pre in prefixes:
