@@ -211,6 +211,17 @@ int mcs_stitch_device(mcs_plan *plan, const uint8_t *const *d_cams,
                       const int64_t *cam_frame_stride, uint8_t *d_out, int64_t out_pitch,
                       int64_t out_frame_stride, int n_frames, void *stream);
 
+/* mcs_stitch_device without prepared tables: every output pixel maps through the exact FP64
+ * OpenCV map in the kernel itself (the direct-gather kernel over all tiles), so a plan is
+ * usable the moment mcs_plan_create returns (host flattening only, microseconds) -- the path for
+ * geometry that changes every capture (per-frame homographies, SURVEY.md 8 C3: estimate ->
+ * stitch).  Paste (MCS_BLEND_NONE) and MCS_BLEND_SEAM plans; the same pixels as
+ * mcs_stitch_device.  Replaces, per capture, StitcherBase.calibrate (:258-354) followed by
+ * StitcherBase.stitch (:211-256). */
+int mcs_stitch_direct(mcs_plan *plan, const uint8_t *const *d_cams,
+                      const int64_t *cam_frame_stride, uint8_t *d_out, int64_t out_pitch,
+                      int64_t out_frame_stride, int n_frames, void *stream);
+
 /* Source pixels each camera actually contributes to the mosaic (for the roofline's algorithmic
  * byte count): touched_px[i] for i < n_cams.  Runs a one-off marking kernel. */
 int mcs_plan_footprint(mcs_plan *plan, int64_t *touched_px, int n_cams);
@@ -272,6 +283,14 @@ int mcs_orb_detect_host(const uint8_t *image, int w, int h, int channels, int nf
                         int nlevels, float scale_factor, int fast_threshold, float *kp_xy,
                         float *kp_response, float *kp_angle, int *kp_level, uint8_t *desc,
                         int *n_out, int device);
+
+/* The same on a frame already in device memory (d_image, dense, on `device`; its producer must
+ * have finished -- the call runs on the calling thread's own stream): no upload, e.g. when the
+ * frame is also stitched (mcs_stitch_direct).  Same outputs, same result. */
+int mcs_orb_detect_device(const uint8_t *d_image, int w, int h, int channels, int nfeatures,
+                          int nlevels, float scale_factor, int fast_threshold, float *kp_xy,
+                          float *kp_response, float *kp_angle, int *kp_level, uint8_t *desc,
+                          int *n_out, int device);
 
 /* BFMatcher(NORM_L2) ("BruteForce").knnMatch(query, train, k=2) for float descriptors (the
  * reference's SIFT matcher, StitcherClass.py:423-424) on MFMA.  Descriptors that

@@ -45,6 +45,7 @@ EXPORTS = (
     "mcs_seam_graphcut_host", "mcs_plan_create_warp", "mcs_plan_create_undistort",
     "mcs_undistort_map_host", "mcs_match_l2_knn2", "mcs_match_l2_knn2_host",
     "mcs_stream_submit_strided", "mcs_build_id", "mcs_homography_refine_host", "mcs_stream_output",
+    "mcs_stitch_direct", "mcs_orb_detect_device",
 )
 
 
@@ -200,6 +201,8 @@ def load() -> ctypes.CDLL:
         L.mcs_orb_detect_host.argtypes = [P, I, I, I, I, I, ctypes.c_float, I, P, P, P, P, P,
                                           ctypes.POINTER(I), I]
         L.mcs_orb_detect_host.restype = I
+        L.mcs_orb_detect_device.argtypes = L.mcs_orb_detect_host.argtypes
+        L.mcs_orb_detect_device.restype = I
         L.mcs_plan_set_blend.argtypes = [P, I]
         L.mcs_plan_create_cylindrical.argtypes = [ctypes.POINTER(CylCamera), I, I, I,
                                                   ctypes.c_double, ctypes.c_double,
@@ -229,6 +232,8 @@ def load() -> ctypes.CDLL:
         L.mcs_stitch_device.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_int64), P,
                                         ctypes.c_int64, ctypes.c_int64, I, P]
         L.mcs_stitch_device.restype = I
+        L.mcs_stitch_direct.argtypes = L.mcs_stitch_device.argtypes
+        L.mcs_stitch_direct.restype = I
         L.mcs_plan_prepare.argtypes = [P, P]
         L.mcs_plan_prepare.restype = I
         L.mcs_plan_stats.argtypes = [P, ctypes.POINTER(ctypes.c_int64), I]
@@ -431,6 +436,18 @@ class Plan:
         ptrs = (ctypes.c_void_p * n)(*[int(p) for p in cam_ptrs])
         strides = (ctypes.c_int64 * n)(*[int(s) for s in cam_frame_strides])
         check(self._lib.mcs_stitch_device(self._h, ptrs, strides, ctypes.c_void_p(int(out_ptr)),
+                                          int(out_pitch), int(out_frame_stride), int(n_frames),
+                                          ctypes.c_void_p(int(stream))))
+
+    def stitch_direct(self, cam_ptrs, cam_frame_strides, out_ptr: int, out_pitch: int,
+                      out_frame_stride: int, n_frames: int, stream: int = 0):
+        """mcs_stitch_direct: the same pixels as stitch_device without prepared tables (the
+        exact map evaluated per pixel in the kernel) -- for a plan built for one capture, e.g.
+        from per-frame homographies.  Paste / seam plans."""
+        n = len(cam_ptrs)
+        ptrs = (ctypes.c_void_p * n)(*[int(p) for p in cam_ptrs])
+        strides = (ctypes.c_int64 * n)(*[int(s) for s in cam_frame_strides])
+        check(self._lib.mcs_stitch_direct(self._h, ptrs, strides, ctypes.c_void_p(int(out_ptr)),
                                           int(out_pitch), int(out_frame_stride), int(n_frames),
                                           ctypes.c_void_p(int(stream))))
 
@@ -668,6 +685,26 @@ def orb_detect(image, nfeatures: int = 2000, nlevels: int = 8, scale_factor: flo
                                 float(scale_factor), fast_threshold, xy.ctypes.data,
                                 resp.ctypes.data, ang.ctypes.data, lvl.ctypes.data,
                                 desc.ctypes.data, ctypes.byref(n), device))
+    k = n.value
+    return dict(xy=xy[:k], response=resp[:k], angle=ang[:k], level=lvl[:k], desc=desc[:k])
+
+
+def orb_detect_device(ptr: int, w: int, h: int, channels: int, nfeatures: int = 2000,
+                      nlevels: int = 8, scale_factor: float = 1.2, fast_threshold: int = 20,
+                      device: int = 0):
+    """mcs_orb_detect_device: ORB of a dense u8 frame already in device memory (e.g. a torch
+    tensor's data_ptr(), its producer finished).  Same dict as orb_detect."""
+    L = load()
+    xy = np.zeros((max(nfeatures, 1), 2), np.float32)
+    resp = np.zeros(max(nfeatures, 1), np.float32)
+    ang = np.zeros(max(nfeatures, 1), np.float32)
+    lvl = np.zeros(max(nfeatures, 1), np.int32)
+    desc = np.zeros((max(nfeatures, 1), 32), np.uint8)
+    n = ctypes.c_int(0)
+    check(L.mcs_orb_detect_device(ctypes.c_void_p(int(ptr)), w, h, channels, nfeatures, nlevels,
+                                  float(scale_factor), fast_threshold, xy.ctypes.data,
+                                  resp.ctypes.data, ang.ctypes.data, lvl.ctypes.data,
+                                  desc.ctypes.data, ctypes.byref(n), device))
     k = n.value
     return dict(xy=xy[:k], response=resp[:k], angle=ang[:k], level=lvl[:k], desc=desc[:k])
 

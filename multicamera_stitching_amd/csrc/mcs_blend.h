@@ -283,7 +283,6 @@ __device__ __forceinline__ void feather_tile(const KBlendArgs &a)
 //                       owner covers the pixel, which it always does).
 // Long launches run in chunks of captures so the scratch stays a few tens of MB.
 constexpr int kMbO1 = 6, kMbO2 = 2, kMbOR = 1;       // array origins: O/2 - 6, O/4 - 2, O/2 - 1
-constexpr int kMbFirst = 2;                           // level-0 origin: O - 16 + 2
 constexpr int kMbU = kMbUsedX * kMbUsedY;             // level-0 samples per owner
 #ifndef MCS_MB_FOOT_BYTES
 #define MCS_MB_FOOT_BYTES 28672
@@ -549,11 +548,17 @@ __device__ __forceinline__ void mb_prep(const KMbArgs &a)
     // the other ("mixed") pixels and the R1 entries they read.
     __shared__ int need_r1[kMbNRX * kMbNRY];
     __shared__ int n_px, n_r1;
+    // per owner slot: mosaic level-1 / level-2 columns the blend reads from it (band pass)
+    __shared__ int nq1lo[kBlendSlots], nq1hi[kBlendSlots], nz2lo[kBlendSlots], nz2hi[kBlendSlots];
     int32_t *t_cnt = t_d2 + kMbN2X * kMbN2Y;
     uint16_t *t_px = reinterpret_cast<uint16_t *>(t_cnt + kMbTabCounts);
     uint16_t *t_r1 = t_px + kMbTilePx;
     for (int e = tid; e < kMbNRX * kMbNRY; e += nt) need_r1[e] = 0;
     if (tid == 0) n_px = n_r1 = 0;
+    if (tid < kBlendSlots) {
+        nq1lo[tid] = nz2lo[tid] = 1 << 30;
+        nq1hi[tid] = nz2hi[tid] = -(1 << 30);
+    }
     __syncthreads();
     for (int i = tid; i < kMbTilePx; i += nt) {
         const int x = G.X0 + i % kBlendTileW, y = G.Y0 + i / kBlendTileW;
@@ -584,10 +589,38 @@ __device__ __forceinline__ void mb_prep(const KMbArgs &a)
             for (int v = 0; v < 3; v++)
                 need_r1[ix2<false>(iy[u], G.YR, kMbNRY) * kMbNRX + ix2<false>(ix[v], G.XR, kMbNRX)] =
                     1;
+        // R0 reads the owner's g1 at the pixel's level-1 taps
+        atomicMin(&nq1lo[s], min(ix[0], ix[1]));
+        atomicMax(&nq1hi[s], max(ix[1], ix[2]));
     }
     __syncthreads();
     for (int e = tid; e < kMbNRX * kMbNRY; e += nt)
         if (need_r1[e]) t_r1[atomicAdd(&n_r1, 1)] = (uint16_t)e;
+    // R1 at a listed entry reads owner j's g1 there and g2 at its level-2 taps where m1_j > 0,
+    // and B2 at those taps reads g2_j where m2_j > 0 (positions in the mosaic: reflected, as the
+    // blend kernel addresses them)
+    for (int e = tid; e < kMbNRX * kMbNRY; e += nt) {
+        if (!need_r1[e]) continue;
+        const int ey = e / kMbNRX, ex = e % kMbNRX;
+        const int p = (ey + kMbRS) * kMbN1X + ex + kMbRS;
+        const int qx = G.XR + ex, qy = G.YR + ey;
+        int zy[3], uy[3], zx[3], ux[3];
+        exp_taps<false>(qy, G.h2, zy, uy);
+        exp_taps<false>(qx, G.w2, zx, ux);
+        for (int j = 0; j < ns; j++) {
+            if (m1[j][p] > 0) {
+                atomicMin(&nq1lo[j], qx);
+                atomicMax(&nq1hi[j], qx);
+            }
+            for (int b = 0; b < 3; b++)
+                for (int c = 0; c < 3; c++)
+                    if (m2[j][ix2<false>(zy[b], G.Y2, kMbN2Y) * kMbN2X +
+                              ix2<false>(zx[c], G.X2, kMbN2X)] > 0) {
+                        atomicMin(&nz2lo[j], zx[c]);
+                        atomicMax(&nz2hi[j], zx[c]);
+                    }
+        }
+    }
     __syncthreads();
     // Column ranges of the level arrays the mixed pixels depend on (interior tiles; mosaic-border
     // tiles keep the full arrays): R1 entries -> their level-2 taps -> the level-1 entries the R1
@@ -625,6 +658,21 @@ __device__ __forceinline__ void mb_prep(const KMbArgs &a)
         t_cnt[0] = n_px;
         t_cnt[1] = n_r1;
         for (int q = 0; q < 6; q++) t_cnt[2 + q] = rng[q];
+        for (int j = 0; j < kBlendSlots; j++) {
+            int q1lo = nq1lo[j], q1hi = nq1hi[j], z2lo = nz2lo[j], z2hi = nz2hi[j];
+            if (n_px == 0 || j >= ns) {
+                q1lo = z2lo = 1 << 30;
+                q1hi = z2hi = -(1 << 30);
+            } else if (q1lo <= q1hi) {
+                // the level-2 taps of those g1 entries (L1 = 16384 g1 - E(g2))
+                z2lo = min(z2lo, (q1lo - 1) >> 1);
+                z2hi = max(z2hi, (q1hi >> 1) + 1);
+            }
+            t_cnt[kMbTabRanges + 4 * j + 0] = q1lo;
+            t_cnt[kMbTabRanges + 4 * j + 1] = q1hi;
+            t_cnt[kMbTabRanges + 4 * j + 2] = z2lo;
+            t_cnt[kMbTabRanges + 4 * j + 3] = z2hi;
+        }
     }
     __syncthreads();
     const int a0 = rng[0], w0 = rng[1] - rng[0] + 1, n_s = kMbUsedY * w0;
@@ -970,6 +1018,347 @@ __device__ __forceinline__ void mb_levels(const KMbArgs &a, MbLvLds<CN> &L)
             og1[e] = L.g1[(e / kMbNRX + kMbRS) * kMbN1X + e % kMbNRX + kMbRS];
         __syncthreads();   // the next capture overwrites level 0 and the pass arrays
     }
+}
+
+// ---- band pass: descriptors once per plan, then per chunk of captures ------------------------
+// Band descriptors: grid (bands), block 256.  Per (array row r, lane l) the global-memory window
+// descriptor (mb_desc) of the band's owner at mosaic (c0 + l, Y0 - 14 + r), positions reflected
+// into the mosaic as mb_prep does (BORDER_DEFAULT: a lane or row past a mosaic edge holds the
+// sample of its reflected position).
+template <int CN, int INTERP>
+__device__ __forceinline__ void mb_bdesc(const KMbBandArgs &a)
+{
+    const KParams &P = a.P;
+    const MbBand B = a.bands[blockIdx.x];
+    int cam, w, h;
+    slot_info(P, B.slot, cam, w, h);
+    const int y0 = B.row * kBlendTileH - kBlendHalo + kMbFirst;
+    uint64_t *o = a.bdesc + (int64_t)blockIdx.x * kMbBandDescRows * kMbBandLanes;
+    for (int i = threadIdx.x; i < kMbBandDescRows * kMbBandLanes; i += blockDim.x) {
+        const int r = i / kMbBandLanes, l = i % kMbBandLanes;
+        const int x = refl(B.c0 + l, P.out_w), y = refl(y0 + r, P.out_h);
+        const uint2 v = mb_desc<CN>(mb_src<INTERP>(P, B.slot, x, y), w, h);
+        o[i] = (uint64_t)v.x | ((uint64_t)v.y << 32);
+    }
+}
+
+// Value of lane l + 1 / l - 1 of the wave (DPP wave_shl:1 / wave_shr:1; the end lanes get 0).
+__device__ __forceinline__ uint32_t lane_next(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t lane_prev(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false);
+}
+// Value of lane `src` (byte address src * 4: ds_bpermute).
+__device__ __forceinline__ int lane_at(int v, int src4)
+{
+    return __builtin_amdgcn_ds_bpermute(src4, v);
+}
+
+// f(std::integral_constant<int, 0>()) .. f(std::integral_constant<int, N - 1>()), in order.
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for_(F &&f)
+{
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>());
+        static_for_<I + 1, N>(f);
+    }
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F &&f) { static_for_<0, N>(f); }
+
+// Scratch targets of one emitted entry: up to two listed tiles of the band's row whose arrays
+// hold the column (base = (list index * slots + local slot) * chunk, col = column in the tile's
+// array); base -1 = none.
+struct MbTarget {
+    int base[2], col[2];
+};
+static_assert(kBlendTileW == 32, "mb_bands: tile columns are found by shifts");
+
+__device__ __forceinline__ void mb_target(const KMbBandArgs &a, int s, int row, int tx, int col,
+                                          MbTarget &T, int k)
+{
+    T.base[k] = -1;
+    T.col[k] = 0;
+    if (tx < 0 || tx >= a.gxb) return;
+    const int bt = a.tile_bt[row * a.gxb + tx];
+    if (bt < 0) return;
+    const uint32_t mask = (uint32_t)a.list[2 + 2 * bt];
+    if (!((mask >> s) & 1u)) return;
+    const int j = __popc(mask & ((1u << s) - 1u));
+    T.base[k] = (bt * a.slots + j) * a.chunk;
+    T.col[k] = col;
+}
+
+// One band, FR captures: grid (bands, ceil(nf / FR)), block 64 (one wave).  Per level-0 row: the
+// lane's replicate-border sample (the owner's frame through L1/L2; descriptors three rows ahead,
+// windows two rows ahead), unpacked to 16-bit lanes and accumulated into the vertical 5-tap sums
+// of the level-1 rows it feeds (three rolling accumulators).  Per finished level-1 row: the
+// horizontal 5-tap over the neighbour lanes (DPP), giving level 1 at the even lanes; its
+// R1-region entries go to the scratch, and the row is accumulated per channel into the vertical
+// sums of level 2.  Per finished level-2 row: the horizontal 5-tap over lanes 2 and 4 apart
+// (ds_bpermute), level 2 at every fourth lane.  Only entries at real mosaic positions are stored
+// (the blend reads no others).  Integer sums, exact: the values of mb_levels' LDS passes.
+// Rows and columns of a unit past the top / left mosaic edge hold reflected level-0 samples, and
+// the reduces computed there are the reflected entries (reflect-101 about 0 commutes with the
+// 2x decimation).  At the bottom / right edges it does not (for even level sizes), so BR units
+// give level 2 the reflected level-1 rows (a history of four) and columns (source lanes).
+template <int CN, int FR, bool BR>
+__device__ __forceinline__ void mb_bands(const KMbBandArgs &a)
+{
+    typedef __attribute__((address_space(1))) const uint8_t gu8;
+    struct __attribute__((packed)) U2 {
+        uint32_t x, y;
+    };
+    typedef __attribute__((address_space(1))) const U2 gu2;
+    typedef __attribute__((address_space(1))) uint2 g2u;
+    typedef __attribute__((address_space(1))) int32_t gi32;
+    const KParams &P = a.P;
+    const int l = threadIdx.x;
+    const int bi = a.band0 + blockIdx.x;
+    const MbBand B = a.bands[bi];
+    const int fl0 = blockIdx.y * FR;
+    if (fl0 >= a.nf) return;
+    int cam, w, h;
+    slot_info(P, B.slot, cam, w, h);
+    const uint32_t pitch = (uint32_t)(w * CN);
+    const gu8 *fb[FR];
+#pragma unroll
+    for (int i = 0; i < FR; i++)
+        fb[i] = (const gu8 *)(P.cams[cam] +
+                              (int64_t)(a.f0 + min(fl0 + i, a.nf - 1)) * P.cam_fstride[cam]);
+    const int W = P.out_w, H = P.out_h;
+    const int w1 = (W + 1) / 2, h1 = (H + 1) / 2, w2 = (w1 + 1) / 2, h2 = (h1 + 1) / 2;
+    const int Y0 = B.row * kBlendTileH, Y1 = Y0 / 2 - kMbO1, Y2 = Y0 / 4 - kMbO2;
+    const int x = B.c0 + l;
+    // level-1 column x / 2 on even lanes 2..60, level-2 column x / 4 on lanes 8, 12, .., 56
+    // (complete there), stored when inside the mosaic
+    MbTarget T1, T2;
+    T1.base[0] = T1.base[1] = T2.base[0] = T2.base[1] = -1;
+    T1.col[0] = T1.col[1] = T2.col[0] = T2.col[1] = 0;
+    if ((l & 1) == 0 && l >= 2 && l <= 61 && x >= 0 && (x >> 1) < w1) {
+        // R1 region of tile tx: columns [16 tx - 1, 16 tx + 16]
+        const int qx = x >> 1, tx = (qx + kMbOR) >> 4;
+        mb_target(a, B.slot, B.row, tx, qx - (tx * (kBlendTileW / 2) - kMbOR), T1, 0);
+        if (((qx + kMbOR) & 15) < kMbNRX - 16)
+            mb_target(a, B.slot, B.row, tx - 1, qx - ((tx - 1) * (kBlendTileW / 2) - kMbOR), T1, 1);
+    }
+    if ((l & 3) == 0 && l >= 8 && l <= 56 && x >= 0 && (x >> 2) < w2) {
+        // level-2 array of tile tx: columns [8 tx - 2, 8 tx + 9]
+        const int z = x >> 2, tx = (z + kMbO2) >> 3;
+        mb_target(a, B.slot, B.row, tx, z - (tx * (kBlendTileW / 4) - kMbO2), T2, 0);
+        if (((z + kMbO2) & 7) < kMbN2X - 8)
+            mb_target(a, B.slot, B.row, tx - 1, z - ((tx - 1) * (kBlendTileW / 4) - kMbO2), T2, 1);
+    }
+    // level-2 horizontal sources: level-1 columns qx - 2 .. qx + 2 (lanes 2 apart), reflected
+    // at the right mosaic edge (BR)
+    int src[4];
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+        int q = (x >> 1) + (t < 2 ? t - 2 : t - 1);
+        if (BR && q >= w1) q = 2 * w1 - 2 - q;
+        src[t] = min(max(2 * q - B.c0, 0), kMbBandLanes - 1) * 4;
+    }
+    // scratch byte offsets (32-bit: the scratch is < 4 GiB) of this lane's targets, capture fl0,
+    // array row 0
+    uint32_t o1[2], o2[2];
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        o1[k] = T1.base[k] < 0 ? 0u : (uint32_t)((T1.base[k] + fl0) * (kMbNRX * kMbNRY) +
+                                                 T1.col[k]) * 8u;
+        o2[k] = T2.base[k] < 0 ? 0u : (uint32_t)((T2.base[k] + fl0) * (kMbN2X * kMbN2Y * CN) +
+                                                 T2.col[k]) * 4u;
+    }
+    typedef __attribute__((address_space(1))) uint8_t g8;
+    g8 *const g1b = (g8 *)a.g1, *const g2b = (g8 *)a.g2;
+    const uint64_t *dsc = a.bdesc + (int64_t)bi * kMbBandDescRows * kMbBandLanes + l;
+    const int nst = min(FR, a.nf - fl0);
+    const uint32_t M = 0x00ff00ffu;
+    // Rolling vertical sums, indexed by row % 3 (compile-time inside the 12-row body): level-1
+    // rows (packed u16: lo = channels 0, 2; hi = 1, 3), level-2 rows (one int per channel).  A
+    // row's sum starts with '=' at its first input row, so the rows before the array (and the
+    // padding rows after it) only ever feed rows that are not stored.
+    uint32_t Vl[FR][3], Vh[FR][3];
+    int V2[FR][3][CN];
+    uint32_t hl[FR][BR ? 4 : 1], hh[FR][BR ? 4 : 1];   // BR: the last four level-1 rows
+#pragma unroll
+    for (int i = 0; i < FR; i++)
+#pragma unroll
+        for (int q = 0; q < 3; q++) {
+            Vl[i][q] = Vh[i][q] = 0u;
+#pragma unroll
+            for (int k = 0; k < CN; k++) V2[i][q][k] = 0;
+            if (q < (BR ? 4 : 1)) hl[i][q] = hh[i][q] = 0u;
+        }
+    if (BR) {
+#pragma unroll
+        for (int i = 0; i < FR; i++) hl[i][BR ? 3 : 0] = hh[i][BR ? 3 : 0] = 0u;
+    }
+    auto load_win = [&](uint64_t dv, uint2 (&r0)[FR], uint2 (&r1)[FR]) {
+        const uint32_t dx = (uint32_t)dv, d = (uint32_t)(dv >> 44) & 7u;
+        const uint32_t o = (dx & 0x7fffffffu) - d, ob = o + ((dx >> 31) ? pitch : 0u);
+#pragma unroll
+        for (int i = 0; i < FR; i++) {
+            const U2 ra = *(const gu2 *)(fb[i] + o), rb = *(const gu2 *)(fb[i] + ob);
+            r0[i] = make_uint2(ra.x, ra.y);
+            r1[i] = make_uint2(rb.x, rb.y);
+        }
+    };
+    // Finished entries wait one row in registers before they are stored: gfx9 counts stores
+    // in vmcnt, so the wait for a row's window loads also waits for every store issued after
+    // those loads -- a store issued early in the next row has that row's work to complete.
+    int pend1 = -1, pend2 = -1;   // array row of the pending level-1 / level-2 entries (-1: none)
+    uint32_t p1l[FR], p1h[FR];
+    int p2[FR][CN];
+    auto flush = [&]() {
+        if (pend1 >= 0) {
+#pragma unroll
+            for (int f = 0; f < FR; f++) {
+                if (f >= nst) break;
+                const uint32_t ro =
+                    (uint32_t)(f * (kMbNRX * kMbNRY) + (pend1 - kMbRS) * kMbNRX) * 8u;
+#pragma unroll
+                for (int k = 0; k < 2; k++)
+                    if (T1.base[k] >= 0) *(g2u *)(g1b + (o1[k] + ro)) = make_uint2(p1l[f], p1h[f]);
+            }
+            pend1 = -1;
+        }
+        if (pend2 >= 0) {
+#pragma unroll
+            for (int f = 0; f < FR; f++) {
+                if (f >= nst) break;
+                const uint32_t ro = (uint32_t)(f * (kMbN2X * kMbN2Y * CN) + pend2 * kMbN2X) * 4u;
+#pragma unroll
+                for (int q = 0; q < 2; q++)
+                    if (T2.base[q] >= 0)
+#pragma unroll
+                        for (int k = 0; k < CN; k++)
+                            *(gi32 *)(g2b + (o2[q] + ro + k * (kMbN2X * kMbN2Y * 4))) = p2[f][k];
+            }
+            pend2 = -1;
+        }
+    };
+    // finished level-1 vertical sums (vl, vh) of array row i = 2m + P2 (m % 3 = M3), capture f
+    auto level1_done = [&](int i, auto P2c, auto M3c, int f, uint32_t vl, uint32_t vh) {
+        constexpr int P2 = decltype(P2c)::value, M3 = decltype(M3c)::value;
+        // horizontal: level-1 entry at lane x = 2 qx reads lanes x - 2 .. x + 2
+        const uint32_t l1 = lane_prev(vl), l2 = lane_prev(l1), r1 = lane_next(vl),
+                       r2 = lane_next(r1);
+        const uint32_t h1_ = lane_prev(vh), h2_ = lane_prev(h1_), s1 = lane_next(vh),
+                       s2 = lane_next(s1);
+        uint32_t gl = (l2 + r2) + 4u * (l1 + r1) + 6u * vl;
+        uint32_t gh = (h2_ + s2) + 4u * (h1_ + s1) + 6u * vh;
+        const int qy = Y1 + i;
+        if (qy >= 0 && qy < h1 && i >= kMbRS && i < kMbRS + kMbNRY) {
+            pend1 = i;   // (stored at the next row, see flush)
+            p1l[f] = gl;
+            p1h[f] = gh;
+        }
+        if (BR) {
+            // rows past the bottom edge feed level 2 as their reflections: h1 -> h1 - 2 (two
+            // rows back), h1 + 1 -> h1 - 3 (four back); deeper rows feed no stored entry
+            if (qy >= h1) {
+                const bool d0 = qy == h1;
+                gl = d0 ? hl[f][1] : hl[f][BR ? 3 : 0];
+                gh = d0 ? hh[f][1] : hh[f][BR ? 3 : 0];
+            }
+#pragma unroll
+            for (int q = (BR ? 3 : 0); q > 0; q--) hl[f][q] = hl[f][q - 1], hh[f][q] = hh[f][q - 1];
+            hl[f][0] = gl, hh[f][0] = gh;
+        }
+        int g[CN];
+#pragma unroll
+        for (int k = 0; k < CN; k++)
+            g[k] = (int)((((k & 1) ? gh : gl) >> ((k & 2) ? 16 : 0)) & 0xffffu);
+        // vertical: level-2 array row e reads level-1 rows 2e .. 2e + 4
+        if (P2 == 0) {
+#pragma unroll
+            for (int k = 0; k < CN; k++) V2[f][(M3 + 1) % 3][k] += g[k];   // row m - 2 done
+            const int e = (i >> 1) - 2, zy = Y2 + e;
+            if (e >= 0 && e < kMbN2Y && zy < h2) {
+                pend2 = e;
+#pragma unroll
+                for (int k = 0; k < CN; k++) {
+                    const int v = V2[f][(M3 + 1) % 3][k];
+                    p2[f][k] = (lane_at(v, src[0]) + lane_at(v, src[3])) +
+                               4 * (lane_at(v, src[1]) + lane_at(v, src[2])) + 6 * v;
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < CN; k++) {
+                V2[f][(M3 + 2) % 3][k] += 6 * g[k];
+                V2[f][M3][k] = g[k];
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < CN; k++) {
+                V2[f][(M3 + 2) % 3][k] += 4 * g[k];
+                V2[f][M3][k] += 4 * g[k];
+            }
+        }
+    };
+    // Pipeline over rows: at row r the windows of rows r + 1 and r + 2 and the descriptor of row
+    // r + 3 are in flight, three buffers each indexed by row % 3.  The 12-row body makes every
+    // buffer and accumulator index a compile-time constant, so no register copy ever reads an
+    // in-flight load (such a copy makes the compiler drain all loads at the loop's back edge).
+    uint64_t dq[3];
+    uint2 wq0[3][FR], wq1[3][FR];
+    dq[0] = dsc[0];
+    dq[1] = dsc[kMbBandLanes];
+    dq[2] = dsc[2 * kMbBandLanes];
+    load_win(dq[0], wq0[0], wq1[0]);
+    load_win(dq[1], wq0[1], wq1[1]);
+    for (int r12 = 0; r12 < kMbBandRows; r12 += 12) {
+        static_for<12>([&](auto PHc) {
+            constexpr int ph = decltype(PHc)::value;
+            const int r = r12 + ph;
+            constexpr int b0 = ph % 3, b2 = (ph + 2) % 3;
+            uint32_t wa, wb;
+            const uint32_t meta = (uint32_t)(dq[b0] >> 32), dd = (meta >> 12) & 7u;
+            mb_weights(meta, wa, wb);
+            uint32_t v[FR];
+#pragma unroll
+            for (int f = 0; f < FR; f++) {
+                v[f] = 0;
+#pragma unroll
+                for (int c = 0; c < CN; c++)
+                    v[f] |= mb_tap<CN>(wq0[b0][f], wq1[b0][f], wa, wb, c, dd) << (8 * c);
+            }
+            // the previous row's finished entries (after this row's window wait), then the loads:
+            // windows of row r + 2 (its descriptor arrived a row ago), descriptor of row r + 3
+            flush();
+            load_win(dq[b2], wq0[b2], wq1[b2]);
+            dq[b0] = dsc[(r + 3) * kMbBandLanes];
+            // level-0 row r = 2k + (ph & 1), k % 3 = K3; level-1 row k - 2 = 2m + P2, m % 3 = M3
+            constexpr int K3 = (ph / 2) % 3;
+            constexpr int q = ph / 2 - 2, P2 = q & 1, M3 = ((q - P2) / 2 + 3) % 3;
+            const int k = r >> 1;
+#pragma unroll
+            for (int f = 0; f < FR; f++) {
+                const uint32_t pl = v[f] & M, ph_ = (v[f] >> 8) & M;
+                // vertical: level-1 array row i reads level-0 rows 2i .. 2i + 4
+                if ((ph & 1) == 0) {
+                    Vl[f][(K3 + 1) % 3] += pl;   // row k - 2 done
+                    Vh[f][(K3 + 1) % 3] += ph_;
+                    level1_done(k - 2, std::integral_constant<int, P2>(),
+                                std::integral_constant<int, M3>(), f, Vl[f][(K3 + 1) % 3],
+                                Vh[f][(K3 + 1) % 3]);
+                    Vl[f][(K3 + 2) % 3] += 6u * pl;
+                    Vh[f][(K3 + 2) % 3] += 6u * ph_;
+                    Vl[f][K3] = pl;
+                    Vh[f][K3] = ph_;
+                } else {
+                    Vl[f][(K3 + 2) % 3] += 4u * pl;
+                    Vh[f][(K3 + 2) % 3] += 4u * ph_;
+                    Vl[f][K3] += 4u * pl;
+                    Vh[f][K3] += 4u * ph_;
+                }
+            }
+        });
+    }
+    flush();
 }
 
 // ---- blend: grid (listed tiles, nf), block kMbBlThreads ------------------------------------------

@@ -3,6 +3,7 @@
 // Replaces, for a calibrated chain, the per-frame work of Stitcher.stitch
 // (PostScripts/Stitcher/StitcherClass.py:114-136).  No exception crosses this boundary: every
 // entry point returns an MCS_* status and leaves a message in mcs_last_error().
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -50,6 +51,12 @@ struct mcs_plan {
     uint16_t *d_mbg1 = nullptr;
     int32_t *d_mbg2 = nullptr;
     int mb_chunk = 0;
+    // multi-band band pass: bands (the first n_bands_in reach no bottom / right mosaic edge),
+    // blend-tile grid -> list index, descriptors; without bands mb_levels computes the levels
+    int n_bands = 0, n_bands_in = 0, gxb = 0;
+    mcs::MbBand *d_bands = nullptr;
+    int *d_tile_bt = nullptr;
+    uint64_t *d_bdesc = nullptr;
     // cylindrical plans: per-column (sin, cos) and per-row h, host copy and device table
     bool cyl = false;
     std::vector<double> cyl_tab;
@@ -88,6 +95,8 @@ struct Kernels {
     hipFunction_t mb_prep[5][2] = {};     // [channels][interp]
     hipFunction_t mb_levels[5] = {};      // [channels]
     hipFunction_t mb_blend[5][2] = {};    // [channels][<= 2 owners : <= 4]
+    hipFunction_t mb_bands[5][2] = {};    // [channels][reaches the bottom / right edge]
+    hipFunction_t mb_bdesc[5][2] = {};    // [channels][interp]
 };
 Kernels g_k[kMaxDevices];
 std::mutex g_k_mu;
@@ -111,6 +120,10 @@ int kernels(const Api *A, int device, const Kernels **out)
             if (rc == MCS_OK) rc = fn(name, &k.resize[c]);
             snprintf(name, sizeof(name), "mcs_mb_levels_c%d", c);
             if (rc == MCS_OK) rc = fn(name, &k.mb_levels[c]);
+            snprintf(name, sizeof(name), "mcs_mb_bands_c%d", c);
+            if (rc == MCS_OK) rc = fn(name, &k.mb_bands[c][0]);
+            snprintf(name, sizeof(name), "mcs_mb_bands_br_c%d", c);
+            if (rc == MCS_OK) rc = fn(name, &k.mb_bands[c][1]);
             snprintf(name, sizeof(name), "mcs_mb_blend_c%d_s2", c);
             if (rc == MCS_OK) rc = fn(name, &k.mb_blend[c][0]);
             snprintf(name, sizeof(name), "mcs_mb_blend_c%d_s4", c);
@@ -122,6 +135,8 @@ int kernels(const Api *A, int device, const Kernels **out)
                 if (rc == MCS_OK) rc = fn(name, &k.feather[c][i]);
                 snprintf(name, sizeof(name), "mcs_mb_prep_c%d_i%d", c, i);
                 if (rc == MCS_OK) rc = fn(name, &k.mb_prep[c][i]);
+                snprintf(name, sizeof(name), "mcs_mb_bdesc_c%d_i%d", c, i);
+                if (rc == MCS_OK) rc = fn(name, &k.mb_bdesc[c][i]);
                 snprintf(name, sizeof(name), "mcs_seam_sample_c%d_i%d", c, i);
                 if (rc == MCS_OK) rc = fn(name, &k.seam_sample[c][i]);
                 for (int o = 0; o < 2 && rc == MCS_OK; o++) {
@@ -216,6 +231,154 @@ void mb_args(const mcs_plan *p, const mcs::KParams &P, mcs::KMbArgs &a)
     a.nf = 0;
 }
 
+void band_args(const mcs_plan *p, const mcs::KParams &P, mcs::KMbBandArgs &a)
+{
+    a.P = P;
+    a.list = p->d_blist;
+    a.tile_bt = p->d_tile_bt;
+    a.bands = p->d_bands;
+    a.bdesc = p->d_bdesc;
+    a.g1 = p->d_mbg1;
+    a.g2 = p->d_mbg2;
+    a.slots = p->mb_slots;
+    a.chunk = p->mb_chunk;
+    a.f0 = 0;
+    a.nf = 0;
+    a.gxb = p->gxb;
+    a.band0 = 0;
+}
+
+// The band pass of a multi-band plan (after mb_prep): per (owner slot, blend-tile row) the
+// level-1 / level-2 mosaic columns the tiles of that row read from that owner (mb_prep's per-slot
+// ranges), merged where they overlap and covered by 64-column windows kMbBandStride apart; then
+// the windows' sample descriptors (once).  Mosaics under 128 px a side (a unit would reach past
+// two opposite edges) and plans whose camera frames are too small for the 8-byte window loads
+// stay with mb_levels.
+int prepare_bands(const Api *A, mcs_plan *p, const Kernels *k, hipStream_t s)
+{
+    const int n = p->n_blend, S = p->mb_slots, C = p->fd.channels;
+    const int W = p->fd.out_w, H = p->fd.out_h;
+    p->gxb = (W + mcs::kBlendTileW - 1) / mcs::kBlendTileW;
+    const int gyb = (H + mcs::kBlendTileH - 1) / mcs::kBlendTileH;
+    const mcs::KParams &P = p->kp;
+    for (int c = 0; c <= P.n_stages; c++) {
+        const int64_t w = c == 0 ? P.cam0_w : P.st[c - 1].src_w;
+        const int64_t h = c == 0 ? P.cam0_h : P.st[c - 1].src_h;
+        if ((h - 1) * w * C < 16) return MCS_OK;   // (mb_levels' guarded window loads)
+    }
+    if (W < 128 || H < 128) return MCS_OK;
+    std::vector<int> list(1 + 2 * (size_t)n);
+    std::vector<int> cnt((size_t)n * mcs::kMbTabCounts);
+    const size_t words = (size_t)mcs::mb_tab_words(S);
+    const size_t cnt_at = (size_t)S * (mcs::kMbNRX * mcs::kMbNRY + mcs::kMbN2X * mcs::kMbN2Y) +
+                          mcs::kMbNRX * mcs::kMbNRY + mcs::kMbN2X * mcs::kMbN2Y;
+    HIP_TRY(A->hipMemcpyAsync(list.data(), p->d_blist, list.size() * sizeof(int),
+                              hipMemcpyDeviceToHost, s));
+    HIP_TRY(A->hipMemcpy2DAsync(cnt.data(), mcs::kMbTabCounts * sizeof(int), p->d_mbtab + cnt_at,
+                                words * sizeof(int), mcs::kMbTabCounts * sizeof(int), (size_t)n,
+                                hipMemcpyDeviceToHost, s));
+    HIP_TRY(A->hipStreamSynchronize(s));
+    // per (plan slot, tile row): the level-1 / level-2 column intervals of its tiles
+    struct Need { int q1lo, q1hi, z2lo, z2hi; };
+    constexpr int kSlots = 32;   // plan slots: bits of a tile's owner mask
+    std::vector<std::vector<Need>> need((size_t)kSlots * gyb);
+    std::vector<int> tile_bt((size_t)p->gxb * gyb, -1);
+    for (int i = 0; i < n; i++) {
+        const int t = list[1 + 2 * i];
+        const uint32_t mask = (uint32_t)list[2 + 2 * i];
+        tile_bt[t] = i;
+        const int Y0 = (t / p->gxb) * mcs::kBlendTileH;
+        const int *c = cnt.data() + (size_t)i * mcs::kMbTabCounts + mcs::kMbTabRanges;
+        uint32_t m = mask;
+        for (int j = 0; m; j++, m &= m - 1) {
+            const int slot = __builtin_ctz(m);
+            Need q{c[4 * j], c[4 * j + 1], c[4 * j + 2], c[4 * j + 3]};
+            if (getenv("MCS_DEBUG_BANDS"))
+                fprintf(stderr, "tile %d slot %d q1 [%d, %d] z2 [%d, %d]\n", t, slot, q.q1lo,
+                        q.q1hi, q.z2lo, q.z2hi);
+            if (q.q1lo > q.q1hi && q.z2lo > q.z2hi) continue;
+            need[(size_t)slot * gyb + Y0 / mcs::kBlendTileH].push_back(q);
+        }
+    }
+    std::vector<mcs::MbBand> bands;
+    const int big = 1 << 30;
+    for (int slot = 0; slot < kSlots; slot++)
+        for (int row = 0; row < gyb; row++) {
+            std::vector<Need> &v = need[(size_t)slot * gyb + row];
+            if (v.empty()) continue;
+            // (a column interval in level-0 terms: its lowest needed level-0 column)
+            auto lo0 = [&](const Need &q) {
+                return std::min(q.z2lo <= q.z2hi ? 4 * q.z2lo : big,
+                                q.q1lo <= q.q1hi ? 2 * q.q1lo : big);
+            };
+            std::sort(v.begin(), v.end(), [&](const Need &a, const Need &b) {
+                return lo0(a) < lo0(b);
+            });
+            size_t i = 0;
+            while (i < v.size()) {
+                Need u = v[i++];
+                auto hi0 = [&](const Need &q) {
+                    return std::max(q.z2lo <= q.z2hi ? 4 * q.z2hi : -big,
+                                    q.q1lo <= q.q1hi ? 2 * q.q1hi : -big);
+                };
+                // merge intervals that overlap or nearly touch (one window covers the gap)
+                while (i < v.size() && lo0(v[i]) <= hi0(u) + 2 * mcs::kMbBandStride) {
+                    const Need &q = v[i++];
+                    if (q.q1lo <= q.q1hi)
+                        u.q1lo = std::min(u.q1lo, q.q1lo), u.q1hi = std::max(u.q1hi, q.q1hi);
+                    if (q.z2lo <= q.z2hi)
+                        u.z2lo = std::min(u.z2lo, q.z2lo), u.z2hi = std::max(u.z2hi, q.z2hi);
+                }
+                // windows: c0 emits level-1 columns [c0/2 + 1, c0/2 + 30] and level-2 columns
+                // [c0/4 + 2, c0/4 + 14] (mb_bands' complete lanes)
+                int c0 = std::min(u.z2lo <= u.z2hi ? 4 * (u.z2lo - 2) : big,
+                                  u.q1lo <= u.q1hi ? 2 * (u.q1lo - 1) : big);
+                c0 = c0 >= 0 ? c0 & ~3 : -((-c0 + 3) & ~3);
+                for (;;) {
+                    bands.push_back(mcs::MbBand{slot, row, c0, 0});
+                    const bool z_ok = u.z2lo > u.z2hi || c0 / 4 + 14 >= u.z2hi;
+                    const bool q_ok = u.q1lo > u.q1hi || c0 / 2 + 30 >= u.q1hi;
+                    if (z_ok && q_ok) break;
+                    c0 += mcs::kMbBandStride;
+                }
+            }
+        }
+    if (getenv("MCS_DEBUG_BANDS"))
+        for (const mcs::MbBand &b : bands)
+            fprintf(stderr, "band slot %d row %d c0 %d\n", b.slot, b.row, b.c0);
+    if (bands.empty()) return MCS_OK;
+    // bands whose rows or columns reach past the bottom / right mosaic edge: the _br kernel
+    auto br = [&](const mcs::MbBand &b) {
+        return b.row * mcs::kBlendTileH - mcs::kBlendHalo + mcs::kMbFirst + mcs::kMbUsedY > H ||
+               b.c0 + mcs::kMbBandLanes > W;
+    };
+    std::stable_partition(bands.begin(), bands.end(), [&](const mcs::MbBand &b) { return !br(b); });
+    p->n_bands_in = (int)(std::find_if(bands.begin(), bands.end(), br) - bands.begin());
+    const size_t nb = bands.size();
+    HIP_TRY(A->hipMalloc((void **)&p->d_bands, nb * sizeof(mcs::MbBand)));
+    HIP_TRY(A->hipMalloc((void **)&p->d_tile_bt, tile_bt.size() * sizeof(int)));
+    HIP_TRY(A->hipMalloc((void **)&p->d_bdesc,
+                         nb * mcs::kMbBandDescRows * mcs::kMbBandLanes * sizeof(uint64_t)));
+    HIP_TRY(A->hipMemcpyAsync(p->d_bands, bands.data(), nb * sizeof(mcs::MbBand),
+                              hipMemcpyHostToDevice, s));
+    HIP_TRY(A->hipMemcpyAsync(p->d_tile_bt, tile_bt.data(), tile_bt.size() * sizeof(int),
+                              hipMemcpyHostToDevice, s));
+    p->n_bands = (int)nb;
+    mcs::KMbBandArgs a;
+    band_args(p, p->kp, a);
+    int rc = launch_args(A, k->mb_bdesc[C][p->fd.interp], (unsigned)nb, 1, 256, 1, &a, sizeof(a),
+                         s);
+    if (rc) return rc;
+    // the band pass writes only the entries the blend reads: the rest of the scratch holds
+    // zeros (or an earlier capture's value of the same entry), never stale garbage
+    HIP_TRY(A->hipMemsetAsync(p->d_mbg1, 0,
+                              (size_t)n * S * p->mb_chunk * mcs::kMbNRX * mcs::kMbNRY * 8, s));
+    HIP_TRY(A->hipMemsetAsync(p->d_mbg2, 0,
+                              (size_t)n * S * p->mb_chunk * mcs::kMbN2X * mcs::kMbN2Y * C * 4, s));
+    HIP_TRY(A->hipStreamSynchronize(s));
+    return MCS_OK;
+}
+
 // Multi-band: per (tile, owner) level-0 sample windows and per-tile masks (once), and the level
 // scratch for chunks of mb_chunk captures (budget kMbScratchBytes).
 int prepare_multiband(const Api *A, mcs_plan *p, const Kernels *k, hipStream_t s)
@@ -243,8 +406,11 @@ int prepare_multiband(const Api *A, mcs_plan *p, const Kernels *k, hipStream_t s
     p->mb_chunk = chunk;
     mcs::KMbArgs a;
     mb_args(p, p->kp, a);
-    return launch_args(A, k->mb_prep[C][p->fd.interp], (unsigned)n, 1, mcs::kMbPrepThreads, 1,
-                       &a, sizeof(a), s);
+    const int rc = launch_args(A, k->mb_prep[C][p->fd.interp], (unsigned)n, 1,
+                               mcs::kMbPrepThreads, 1, &a, sizeof(a), s);
+    if (rc) return rc;
+    static const bool bands_on = !getenv("MCS_MB_BANDS") || strcmp(getenv("MCS_MB_BANDS"), "0");
+    return bands_on ? prepare_bands(A, p, k, s) : MCS_OK;
 }
 
 // Blended modes: the owner map and the list of 32-px tiles the blend kernels recompute.
@@ -294,8 +460,13 @@ void release_tables(const Api *A, mcs_plan *p)
     for (void *q : {(void *)p->d_tiles, (void *)p->d_desc, (void *)p->d_fallback,
                     (void *)p->d_owner, (void *)p->d_binfo, (void *)p->d_blist,
                     (void *)p->d_mbdesc, (void *)p->d_mbtab, (void *)p->d_mbfoot, (void *)p->d_mbg1,
-                    (void *)p->d_mbg2})
+                    (void *)p->d_mbg2, (void *)p->d_bands, (void *)p->d_tile_bt,
+                    (void *)p->d_bdesc})
         if (q) (void)A->hipFree(q);
+    p->d_bands = nullptr;
+    p->d_tile_bt = nullptr;
+    p->d_bdesc = nullptr;
+    p->n_bands = p->n_bands_in = p->gxb = 0;
     p->d_mbdesc = nullptr;
     p->d_mbtab = nullptr;
     p->d_mbfoot = nullptr;
@@ -377,11 +548,29 @@ int prepare(const Api *A, mcs_plan *p, hipStream_t s)
 // One launch pair (stream over all tiles + direct over the fallback tiles) for n_frames captures
 // that share one frame stride.
 // Multi-band level pyramids of captures [f0, f0 + nf) on stream s.
+// (the band pass when the plan has one, else mb_levels)
 int launch_mb_levels(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KMbArgs &m, int f0,
                      int nf, hipStream_t s)
 {
     m.f0 = f0;
     m.nf = nf;
+    if (p->n_bands > 0) {
+        mcs::KMbBandArgs b;
+        band_args(p, m.P, b);
+        b.f0 = f0;
+        b.nf = nf;
+        const unsigned gy = (unsigned)((nf + mcs::kMbBandFrames - 1) / mcs::kMbBandFrames);
+        int rc = MCS_OK;
+        if (p->n_bands_in > 0)
+            rc = launch_args(A, k->mb_bands[p->fd.channels][0], (unsigned)p->n_bands_in, gy,
+                             mcs::kMbBandLanes, 1, &b, sizeof(b), s);
+        b.band0 = p->n_bands_in;
+        if (rc == MCS_OK && p->n_bands > p->n_bands_in)
+            rc = launch_args(A, k->mb_bands[p->fd.channels][1],
+                             (unsigned)(p->n_bands - p->n_bands_in), gy, mcs::kMbBandLanes, 1, &b,
+                             sizeof(b), s);
+        return rc;
+    }
     const unsigned gz = (unsigned)((nf + mcs::kMbLvFrames - 1) / mcs::kMbLvFrames);
     size_t sz = sizeof(m);
     void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, (void *)&m, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz,
@@ -943,9 +1132,10 @@ int mcs_resize_linear_device(const uint8_t *d_src, int src_w, int src_h, int64_t
                          dfs, channels, n_frames, (hipStream_t)stream);
 }
 
-int mcs_stitch_device(mcs_plan *p, const uint8_t *const *d_cams, const int64_t *cam_frame_stride,
-                      uint8_t *d_out, int64_t out_pitch, int64_t out_frame_stride, int n_frames,
-                      void *stream)
+// Kernel parameters of a device-resident batch (mcs_stitch_device / mcs_stitch_direct).
+static int device_kparams(const mcs_plan *p, const uint8_t *const *d_cams,
+                          const int64_t *cam_frame_stride, uint8_t *d_out, int64_t out_pitch,
+                          int64_t out_frame_stride, int n_frames, mcs::KParams *kp)
 {
     if (!p || !d_cams || !d_out) return mcs::fail(MCS_E_INVALID, "NULL plan/d_cams/d_out");
     if (n_frames < 0 || n_frames > 65535) return mcs::fail(MCS_E_INVALID, "n_frames=%d", n_frames);
@@ -953,24 +1143,91 @@ int mcs_stitch_device(mcs_plan *p, const uint8_t *const *d_cams, const int64_t *
     if (out_pitch < (int64_t)p->fd.out_w * C)
         return mcs::fail(MCS_E_INVALID, "out_pitch %lld < row bytes %lld", (long long)out_pitch,
                          (long long)p->fd.out_w * C);
-    const Api *A = mcs::rt::api();
-    if (!A) return MCS_E_HIP;
-    mcs::KParams kp = p->kp;
+    *kp = p->kp;
     bool need[MCS_MAX_CAMS];
     need_mask(p->fd, need);
     for (int i = 0; i < p->fd.n_cams; i++) {
         if (need[i] && !d_cams[i]) return mcs::fail(MCS_E_INVALID, "d_cams[%d] NULL", i);
-        kp.cams[i] = d_cams[i];
-        kp.cam_fstride[i] = cam_frame_stride ? cam_frame_stride[i]
-                                             : (int64_t)p->fd.cam_w[i] * p->fd.cam_h[i] * C;
+        kp->cams[i] = d_cams[i];
+        kp->cam_fstride[i] = cam_frame_stride ? cam_frame_stride[i]
+                                              : (int64_t)p->fd.cam_w[i] * p->fd.cam_h[i] * C;
     }
-    kp.out = d_out;
-    kp.out_pitch = out_pitch;
-    kp.out_fstride = out_frame_stride ? out_frame_stride : out_pitch * p->fd.out_h;
+    kp->out = d_out;
+    kp->out_pitch = out_pitch;
+    kp->out_fstride = out_frame_stride ? out_frame_stride : out_pitch * p->fd.out_h;
+    return MCS_OK;
+}
+
+int mcs_stitch_device(mcs_plan *p, const uint8_t *const *d_cams, const int64_t *cam_frame_stride,
+                      uint8_t *d_out, int64_t out_pitch, int64_t out_frame_stride, int n_frames,
+                      void *stream)
+{
+    mcs::KParams kp;
+    int rc = device_kparams(p, d_cams, cam_frame_stride, d_out, out_pitch, out_frame_stride,
+                            n_frames, &kp);
+    if (rc) return rc;
+    const Api *A = mcs::rt::api();
+    if (!A) return MCS_E_HIP;
     DeviceGuard g(A, p->device);
     if (g.err != hipSuccess)
         return mcs::fail(MCS_E_HIP, "hipSetDevice(%d): %s", p->device, A->hipGetErrorString(g.err));
     return launch_stitch(A, p, kp, n_frames, (hipStream_t)stream);
+}
+
+int mcs_stitch_direct(mcs_plan *p, const uint8_t *const *d_cams, const int64_t *cam_frame_stride,
+                      uint8_t *d_out, int64_t out_pitch, int64_t out_frame_stride, int n_frames,
+                      void *stream)
+{
+    mcs::KParams kp;
+    int rc = device_kparams(p, d_cams, cam_frame_stride, d_out, out_pitch, out_frame_stride,
+                            n_frames, &kp);
+    if (rc) return rc;
+    if (p->blend != MCS_BLEND_NONE && p->blend != MCS_BLEND_SEAM)
+        return mcs::fail(MCS_E_UNSUPPORTED, "mcs_stitch_direct renders paste / seam plans; "
+                         "blended plans need their prepared tables (mcs_stitch_device)");
+    if (kp.out_w <= 0 || kp.out_h <= 0 || n_frames == 0) return MCS_OK;
+    const Api *A = mcs::rt::api();
+    if (!A) return MCS_E_HIP;
+    DeviceGuard g(A, p->device);
+    if (g.err != hipSuccess)
+        return mcs::fail(MCS_E_HIP, "hipSetDevice(%d): %s", p->device, A->hipGetErrorString(g.err));
+    const Kernels *k = nullptr;
+    rc = kernels(A, p->device, &k);
+    if (rc) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    rc = ensure_cyl(A, p, s);   // (cylinder / table plans: their device tables, once)
+    if (rc) return rc;
+    kp.cyl_tab = p->kp.cyl_tab;
+    kp.map_tab = p->kp.map_tab;
+    kp.seam_hint = p->kp.seam_hint;
+    const int gx = (p->fd.out_w + mcs::kTileW - 1) / mcs::kTileW;
+    const int gy = (p->fd.out_h + mcs::kTileH - 1) / mcs::kTileH;
+    // one frame stride for every camera per launch (the kernel's walk), else frame by frame
+    bool uniform = true;
+    for (int j = 0; j < p->fd.n_stages; j++)
+        uniform = uniform && kp.cam_fstride[p->fd.st[j].cam] == kp.cam_fstride[0];
+    const int runs = uniform ? 1 : n_frames;
+    for (int f = 0; f < runs; f++) {
+        mcs::KDirectArgs args;
+        args.P = kp;
+        if (!uniform) {
+            for (int i = 0; i < p->fd.n_cams; i++)
+                args.P.cams[i] = kp.cams[i] ? kp.cams[i] + (int64_t)f * kp.cam_fstride[i] : nullptr;
+            args.P.out = kp.out + (int64_t)f * kp.out_fstride;
+        }
+        const bool off32 = offset_base(p, args.P, &args.P.base);
+        args.fallback = nullptr;   // every tile
+        args.n_frames = uniform ? n_frames : 1;
+        args.pad_ = 0;
+        const unsigned fy = (unsigned)((args.n_frames + mcs::kDirectFrames - 1) / mcs::kDirectFrames);
+        size_t sz = sizeof(args);
+        void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, (void *)&args, HIP_LAUNCH_PARAM_BUFFER_SIZE,
+                       &sz, HIP_LAUNCH_PARAM_END};
+        HIP_TRY(A->hipModuleLaunchKernel(k->direct[p->fd.channels][p->fd.interp][off32 ? 1 : 0],
+                                         (unsigned)(gx * gy), fy, 1, mcs::kWave,
+                                         mcs::kWavesPerBlock, 1, 0, s, nullptr, cfg));
+    }
+    return MCS_OK;
 }
 
 int mcs_plan_prepare(mcs_plan *p, void *stream)

@@ -423,10 +423,13 @@ int mcs_ransac_homography_host(const float *src_xy, const float *dst_xy, int n, 
     return MCS_OK;
 }
 
-int mcs_orb_detect_host(const uint8_t *image, int w, int h, int channels, int nfeatures,
-                        int nlevels, float scale_factor, int fast_threshold, float *kp_xy,
-                        float *kp_response, float *kp_angle, int *kp_level, uint8_t *desc,
-                        int *n_out, int device)
+namespace {
+// ORB of one image (host memory, or device memory when on_device); mcs_orb_detect_host /
+// mcs_orb_detect_device below.
+int orb_detect(const uint8_t *image, bool on_device, int w, int h, int channels, int nfeatures,
+               int nlevels, float scale_factor, int fast_threshold, float *kp_xy,
+               float *kp_response, float *kp_angle, int *kp_level, uint8_t *desc, int *n_out,
+               int device)
 {
     mcs::clear_error();
     if (!image || !kp_xy || !desc || !n_out) return mcs::fail(MCS_E_INVALID, "NULL buffer");
@@ -508,18 +511,21 @@ int mcs_orb_detect_host(const uint8_t *image, int w, int h, int channels, int nf
     std::vector<int> kp;
     std::vector<double> orient, resp;
     uint8_t *lvl0 = buf + o_lvl;
-    hipError_t e = A->hipMemcpyAsync(buf + o_in, image, in_bytes, hipMemcpyHostToDevice, s);
+    // the frame: uploaded into the workspace, or read where it lies on the device
+    const uint8_t *in = on_device ? image : buf + o_in;
+    hipError_t e = on_device ? hipSuccess
+                             : A->hipMemcpyAsync(buf + o_in, image, in_bytes, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = A->hipMemsetAsync(buf + o_cnt, 0, mcs::kOrbMaxLevels * sizeof(int), s);
     if (e == hipSuccess) {
         if (channels == 3) {
             mcs::KGrayArgs ga;
-            ga.bgr = buf + o_in;
+            ga.bgr = in;
             ga.gray = lvl0;
             ga.n = w * h;
             ga.pad_ = 0;
             rc = launch(A, k->orb_gray, (w * h + 255) / 256, 1, 256, &ga, sizeof(ga), s);
         } else {
-            e = A->hipMemcpyAsync(lvl0, buf + o_in, in_bytes, hipMemcpyDeviceToDevice, s);
+            e = A->hipMemcpyAsync(lvl0, in, in_bytes, hipMemcpyDeviceToDevice, s);
         }
     }
     for (int l = 1; l < nlevels && e == hipSuccess && rc == MCS_OK; l++)
@@ -669,6 +675,25 @@ int mcs_orb_detect_host(const uint8_t *image, int w, int h, int channels, int nf
     }
     *n_out = n;
     return MCS_OK;
+}
+}  // namespace
+
+int mcs_orb_detect_host(const uint8_t *image, int w, int h, int channels, int nfeatures,
+                        int nlevels, float scale_factor, int fast_threshold, float *kp_xy,
+                        float *kp_response, float *kp_angle, int *kp_level, uint8_t *desc,
+                        int *n_out, int device)
+{
+    return orb_detect(image, false, w, h, channels, nfeatures, nlevels, scale_factor,
+                      fast_threshold, kp_xy, kp_response, kp_angle, kp_level, desc, n_out, device);
+}
+
+int mcs_orb_detect_device(const uint8_t *d_image, int w, int h, int channels, int nfeatures,
+                          int nlevels, float scale_factor, int fast_threshold, float *kp_xy,
+                          float *kp_response, float *kp_angle, int *kp_level, uint8_t *desc,
+                          int *n_out, int device)
+{
+    return orb_detect(d_image, true, w, h, channels, nfeatures, nlevels, scale_factor,
+                      fast_threshold, kp_xy, kp_response, kp_angle, kp_level, desc, n_out, device);
 }
 
 }  // extern "C"

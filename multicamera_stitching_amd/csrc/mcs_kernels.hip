@@ -776,7 +776,7 @@ __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *til
 template <int CN, int INTERP, bool OFF32>
 __device__ __forceinline__ void direct_tile(const KParams &P, const int *fallback, int n_frames)
 {
-    const int tile = fallback[1 + blockIdx.x];
+    const int tile = fallback ? fallback[1 + blockIdx.x] : (int)blockIdx.x;   // NULL: every tile
     const int f0 = blockIdx.y * kDirectFrames;
     const int gx = (P.out_w + kTileW - 1) / kTileW;
     const int tx = tile % gx, ty = tile / gx;
@@ -965,6 +965,11 @@ extern "C" __global__ __launch_bounds__(256) void mcs_blend_classify(const mcs::
         const mcs::KMbArgs a)                                                                  \
     {                                                                                          \
         mcs::mb_prep<CN, IN>(a);                                                               \
+    }                                                                                          \
+    extern "C" __global__ __launch_bounds__(256) void mcs_mb_bdesc_c##CN##_i##IN(              \
+        const mcs::KMbBandArgs a)                                                              \
+    {                                                                                          \
+        mcs::mb_bdesc<CN, IN>(a);                                                              \
     }
 #ifndef MCS_MB_WAVES
 #define MCS_MB_WAVES 4
@@ -975,6 +980,16 @@ extern "C" __global__ __launch_bounds__(256) void mcs_blend_classify(const mcs::
     {                                                                                          \
         __shared__ mcs::MbLvLds<CN> lds;                                                       \
         mcs::mb_levels<CN>(a, lds);                                                            \
+    }                                                                                          \
+    extern "C" __global__ __launch_bounds__(64) void mcs_mb_bands_c##CN(                       \
+        const mcs::KMbBandArgs a)                                                              \
+    {                                                                                          \
+        mcs::mb_bands<CN, mcs::kMbBandFrames, false>(a);                                       \
+    }                                                                                          \
+    extern "C" __global__ __launch_bounds__(64) void mcs_mb_bands_br_c##CN(                    \
+        const mcs::KMbBandArgs a)                                                              \
+    {                                                                                          \
+        mcs::mb_bands<CN, mcs::kMbBandFrames, true>(a);                                        \
     }                                                                                          \
     extern "C" __global__ __launch_bounds__(256) void mcs_mb_blend_c##CN##_s2(                \
         const mcs::KMbArgs a)                                                                  \

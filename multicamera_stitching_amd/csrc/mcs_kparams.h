@@ -158,15 +158,19 @@ constexpr int64_t kMbScratchBytes = 1ll << 30;    // level scratch budget per pl
 // (T + 25), level 1 [O/2 - 6, O/2 + T/2 + 4] (T/2 + 11), level 2 [O/4 - 2, O/4 + T/4 + 1]
 // (T/4 + 4), the collapsed level 1 ("R1 region") [O/2 - 1, O/2 + T/2] (T/2 + 2).
 constexpr int kMbUsedX = kBlendTileW + 25, kMbUsedY = kBlendTileH + 25;
+constexpr int kMbFirst = 2;        // level-0 array origin: O - kBlendHalo + kMbFirst
 constexpr int kMbN1X = kBlendTileW / 2 + 11, kMbN1Y = kBlendTileH / 2 + 11;
 constexpr int kMbN2X = kBlendTileW / 4 + 4, kMbN2Y = kBlendTileH / 4 + 4;
 constexpr int kMbNRX = kBlendTileW / 2 + 2, kMbNRY = kBlendTileH / 2 + 2;
 constexpr int kMbTilePx = kBlendTileW * kBlendTileH;
 // per-tile table (int32 words): m1 (R1 region) [slots], m2 [slots], d1 (R1 region), d2, then
 // the work lists: n_px, n_r1, the level-0 / level-1 / level-2 column ranges (first, last) the
-// mixed pixels depend on, the tile pixels to blend (u16, one per tile pixel) and the R1 entries
+// mixed pixels depend on, per owner slot the level-1 and level-2 mosaic columns (first, last,
+// first, last) of the entries the blend reads from that owner (the band pass computes only
+// these), the tile pixels to blend (u16, one per tile pixel) and the R1 entries
 // they read (u16, one per R1 entry)
-constexpr int kMbTabCounts = 8;
+constexpr int kMbTabRanges = 8;
+constexpr int kMbTabCounts = kMbTabRanges + 4 * kBlendSlots;
 constexpr int kMbTabLists = kMbTabCounts + kMbTilePx / 2 + (kMbNRX * kMbNRY + 1) / 2;
 constexpr int mb_tab_words(int slots)
 {
@@ -193,6 +197,41 @@ struct KMbArgs {
     int slots;                     // owners per tile (the tables' slot dimension)
     int chunk;                     // scratch capture stride
     int f0, nf;                    // captures [f0, f0 + nf) of this launch
+};
+
+// Band pass of the multi-band levels (mcs_mb_bands_c*): one wave per (band, kMbBandFrames
+// captures).  A band is one owner slot's pyramid over a 64-column window of the mosaic and the
+// level-0 rows of one blend-tile row (its 89-row array): lane = level-0 column, rows walked top
+// to bottom with the 5-tap reduces rolling in registers (no LDS, no barriers); the finished level-1
+// / level-2 entries go to the per-(tile, owner) scratch of every listed blend tile of that row
+// whose arrays contain them.  Windows start at multiples of 4 columns, so even lanes hold
+// level-1 columns and every fourth lane a level-2 column.  Bands reaching past the bottom or
+// right mosaic edge run the _br variant (reflected level-1 inputs of level 2).
+struct MbBand {
+    int slot, row, c0, pad_;
+};
+constexpr int kMbBandLanes = 64;
+// rows walked per band: the 89-row level-0 array padded to the 12-row unrolled body (the extra
+// rows feed no stored entry), and descriptor rows for the 3-row lookahead past it, so that no
+// load in the loop needs a guard
+constexpr int kMbBandRows = (kMbUsedY + 11) / 12 * 12;
+constexpr int kMbBandDescRows = kMbBandRows + 3;
+constexpr int kMbBandStride = 52;  // window step: consecutive windows' level-2 outputs abut
+#ifndef MCS_MB_BAND_FRAMES
+#define MCS_MB_BAND_FRAMES 2
+#endif
+constexpr int kMbBandFrames = MCS_MB_BAND_FRAMES;
+struct KMbBandArgs {
+    KParams P;
+    const int *list;               // blend tile list (tile, mask)
+    const int *tile_bt;            // blend-tile grid -> list index (-1: not listed)
+    const MbBand *bands;
+    uint64_t *bdesc;               // [bands][kMbBandDescRows][kMbBandLanes] window descriptors
+    uint16_t *g1;                  // scratch, as KMbArgs
+    int32_t *g2;
+    int slots, chunk, f0, nf;
+    int gxb;                       // blend tiles per mosaic row
+    int band0;                     // first band of this launch
 };
 struct KBlendArgs {
     KParams P;

@@ -1,0 +1,163 @@
+"""Per-capture homography estimation and stitch (SURVEY.md 8 C3 end to end, BASELINE configs[2]).
+
+The reference estimates its homographies once, at calibration (Stitcher.calibrate_stitcher ->
+StitcherBase.calibrate -> detectAndDescribe + matchKeypoints, PostScripts/Stitcher/
+StitcherClass.py:77-112, :258-354, :356-448), and then warps every capture with them.  Config 3
+re-estimates them for every capture; this module closes that loop on the GPU:
+
+  1. ORB (nfeatures, 8 levels x 1.2, FAST 20) of every camera frame, read where it lies in device
+     memory (mcs_orb_detect_device: the same frames are stitched afterwards, so nothing is
+     uploaded twice); one host thread per camera, each with its own HIP stream in libmcs;
+  2. per adjacent pair (camera k+1 -> camera k): BF Hamming kNN-2 (mcs_match_hamming_knn2),
+     Lowe's ratio 0.75 (strict, as :432), and findHomography's RANSAC + LM refinement
+     (mcs_ransac_homography_host, 3.0 px);
+  3. the chain geometry on the host: stage k maps camera k+1 into the mosaic of cameras 0..k,
+     H_k = T(o_k) . H_0 . H_1 ... H_k (pair homographies composed into camera 0's frame, o_k =
+     camera 0's origin in that mosaic), and each stage's plan fields come from geometry.py --
+     the arithmetic of StitcherBase.calibrate (:293-351), bit-identical to the reference's;
+  4. a plan for this capture (host flattening, microseconds) and mcs_stitch_direct: every output
+     pixel mapped by the exact FP64 OpenCV map in the kernel itself, no prepared tables.
+
+A pair whose estimate fails (too few matches or inliers, the reference's H = None) keeps the
+previous capture's homography for that pair; with none yet, its stage stays uncalibrated and
+passes B through, as the reference's reset() stage does (:253-256).
+
+(The reference matches camera k+1 against the mosaic B_k; matching it against camera k and
+composing gives the same homography up to estimation noise without re-stitching the mosaic
+between stages -- each capture needs one stitch launch, not N - 1.)
+"""
+from __future__ import annotations
+
+from concurrent.futures import ThreadPoolExecutor
+from types import SimpleNamespace
+
+import numpy as np
+
+from . import _capi, geometry
+
+
+def _T(tx, ty):
+    return np.array([[1.0, 0.0, tx], [0.0, 1.0, ty], [0.0, 0.0, 1.0]])
+
+
+def ratio_filter(idx, dist, ratio: float = 0.75):
+    """Query indices passing Lowe's test, m0.distance < ratio * m1.distance (strict, as
+    StitcherClass.py:432), vectorised over the kNN-2 output."""
+    ok = (idx[:, 1] >= 0) & (dist[:, 0].astype(np.float64) < dist[:, 1].astype(np.float64) * ratio)
+    return np.nonzero(ok)[0]
+
+
+def chain_stages(pair_H, cam_shapes, super_mode: bool = False):
+    """Stage records (the StitcherBase fields the plan needs) of a left-to-right chain whose
+    adjacent-pair homographies pair_H[k] map camera k+1 into camera k (None: uncalibrated).
+    cam_shapes: (h, w[, C]) of every camera in sorted-label order."""
+    stages = []
+    b_shape = tuple(cam_shapes[0])
+    ox, oy = 0, 0               # camera 0's origin in the mosaic B_k
+    P = np.eye(3)               # camera k+1 -> camera 0
+    broken = False
+    for k in range(len(cam_shapes) - 1):
+        a_shape = tuple(cam_shapes[k + 1])
+        rec = SimpleNamespace(cachedAH=None, super_mode=super_mode, AimgSize=a_shape,
+                              BimgSize=b_shape)
+        if pair_H[k] is None or broken:
+            broken = True       # (the rest of the chain has no reference frame)
+            stages.append(rec)
+            continue
+        P = P @ np.asarray(pair_H[k], np.float64)
+        H = _T(ox, oy) @ P
+        H = H / H[2, 2]
+        g = geometry.stage_geometry(H, a_shape, b_shape)
+        rec.cachedAH = g["cachedAH"]
+        rec.ABSize, rec.Bpts = g["ABSize"], g["Bpts"]
+        rec.x_limits, rec.y_limits = g["x_limits"], g["y_limits"]
+        stages.append(rec)
+        ox += int(g["Bpts"][0][0])
+        oy += int(g["Bpts"][0][1])
+        W, Hh = int(g["ABSize"][0]), int(g["ABSize"][1])
+        if super_mode:
+            x0, x1, _ = slice(int(g["x_limits"][0]), int(g["x_limits"][1])).indices(W)
+            y0, y1, _ = slice(int(g["y_limits"][0]), int(g["y_limits"][1])).indices(Hh)
+            ox -= x0
+            oy -= y0
+            W, Hh = max(0, x1 - x0), max(0, y1 - y0)
+        b_shape = (Hh, W) + tuple(b_shape[2:])
+    return stages
+
+
+class CaptureEstimator:
+    """ORB + Hamming kNN-2 + RANSAC homographies of every adjacent camera pair, per capture, and
+    the stitch of that capture with them (see the module docstring)."""
+
+    def __init__(self, n_cams: int, width: int, height: int, channels: int = 3,
+                 nfeatures: int = 2000, nlevels: int = 8, scale_factor: float = 1.2,
+                 fast_threshold: int = 20, ratio: float = 0.75, reproj_thresh: float = 3.0,
+                 iters: int = 2000, seed: int = 0, super_mode: bool = False,
+                 interp: int = _capi.MCS_INTER_LINEAR, device: int = 0, threads: int = None):
+        self.n_cams, self.w, self.h, self.c = n_cams, width, height, channels
+        self.orb = (nfeatures, nlevels, scale_factor, fast_threshold)
+        self.ratio, self.thresh, self.iters, self.seed = ratio, reproj_thresh, iters, seed
+        self.super_mode, self.interp, self.device = super_mode, interp, device
+        self.pool = ThreadPoolExecutor(max_workers=threads or max(1, n_cams))
+        self.last_H = [None] * (n_cams - 1)
+        self.stats = {}
+
+    def close(self):
+        self.pool.shutdown()
+
+    def features(self, frame_ptrs):
+        """ORB of every camera frame (device pointers, dense h x w x C, producers finished)."""
+        nf, nl, sf, ft = self.orb
+        return list(self.pool.map(
+            lambda p: _capi.orb_detect_device(p, self.w, self.h, self.c, nf, nl, sf, ft,
+                                              self.device), frame_ptrs))
+
+    def pair_homography(self, fa, fb):
+        """Camera A -> camera B (A = query, as matchKeypoints' ptsA): H or None, matches,
+        inliers."""
+        idx, dist = _capi.match_hamming_knn2(fa["desc"], fb["desc"], self.device)
+        q = ratio_filter(idx, dist, self.ratio)
+        if len(q) <= 4:                       # matchKeypoints needs more than 4 (:437)
+            return None, len(q), 0
+        src = np.ascontiguousarray(fa["xy"][q], np.float32)
+        dst = np.ascontiguousarray(fb["xy"][idx[q, 0]], np.float32)
+        H, mask = _capi.ransac_homography(src, dst, self.thresh, self.iters, self.seed,
+                                          device=self.device)
+        n_in = int(mask.sum()) if mask is not None else 0
+        return (H if n_in > 0 else None), len(q), n_in
+
+    def estimate(self, frame_ptrs):
+        """Pair homographies of one capture (camera k+1 -> camera k); a failed pair keeps the
+        previous capture's estimate."""
+        feats = self.features(frame_ptrs)
+        res = list(self.pool.map(lambda k: self.pair_homography(feats[k + 1], feats[k]),
+                                 range(self.n_cams - 1)))
+        pair_H = []
+        for k, (H, n_m, n_in) in enumerate(res):
+            if H is not None:
+                self.last_H[k] = H
+            pair_H.append(self.last_H[k])
+        self.stats = {"keypoints": [len(f["xy"]) for f in feats],
+                      "matches": [r[1] for r in res], "inliers": [r[2] for r in res]}
+        return pair_H
+
+    def plan(self, pair_H):
+        """The plan of one capture's geometry (host only)."""
+        from .StitcherClass import _stage_desc
+        shapes = [(self.h, self.w, self.c)] * self.n_cams
+        stages = chain_stages(pair_H, shapes, self.super_mode)
+        return _capi.Plan([_stage_desc(sb) for sb in stages], self.w, self.h, self.c, self.interp,
+                          device=self.device), stages
+
+    def stitch(self, frame_ptrs, pair_H, out_ptr: int, out_pitch: int, out_capacity: int,
+               stream: int = 0):
+        """Stitch one capture with its homographies into out (rows out_pitch bytes apart,
+        out_capacity bytes).  Returns the plan (its out_w / out_h give the mosaic's size)."""
+        plan, _ = self.plan(pair_H)
+        if plan.out_w * self.c > out_pitch or plan.out_h * out_pitch > out_capacity:
+            plan.close()
+            raise ValueError(f"mosaic {plan.out_w} x {plan.out_h} does not fit the output buffer")
+        fs = self.w * self.h * self.c
+        plan.stitch_direct(frame_ptrs, [fs] * self.n_cams, out_ptr, out_pitch,
+                           out_pitch * plan.out_h, 1, stream)
+        return plan
