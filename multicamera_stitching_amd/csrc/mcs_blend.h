@@ -297,6 +297,15 @@ constexpr int kMbFoot = MCS_MB_FOOT_BYTES;             // bytes of one LDS footp
 constexpr int kMbFootBufs = MCS_MB_FOOT_BUFS;          // 2: double buffer, 1: refilled during
                                                        // the reduces
 constexpr int kMbRS = kMbO1 - kMbOR;                  // R1 region origin in the level-1 array (5)
+// Level scratch of one (tile, owner, capture), row-major (a band's lanes, adjacent columns,
+// store contiguous bytes): g1 (R1 region, 8 B entries) at row * kMbNRX + col, g2 with the
+// channels of an entry together at (row * kMbN2X + col) * CN + channel.
+__device__ __forceinline__ int mb_g1_at(int col, int row) { return row * kMbNRX + col; }
+template <int CN>
+__device__ __forceinline__ int mb_g2_at(int col, int row, int k)
+{
+    return (row * kMbN2X + col) * CN + k;
+}
 
 // Expand taps of fine index x into a coarse level of size n (IN: no reflection needed).
 template <bool IN>
@@ -974,7 +983,7 @@ __device__ __forceinline__ void mb_levels(const KMbArgs &a, MbLvLds<CN> &L)
                     acc[3] += w5[u] * t.w;
                 }
 #pragma unroll
-                for (int k = 0; k < CN; k++) og2[k * (kMbN2X * kMbN2Y) + ey * kMbN2X + ex] = acc[k];
+                for (int k = 0; k < CN; k++) og2[mb_g2_at<CN>(ex, ey, k)] = acc[k];
             }
         } else {
             // mosaic-border tiles: 25-tap form with reflection at every level
@@ -1010,12 +1019,13 @@ __device__ __forceinline__ void mb_levels(const KMbArgs &a, MbLvLds<CN> &L)
                     }
                 }
 #pragma unroll
-                for (int k = 0; k < CN; k++) og2[k * (kMbN2X * kMbN2Y) + e] = acc[k];
+                for (int k = 0; k < CN; k++) og2[mb_g2_at<CN>(e % kMbN2X, e / kMbN2X, k)] = acc[k];
             }
         }
         // the R1 region of g1 (level-1 entries from kMbRS on, both axes)
         for (int e = tid; e < kMbNRX * kMbNRY; e += NT)
-            og1[e] = L.g1[(e / kMbNRX + kMbRS) * kMbN1X + e % kMbNRX + kMbRS];
+            og1[mb_g1_at(e % kMbNRX, e / kMbNRX)] =
+                L.g1[(e / kMbNRX + kMbRS) * kMbN1X + e % kMbNRX + kMbRS];
         __syncthreads();   // the next capture overwrites level 0 and the pass arrays
     }
 }
@@ -1068,6 +1078,28 @@ __device__ __forceinline__ void static_for_(F &&f)
 }
 template <int N, class F>
 __device__ __forceinline__ void static_for(F &&f) { static_for_<0, N>(f); }
+
+// CN consecutive ints (one wide store: 4-byte aligned).
+template <int CN>
+__device__ __forceinline__ void mb_store_ch(__attribute__((address_space(1))) uint8_t *p,
+                                            const int (&v)[CN])
+{
+    typedef __attribute__((address_space(1))) int gi;
+    typedef int i3 __attribute__((ext_vector_type(3), aligned(4)));
+    typedef int i4 __attribute__((ext_vector_type(4), aligned(4)));
+    if (CN == 3) {
+        i3 t;
+        t.x = v[0], t.y = v[CN > 1 ? 1 : 0], t.z = v[CN > 2 ? 2 : 0];
+        *(__attribute__((address_space(1))) i3 *)p = t;
+    } else if (CN == 4) {
+        i4 t;
+        t.x = v[0], t.y = v[CN > 1 ? 1 : 0], t.z = v[CN > 2 ? 2 : 0], t.w = v[CN > 3 ? 3 : 0];
+        *(__attribute__((address_space(1))) i4 *)p = t;
+    } else {
+#pragma unroll
+        for (int k = 0; k < CN; k++) ((gi *)p)[k] = v[k];
+    }
+}
 
 // Scratch targets of one emitted entry: up to two listed tiles of the band's row whose arrays
 // hold the column (base = (list index * slots + local slot) * chunk, col = column in the tile's
@@ -1167,9 +1199,9 @@ __device__ __forceinline__ void mb_bands(const KMbBandArgs &a)
 #pragma unroll
     for (int k = 0; k < 2; k++) {
         o1[k] = T1.base[k] < 0 ? 0u : (uint32_t)((T1.base[k] + fl0) * (kMbNRX * kMbNRY) +
-                                                 T1.col[k]) * 8u;
+                                                 mb_g1_at(T1.col[k], 0)) * 8u;
         o2[k] = T2.base[k] < 0 ? 0u : (uint32_t)((T2.base[k] + fl0) * (kMbN2X * kMbN2Y * CN) +
-                                                 T2.col[k]) * 4u;
+                                                 mb_g2_at<CN>(T2.col[k], 0, 0)) * 4u;
     }
     typedef __attribute__((address_space(1))) uint8_t g8;
     g8 *const g1b = (g8 *)a.g1, *const g2b = (g8 *)a.g2;
@@ -1198,7 +1230,11 @@ __device__ __forceinline__ void mb_bands(const KMbBandArgs &a)
     }
     auto load_win = [&](uint64_t dv, uint2 (&r0)[FR], uint2 (&r1)[FR]) {
         const uint32_t dx = (uint32_t)dv, d = (uint32_t)(dv >> 44) & 7u;
-        const uint32_t o = (dx & 0x7fffffffu) - d, ob = o + ((dx >> 31) ? pitch : 0u);
+        uint32_t o = (dx & 0x7fffffffu) - d, ob = o + ((dx >> 31) ? pitch : 0u);
+#ifdef MCS_MB_BAND_ALIGNED_TEST
+        o &= ~7u;   // (timing experiment only: wrong pixels)
+        ob &= ~7u;
+#endif
 #pragma unroll
         for (int i = 0; i < FR; i++) {
             const U2 ra = *(const gu2 *)(fb[i] + o), rb = *(const gu2 *)(fb[i] + ob);
@@ -1218,7 +1254,7 @@ __device__ __forceinline__ void mb_bands(const KMbBandArgs &a)
             for (int f = 0; f < FR; f++) {
                 if (f >= nst) break;
                 const uint32_t ro =
-                    (uint32_t)(f * (kMbNRX * kMbNRY) + (pend1 - kMbRS) * kMbNRX) * 8u;
+                    (uint32_t)(f * (kMbNRX * kMbNRY) + mb_g1_at(0, pend1 - kMbRS)) * 8u;
 #pragma unroll
                 for (int k = 0; k < 2; k++)
                     if (T1.base[k] >= 0) *(g2u *)(g1b + (o1[k] + ro)) = make_uint2(p1l[f], p1h[f]);
@@ -1229,13 +1265,11 @@ __device__ __forceinline__ void mb_bands(const KMbBandArgs &a)
 #pragma unroll
             for (int f = 0; f < FR; f++) {
                 if (f >= nst) break;
-                const uint32_t ro = (uint32_t)(f * (kMbN2X * kMbN2Y * CN) + pend2 * kMbN2X) * 4u;
+                const uint32_t ro =
+                    (uint32_t)(f * (kMbN2X * kMbN2Y * CN) + mb_g2_at<CN>(0, pend2, 0)) * 4u;
 #pragma unroll
                 for (int q = 0; q < 2; q++)
-                    if (T2.base[q] >= 0)
-#pragma unroll
-                        for (int k = 0; k < CN; k++)
-                            *(gi32 *)(g2b + (o2[q] + ro + k * (kMbN2X * kMbN2Y * 4))) = p2[f][k];
+                    if (T2.base[q] >= 0) mb_store_ch<CN>(g2b + (o2[q] + ro), p2[f]);
             }
             pend2 = -1;
         }
@@ -1573,6 +1607,7 @@ __device__ __forceinline__ void mb_blend(const KMbArgs &a, MbBlLds<CN, S> &L)
         for (int q = 0; q < N2; q++)
             r2[j][q] = s2[min(tid + q * kMbBlThreads, kMbN2X * kMbN2Y * CN - 1)];
     }
+    // (the scratch holds an entry's channels together, mb_g2_at; LDS is channel-planar)
 #pragma unroll
     for (int j = 0; j < S; j++) {
         if (j >= ns) break;
@@ -1580,9 +1615,10 @@ __device__ __forceinline__ void mb_blend(const KMbArgs &a, MbBlLds<CN, S> &L)
         for (int q = 0; q < N1; q++)
             if (tid + q * kMbBlThreads < kMbNRX * kMbNRY) L.g1[j][tid + q * kMbBlThreads] = r1[j][q];
 #pragma unroll
-        for (int q = 0; q < N2; q++)
-            if (tid + q * kMbBlThreads < kMbN2X * kMbN2Y * CN)
-                (&L.g2[j][0][0])[tid + q * kMbBlThreads] = r2[j][q];
+        for (int q = 0; q < N2; q++) {
+            const int e = tid + q * kMbBlThreads;
+            if (e < kMbN2X * kMbN2Y * CN) L.g2[j][e % CN][e / CN] = r2[j][q];
+        }
     }
     __syncthreads();
     if (G.interior) mb_blend_tile<CN, S, true>(a, G, L, px, mask, ns, f);
