@@ -150,6 +150,26 @@ def corner_texture(h, w, seed=0, n_rects=None):
     return np.clip(img, 1, 255).astype(np.uint8)
 
 
+def corner_world(h, w, channels=3, seed=0):
+    """World texture for estimation rigs (ORB needs corners): corner_texture with a small
+    per-channel tint, clipped to [1, 255] (world_frames' world_fn)."""
+    g = corner_texture(h, w, seed=seed).astype(np.int32)
+    tint = np.array([0, 7, -9, 4][:channels], np.int32)
+    return np.clip(g[..., None] + tint, 1, 255).astype(np.uint8)
+
+
+def estimation_rig(n_cams=4, width=1920, height=1080, channels=3, seed=0):
+    """(C, frames, truth) of a rig rendered from one shared corner world:
+    truth[k] = the exact homography camera k+1 -> camera k (H[2][2] = 1)."""
+    C = camera_models(n_cams, width, height, seed=seed)
+    frames = world_frames(C, width, height, channels, seed=seed, world_fn=corner_world)
+    truth = []
+    for k in range(n_cams - 1):
+        T = np.linalg.inv(C[k]) @ C[k + 1]
+        truth.append(T / T[2, 2])
+    return C, frames, truth
+
+
 def labels(n_cams):
     return ["CAM{}".format(i + 1) for i in range(n_cams)]
 

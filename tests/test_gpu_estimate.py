@@ -1,0 +1,99 @@
+"""Per-capture estimate -> stitch on the GPU (SURVEY.md 8 C3 end to end, BASELINE configs[2]):
+at full size (4 x 1920x1080 BGR) the homographies estimated from the frames on the device (ORB
+-> Hamming kNN-2 -> ratio -> RANSAC + LM) are within 1 px of the true ones over the overlaps,
+and the capture stitched with them (a fresh plan, mcs_stitch_direct: no prepared tables) is
+bit-identical to the CPU restatement rendering the same geometry -- and to the prepared-table
+path (mcs_stitch_device) on the same plan."""
+import numpy as np
+import pytest
+
+from oracle import oracle
+from multicamera_stitching_amd import rig
+
+pytestmark = pytest.mark.gpu
+
+
+def _reproj_err(H, T, w, h):
+    """max |H p - T p| over the query camera's left fifth (the overlap with its neighbour)."""
+    u, v = np.meshgrid(np.linspace(0, w * 0.2, 8), np.linspace(0, h - 1, 8))
+    g = np.stack([u.ravel(), v.ravel(), np.ones(u.size)], axis=1)
+    p, q = g @ np.asarray(H).T, g @ np.asarray(T).T
+    return float(np.abs(p[:, :2] / p[:, 2:] - q[:, :2] / q[:, 2:]).max())
+
+
+@pytest.mark.parametrize("super_mode", [False, True])
+def test_estimate_then_stitch_full_size(super_mode):
+    import torch
+    from multicamera_stitching_amd import estimate
+    W, H, N = 1920, 1080, 4
+    _, frames, truth = rig.estimation_rig(N, W, H, 3, seed=0)
+    dev = torch.device("cuda", 0)
+    d = [torch.from_numpy(f).to(dev) for f in frames]
+    torch.cuda.synchronize()
+    ptrs = [t.data_ptr() for t in d]
+    est = estimate.CaptureEstimator(N, W, H, 3, super_mode=super_mode)
+    try:
+        pair_H = est.estimate(ptrs)
+        for k, (Hk, Tk) in enumerate(zip(pair_H, truth)):
+            assert Hk is not None, (k, est.stats)
+            assert _reproj_err(Hk, Tk, W, H) < 1.0, (k, est.stats)
+        pitch = 8192 * 3
+        out = torch.zeros((2048, pitch), dtype=torch.uint8, device=dev)
+        plan = est.stitch(ptrs, pair_H, out.data_ptr(), pitch, out.numel())
+        torch.cuda.synchronize()
+        ow, oh = plan.out_w, plan.out_h
+        # (super mode crops each stage to its overlap limits, StitcherClass.py:248-251)
+        assert (ow > 0 and oh > 0) if super_mode else (ow > 3 * W and oh >= H)
+        got = out[:oh, :ow * 3].cpu().numpy().reshape(oh, ow, 3)
+        want = oracle.flat_stitch(plan.describe(), frames)
+        assert got.shape == want.shape
+        assert int(np.abs(got.astype(np.int16) - want.astype(np.int16)).max()) == 0
+        # the prepared-table path on the same plan renders the same pixels
+        out2 = torch.zeros_like(out)
+        fs = W * H * 3
+        plan.stitch_device(ptrs, [fs] * N, out2.data_ptr(), pitch, pitch * oh, 1)
+        torch.cuda.synchronize()
+        assert torch.equal(out[:oh], out2[:oh])
+        plan.close()
+    finally:
+        est.close()
+
+
+def test_orb_device_input_equals_host_input():
+    import torch
+    from multicamera_stitching_amd import _capi
+    img = rig.corner_world(480, 640, 3, seed=5)
+    d = torch.from_numpy(img).to("cuda:0")
+    torch.cuda.synchronize()
+    a = _capi.orb_detect(img, nfeatures=800)
+    b = _capi.orb_detect_device(d.data_ptr(), 640, 480, 3, nfeatures=800)
+    for key in ("xy", "response", "angle", "level", "desc"):
+        assert np.array_equal(a[key], b[key]), key
+
+
+def test_stitch_direct_batch_and_refusal():
+    """A batch of captures through mcs_stitch_direct equals mcs_stitch_device on the same plan
+    (paste); a blended plan is refused (its owner/blend tables need mcs_plan_prepare)."""
+    import torch
+    from multicamera_stitching_amd import _capi
+    from multicamera_stitching_amd.StitcherClass import _stage_desc
+    st, images, _ = rig.calibrated_stitcher(4, 320, 180, 3, seed=1, rot_deg=2.0, persp=5e-5)
+    cams = [images[lab] for lab in st.img_labels]
+    plan = _capi.Plan([_stage_desc(sb) for sb in st.stitchers], 320, 180, 3, 1)
+    F = 5
+    dev = torch.device("cuda", 0)
+    d = [torch.stack([torch.roll(torch.from_numpy(c), f, 0) for f in range(F)]).to(dev)
+         for c in cams]
+    pitch = plan.out_w * 3
+    a = torch.zeros((F, plan.out_h, pitch), dtype=torch.uint8, device=dev)
+    b = torch.ones_like(a)
+    strides = [t[0].numel() for t in d]
+    plan.stitch_direct([t.data_ptr() for t in d], strides, a.data_ptr(), pitch, a[0].numel(), F)
+    plan.stitch_device([t.data_ptr() for t in d], strides, b.data_ptr(), pitch, b[0].numel(), F)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    plan.set_blend(_capi.MCS_BLEND_MULTIBAND)
+    with pytest.raises(_capi.McsError):
+        plan.stitch_direct([t.data_ptr() for t in d], strides, a.data_ptr(), pitch, a[0].numel(),
+                           F)
+    plan.close()
