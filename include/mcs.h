@@ -324,6 +324,28 @@ int mcs_ransac_homography_host(const float *src_xy, const float *dst_xy, int n, 
 int mcs_homography_refine_host(const float *src_xy, const float *dst_xy, int n,
                                const uint8_t *mask, double *H);
 
+/* ---- Multi-GPU group ---------------------------------------------------
+ * One process per GPU of a node.  Rig captures are independent (capture f -> rank f mod N, each
+ * rank stitching with its own plan, no collective in the stitch itself); the one collective is
+ * the final mosaic gather to the consumer's rank, over RCCL (xGMI point-to-point links).  RCCL
+ * is bound at run time like the HIP runtime: the librccl beside the runtime in the process
+ * (PyTorch-ROCm's), else $MCS_RCCL_LIBRARY, else ROCm's.
+ * unique_id: rank 0 creates the id (MCS_GROUP_ID_BYTES bytes) and hands it to every rank by any
+ * means (a file, a socket, torch.distributed.broadcast_object_list); create: every rank, with
+ * the same n_ranks and id, its own rank and device (collective: blocks until all joined).
+ * gather: every rank's `bytes` contiguous bytes at d_mosaics (e.g. its F finished mosaics) to
+ * rank `root`, which receives rank r's at d_recv + r * bytes (its own copied on the device);
+ * non-roots pass d_recv = NULL.  One grouped send/recv, enqueued on `stream`. */
+#define MCS_GROUP_ID_BYTES 128
+typedef struct mcs_group mcs_group;
+int mcs_group_unique_id(uint8_t *id);
+int mcs_group_create(int n_ranks, int rank, const uint8_t *id, int device, mcs_group **out);
+int mcs_group_gather(mcs_group *group, const uint8_t *d_mosaics, int64_t bytes, uint8_t *d_recv,
+                     int root, void *stream);
+int mcs_group_destroy(mcs_group *group);
+/* Path (or soname) of the bound RCCL ("" when none was found). */
+const char *mcs_rccl_library(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -45,8 +45,10 @@ EXPORTS = (
     "mcs_seam_graphcut_host", "mcs_plan_create_warp", "mcs_plan_create_undistort",
     "mcs_undistort_map_host", "mcs_match_l2_knn2", "mcs_match_l2_knn2_host",
     "mcs_stream_submit_strided", "mcs_build_id", "mcs_homography_refine_host", "mcs_stream_output",
-    "mcs_stitch_direct", "mcs_orb_detect_device",
+    "mcs_stitch_direct", "mcs_orb_detect_device", "mcs_group_unique_id", "mcs_group_create",
+    "mcs_group_gather", "mcs_group_destroy", "mcs_rccl_library",
 )
+MCS_GROUP_ID_BYTES = 128
 
 
 class McsError(RuntimeError):
@@ -234,6 +236,16 @@ def load() -> ctypes.CDLL:
         L.mcs_stitch_device.restype = I
         L.mcs_stitch_direct.argtypes = L.mcs_stitch_device.argtypes
         L.mcs_stitch_direct.restype = I
+        L.mcs_group_unique_id.argtypes = [P]
+        L.mcs_group_unique_id.restype = I
+        L.mcs_group_create.argtypes = [I, I, P, I, ctypes.POINTER(P)]
+        L.mcs_group_create.restype = I
+        L.mcs_group_gather.argtypes = [P, P, ctypes.c_int64, P, I, P]
+        L.mcs_group_gather.restype = I
+        L.mcs_group_destroy.argtypes = [P]
+        L.mcs_group_destroy.restype = I
+        L.mcs_rccl_library.argtypes = []
+        L.mcs_rccl_library.restype = ctypes.c_char_p
         L.mcs_plan_prepare.argtypes = [P, P]
         L.mcs_plan_prepare.restype = I
         L.mcs_plan_stats.argtypes = [P, ctypes.POINTER(ctypes.c_int64), I]
@@ -687,6 +699,51 @@ def orb_detect(image, nfeatures: int = 2000, nlevels: int = 8, scale_factor: flo
                                 desc.ctypes.data, ctypes.byref(n), device))
     k = n.value
     return dict(xy=xy[:k], response=resp[:k], angle=ang[:k], level=lvl[:k], desc=desc[:k])
+
+
+class Group:
+    """mcs_group: RCCL communicator of one process per GPU (include/mcs.h) for
+    the final mosaic gather.  Group.unique_id() on rank 0, passed to every rank; then
+    Group(n_ranks, rank, uid, device) on each (collective)."""
+
+    @staticmethod
+    def unique_id() -> bytes:
+        L = load()
+        buf = (ctypes.c_uint8 * MCS_GROUP_ID_BYTES)()
+        check(L.mcs_group_unique_id(buf))
+        return bytes(buf)
+
+    def __init__(self, n_ranks: int, rank: int, uid: bytes, device: int = 0):
+        L = load()
+        if len(uid) != MCS_GROUP_ID_BYTES:
+            raise ValueError("uid must be %d bytes" % MCS_GROUP_ID_BYTES)
+        buf = (ctypes.c_uint8 * MCS_GROUP_ID_BYTES).from_buffer_copy(uid)
+        h = ctypes.c_void_p()
+        check(L.mcs_group_create(int(n_ranks), int(rank), buf, int(device), ctypes.byref(h)))
+        self._h, self._lib = h, L
+        self.n_ranks, self.rank, self.device = int(n_ranks), int(rank), int(device)
+
+    def gather(self, src_ptr: int, nbytes: int, recv_ptr: int = 0, root: int = 0,
+               stream: int = 0):
+        """Every rank's nbytes at src_ptr to `root`'s recv_ptr + rank * nbytes (enqueued)."""
+        check(self._lib.mcs_group_gather(self._h, ctypes.c_void_p(int(src_ptr)), int(nbytes),
+                                         ctypes.c_void_p(int(recv_ptr)) if recv_ptr else None,
+                                         int(root), ctypes.c_void_p(int(stream))))
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._lib.mcs_group_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def rccl_library() -> str:
+    return (load().mcs_rccl_library() or b"").decode()
 
 
 def orb_detect_device(ptr: int, w: int, h: int, channels: int, nfeatures: int = 2000,

@@ -1146,7 +1146,6 @@ __device__ __forceinline__ void mb_bands(const KMbBandArgs &a)
     };
     typedef __attribute__((address_space(1))) const U2 gu2;
     typedef __attribute__((address_space(1))) uint2 g2u;
-    typedef __attribute__((address_space(1))) int32_t gi32;
     const KParams &P = a.P;
     const int l = threadIdx.x;
     const int bi = a.band0 + blockIdx.x;

@@ -55,6 +55,28 @@ def gather_mosaics(local, dst: int = 0, bufs=None):
     return None
 
 
+def mcs_group(device: int):
+    """The libmcs RCCL group (mcs_group_create) of this torch.distributed job: rank 0's
+    unique id reaches every rank through the process group; collective."""
+    import torch.distributed as dist
+    from . import _capi
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    box = [_capi.Group.unique_id() if rank == 0 else None]
+    if world > 1:
+        dist.broadcast_object_list(box, src=0)
+    return _capi.Group(world, rank, box[0], device)
+
+
+def gather_mosaics_group(group, local, recv=None, dst: int = 0, stream: int = 0):
+    """Every rank's mosaics (contiguous tensor `local`, same size everywhere) to rank `dst`
+    through mcs_group_gather: recv (on dst) = a (world, *local.shape) tensor, rank r's at
+    recv[r].  Enqueued on `stream`."""
+    group.gather(local.data_ptr(), local.numel() * local.element_size(),
+                 recv.data_ptr() if recv is not None else 0, dst, stream)
+    return recv
+
+
 def timed_loop(step, steps: int, warmup: int, sync, record=None) -> float:
     """The bench contract's timed region on this rank: `warmup` untimed steps, then exactly
     `steps` timed ones bracketed on both sides by (sync, barrier, sync); returns this rank's
