@@ -178,7 +178,8 @@ __device__ __forceinline__ int owner(const KParams &P, int x, int y)
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 
-// 8 bytes of LDS starting at byte a (any alignment): three dword reads + v_alignbyte.
+// 8 bytes of LDS starting at byte a (any alignment): three dword reads + v_alignbyte.  (An
+// unaligned ds_read_b64 is legal on gfx950 but measured 2.5x slower in the streaming kernel.)
 __device__ __forceinline__ uint2 lds_window(const uint8_t *smem, uint32_t a)
 {
     const lds_u32 *d = (const lds_u32 *)(((const lds_u8 *)smem) + (a & ~3u));
@@ -190,7 +191,15 @@ __device__ __forceinline__ uint2 lds_window(const uint8_t *smem, uint32_t a)
     return r;
 }
 
-// Channel k of a pixel from its two row windows: v_perm_b32 + 2 x v_dot2_u32_u16.
+// Bilinear weights of the stitch kernels as u16 pairs: remapBilinear's 15-bit weight w (the four
+// sum to 32768) is stored doubled, min(2 w, 65535), so that a channel's sum
+// s = sum p (2 w) + 32768 carries (sum p w + 2^14) >> 15 -- remapBilinear's value -- in its
+// byte 2.  (Only fx = fy = 0 gives w = 32768, all on one tap: 65535 p + 32768 still has p in
+// byte 2.)  pack_b2 then assembles output bytes with v_perm instead of shift + or per byte.
+__device__ __forceinline__ uint32_t w2x(uint32_t w) { return w >= 32768u ? 65535u : 2u * w; }
+
+// Channel k of a pixel from its two row windows (v_perm_b32 + 2 x v_dot2_u32_u16): the result
+// byte is byte 2 of the returned sum (bits 24+ are 0).
 template <int CN>
 __device__ __forceinline__ uint32_t blend(uint2 r0, uint2 r1, uint32_t w0, uint32_t w1, int k)
 {
@@ -199,9 +208,15 @@ __device__ __forceinline__ uint32_t blend(uint2 r0, uint2 r1, uint32_t w0, uint3
     const uint32_t a0 = __builtin_amdgcn_perm(r0.y, r0.x, sel);
     const uint32_t a1 = __builtin_amdgcn_perm(r1.y, r1.x, sel);
     uint32_t s = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, a0), __builtin_bit_cast(us2, w0),
-                                        16384u, false);
+                                        32768u, false);
     s = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, a1), __builtin_bit_cast(us2, w1), s, false);
-    return s >> 15;
+    return s;
+}
+
+// Byte 2 of a, b, c, d as the bytes 0..3 of one word (two v_perm + or).
+__device__ __forceinline__ uint32_t pack_b2(uint32_t a, uint32_t b, uint32_t c, uint32_t d)
+{
+    return __builtin_amdgcn_perm(b, a, 0x0c0c0602u) | __builtin_amdgcn_perm(d, c, 0x06020c0cu);
 }
 
 }  // namespace mcs
@@ -236,6 +251,18 @@ struct OutWords {
         return i == 0 ? w0 : (i == 1 ? w1 : (i == 2 ? w2 : w3));
     }
 };
+
+// The lane's 4 * CN output bytes from the blend sums of its 4 pixels (channel-interleaved).
+template <int CN>
+__device__ __forceinline__ OutWords pack_words(const uint32_t (&r)[kPx * CN])
+{
+    OutWords w;
+    w.w0 = pack_b2(r[0], r[1], r[2], r[3]);
+    if (CN > 1) w.w1 = pack_b2(r[4 % (kPx * CN)], r[5 % (kPx * CN)], r[6 % (kPx * CN)], r[7 % (kPx * CN)]);
+    if (CN > 2) w.w2 = pack_b2(r[8 % (kPx * CN)], r[9 % (kPx * CN)], r[10 % (kPx * CN)], r[11 % (kPx * CN)]);
+    if (CN > 3) w.w3 = pack_b2(r[12 % (kPx * CN)], r[13 % (kPx * CN)], r[14 % (kPx * CN)], r[15 % (kPx * CN)]);
+    return w;
+}
 
 // Inserts pixel p's packed bytes (channel k = byte k of v) into the lane's output words.
 template <int CN>
@@ -348,8 +375,8 @@ __device__ __forceinline__ Geo describe_geo(const KParams &P, int x, int y)
     g.c1 = place_cols(sx, sw, y1_in ? w10 : 0u, y1_in ? w11 : 0u, a1, b1) * CN;
     g.r0 = y0_in ? sy : 0;
     g.r1 = y1_in ? sy + 1 : 0;
-    g.w0 = a0 | (b0 << 16);
-    g.w1 = a1 | (b1 << 16);
+    g.w0 = w2x(a0) | (w2x(b0) << 16);
+    g.w1 = w2x(a1) | (w2x(b1) << 16);
     if (g.w0 == 0u) {            // no live tap in row 0: reuse row 1's window
         g.r0 = g.r1;
         g.c0 = g.c1;
@@ -422,14 +449,12 @@ __device__ __forceinline__ void stitch_direct(const KParams &P, int f0, int n_fr
                 r1[p] = shr_bytes(r1[p], d[p].shift >> 4);
             }
         }
-        OutWords w;
+        uint32_t rr[kPx * CN];
 #pragma unroll
         for (int p = 0; p < kPx; p++)
 #pragma unroll
-            for (int k = 0; k < CN; k++) {
-                const int b = p * CN + k;
-                w.or_at(b >> 2, blend<CN>(r0[p], r1[p], d[p].w0, d[p].w1, k) << (8 * (b & 3)));
-            }
+            for (int k = 0; k < CN; k++) rr[p * CN + k] = blend<CN>(r0[p], r1[p], d[p].w0, d[p].w1, k);
+        const OutWords w = pack_words<CN>(rr);
         uint8_t *o = dst + (int64_t)f * P.out_fstride;
         if (wide) {
             uint32_t *o32 = reinterpret_cast<uint32_t *>(o);
@@ -733,20 +758,18 @@ __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *til
         if (full) stage_capture(J, ring0 + slot_a * buf_bytes, (int64_t)ahead * fstride, lane);
         const uint8_t *b = ring0 + slot_f * buf_bytes;
         if (live) {
-            OutWords w;
+            uint32_t rr[kPx * CN];
 #pragma unroll
             for (int p = 0; p < kPx; p++) {
                 const uint32_t win = d[p * kDescWords];
                 const uint2 r0 = lds_window(b, win & 0xffffu);
                 const uint2 r1 = lds_window(b, win >> 16);
 #pragma unroll
-                for (int k = 0; k < CN; k++) {
-                    const int bb = p * CN + k;
-                    w.or_at(bb >> 2, blend<CN>(r0, r1, d[p * kDescWords + 1],
-                                               d[p * kDescWords + 2], k)
-                                         << (8 * (bb & 3)));
-                }
+                for (int k = 0; k < CN; k++)
+                    rr[p * CN + k] = blend<CN>(r0, r1, d[p * kDescWords + 1],
+                                               d[p * kDescWords + 2], k);
             }
+            const OutWords w = pack_words<CN>(rr);
             uint8_t *o = dst + (int64_t)f * P.out_fstride;
             if (wide) {
                 uint32_t *o32 = reinterpret_cast<uint32_t *>(o);
