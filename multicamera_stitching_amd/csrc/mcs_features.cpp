@@ -22,8 +22,7 @@ struct FeatureKernels {
     bool loaded = false;
     hipFunction_t knn2 = nullptr, knn2_finalize = nullptr;
     hipFunction_t ransac_score = nullptr, ransac_mask = nullptr;
-    hipFunction_t orb_gray = nullptr, orb_blur_h = nullptr, orb_blur_v = nullptr;
-    hipFunction_t orb_fast = nullptr, orb_nms = nullptr, orb_describe = nullptr;
+    hipFunction_t orb_gray = nullptr, orb_level = nullptr, orb_describe = nullptr;
     hipFunction_t orb_select = nullptr;
     hipFunction_t l2_prep = nullptr, l2_i8 = nullptr, l2_f32 = nullptr, l2_finalize = nullptr;
 };
@@ -81,9 +80,8 @@ int feature_kernels(const Api *A, int device, const FeatureKernels **out)
         const struct {
             const char *name;
             hipFunction_t *f;
-        } orb[] = {{"mcs_orb_gray", &k.orb_gray},     {"mcs_orb_blur_h", &k.orb_blur_h},
-                   {"mcs_orb_blur_v", &k.orb_blur_v}, {"mcs_orb_fast", &k.orb_fast},
-                   {"mcs_orb_nms", &k.orb_nms},       {"mcs_orb_describe", &k.orb_describe},
+        } orb[] = {{"mcs_orb_gray", &k.orb_gray},     {"mcs_orb_level", &k.orb_level},
+                   {"mcs_orb_describe", &k.orb_describe},
                    {"mcs_orb_select", &k.orb_select},
                    {"mcs_l2_prep", &k.l2_prep},       {"mcs_l2_knn2_i8", &k.l2_i8},
                    {"mcs_l2_knn2_f32", &k.l2_f32},    {"mcs_l2_knn2_finalize", &k.l2_finalize}};
@@ -489,8 +487,7 @@ int orb_detect(const uint8_t *image, bool on_device, int w, int h, int channels,
         o += (bytes + 255) & ~(size_t)255;
         return at;
     };
-    const size_t o_in = take(in_bytes), o_lvl = take(pix), o_h16 = take(2 * pix);
-    const size_t o_blur = take(pix), o_score = take(pix);
+    const size_t o_in = take(in_bytes), o_lvl = take(pix), o_blur = take(pix);
     const size_t o_cand = take(cap_total * sizeof(mcs::OrbCand));
     const size_t o_cnt = take(mcs::kOrbMaxLevels * sizeof(int));
     const size_t o_kp = take((size_t)std::max(nfeatures, 1) * 3 * sizeof(int));
@@ -533,13 +530,11 @@ int orb_detect(const uint8_t *image, bool on_device, int w, int h, int channels,
                                       0, buf + o_lvl + off[l], lw[l], lh[l], lw[l], 0, 1, 1,
                                       device, s);
     if (e == hipSuccess && rc == MCS_OK) {
-        // blur, FAST and NMS of every level: one launch each
+        // blur, FAST, NMS and Harris of every level: one launch (mcs_orb_level, 64 x 16 tiles)
         mcs::KOrbPyrArgs pa;
         std::memset(&pa, 0, sizeof(pa));
         pa.img = buf + o_lvl;
-        pa.hblur = reinterpret_cast<uint16_t *>(buf + o_h16);
         pa.blur = buf + o_blur;
-        pa.score = buf + o_score;
         pa.cand = reinterpret_cast<mcs::OrbCand *>(buf + o_cand);
         pa.ncand = reinterpret_cast<int *>(buf + o_cnt);
         pa.nlevels = nlevels;
@@ -550,11 +545,9 @@ int orb_detect(const uint8_t *image, bool on_device, int w, int h, int channels,
             pa.w[l] = lw[l];
             pa.h[l] = lh[l];
             pa.cap[l] = (int)cap[l];
-            pa.bstart[l + 1] = pa.bstart[l] + (lw[l] + 255) / 256 * lh[l];
+            pa.bstart[l + 1] = pa.bstart[l] + (lw[l] + 63) / 64 * ((lh[l] + 15) / 16);
         }
-        for (hipFunction_t f : {k->orb_blur_h, k->orb_blur_v, k->orb_fast, k->orb_nms})
-            if (rc == MCS_OK)
-                rc = launch(A, f, (unsigned)pa.bstart[nlevels], 1, 256, &pa, sizeof(pa), s);
+        rc = launch(A, k->orb_level, (unsigned)pa.bstart[nlevels], 1, 256, &pa, sizeof(pa), s);
     }
     // Device ranking (mcs_orb_select) and description, then ONE copy back of counts,
     // keypoints, descriptors, orientations and responses.  A level with more than kOrbSelMax

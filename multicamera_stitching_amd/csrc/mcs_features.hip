@@ -348,123 +348,118 @@ __device__ __forceinline__ int orb_refl(int i, int n)
     return i < 0 ? -i : (i >= n ? 2 * n - 2 - i : i);
 }
 
-// horizontal 7-tap pass (u16, exact).
-__device__ __forceinline__ void orb_blur_h(const mcs::KOrbLevelArgs a, const int x, const int y)
-{
-    if (x >= a.w) return;
-    const uint8_t *r = a.img + (int64_t)y * a.w;
-    int s = 0;
-#pragma unroll
-    for (int i = 0; i < 7; i++) s += mcs::kOrbBlur[i] * r[orb_refl(x + i - 3, a.w)];
-    a.hblur[(int64_t)y * a.w + x] = (uint16_t)s;
-}
+// One launch per frame over every pyramid level: per 64 x 16 tile of a level (block ->
+// level by the prefix table bstart, tiles row-major), the level image with a 4-pixel halo
+// (reflect-101 positions, for the blur) is staged in LDS once; from it
+//   - the 7-tap Gaussian blur (horizontal pass in u16 into LDS, vertical pass with one
+//     rounding, (s + 32768) >> 16: the descriptors' image),
+//   - the FAST-9 scores of the tile and a one-pixel ring (score > threshold, else 0; 0 outside
+//     the region where a keypoint's NMS can look),
+//   - the 3x3 non-maximum suppression of the tile's pixels (strict, inside the kOrbEdge
+//     border), the survivors compacted in LDS so that the Harris sums (32-bit exact, 7x7 Sobel
+//     on the staged image) run on full waves, and appended to the level's candidates (their
+//     order is irrelevant: the level is ranked afterwards by response, y, x).
+// Same values as the four per-pixel passes it replaces (blur_h, blur_v, fast, nms).
+constexpr int kOrbTX = 64, kOrbTY = 16, kOrbHalo = 4;
+constexpr int kOrbLX = kOrbTX + 2 * kOrbHalo, kOrbLY = kOrbTY + 2 * kOrbHalo;   // 72 x 24
+constexpr int kOrbSX = kOrbTX + 2, kOrbSY = kOrbTY + 2;                         // score ring
 
-// vertical pass, one rounding.
-__device__ __forceinline__ void orb_blur_v(const mcs::KOrbLevelArgs a, const int x, const int y)
+extern "C" __global__ __launch_bounds__(256) void mcs_orb_level(const mcs::KOrbPyrArgs p)
 {
-    if (x >= a.w) return;
-    int s = 0;
-#pragma unroll
-    for (int j = 0; j < 7; j++)
-        s += mcs::kOrbBlur[j] * (int)a.hblur[(int64_t)orb_refl(y + j - 3, a.h) * a.w + x];
-    a.blur[(int64_t)y * a.w + x] = (uint8_t)((s + 32768) >> 16);
-}
-
-// FAST scores of corners (score > threshold) where the NMS of a
-// keypoint candidate can look (one pixel around the keypoint region), 0 elsewhere.
-__device__ __forceinline__ void orb_fast(const mcs::KOrbLevelArgs a, const int x, const int y)
-{
-    if (x >= a.w) return;
-    const int lo = mcs::kOrbEdge - 1;
-    uint8_t v = 0;
-    if (x >= lo && y >= lo && x < a.w - lo && y < a.h - lo) {
-        const int sc = mcs::orb_fast_score(a.img + (int64_t)y * a.w + x, a.w);
-        v = sc > a.threshold ? (uint8_t)sc : 0;
-    }
-    a.score[(int64_t)y * a.w + x] = v;
-}
-
-// 3x3 non-maximum suppression + Harris response; survivors appended.
-// The block first gathers its row segment's survivors in LDS, so the Harris sums run on the
-// first ceil(n / 64) waves only, every lane busy, instead of on every wave holding a survivor.
-__device__ __forceinline__ void orb_nms(const mcs::KOrbLevelArgs a, const int x, const int y)
-{
-    __shared__ int sx[256];
+    __shared__ uint8_t img[kOrbLY * kOrbLX];
+    __shared__ uint16_t hb[(kOrbTY + 6) * kOrbTX];
+    __shared__ uint8_t sc[kOrbSY * kOrbSX];
+    __shared__ int sx[kOrbTX * kOrbTY];
     __shared__ int ns;
-    const int e = mcs::kOrbEdge;
-    if (threadIdx.x == 0) ns = 0;
-    __syncthreads();
-    bool keep = x >= e && y >= e && x < a.w - e && y < a.h - e;
-    if (keep) {
-        const uint8_t *s = a.score + (int64_t)y * a.w + x;
-        const int c = s[0];
-        keep = c != 0;
-#pragma unroll
-        for (int dy = -1; dy <= 1; dy++)
-#pragma unroll
-            for (int dx = -1; dx <= 1; dx++)
-                if (dx || dy) keep = keep && c > s[dy * a.w + dx];
+    const int b = blockIdx.x, tid = threadIdx.x;
+    int l = 0;
+    for (int k = 1; k < p.nlevels; k++) l += b >= p.bstart[k] ? 1 : 0;
+    const int w = p.w[l], h = p.h[l];
+    const int bx = (w + kOrbTX - 1) / kOrbTX, loc = b - p.bstart[l];
+    const int y0 = (loc / bx) * kOrbTY, x0 = (loc % bx) * kOrbTX;
+    const uint8_t *im = p.img + p.off[l];
+    if (tid == 0) ns = 0;
+    for (int i = tid; i < kOrbLY * kOrbLX; i += 256) {
+        const int yy = orb_refl(min(max(y0 - kOrbHalo + i / kOrbLX, -(h - 1)), 2 * h - 2), h);
+        const int xx = orb_refl(min(max(x0 - kOrbHalo + i % kOrbLX, -(w - 1)), 2 * w - 2), w);
+        img[i] = im[(int64_t)yy * w + xx];
     }
-    if (keep) {
-        const unsigned long long act = __ballot(1);
-        const int lane = __lane_id(), leader = __ffsll((long long)act) - 1;
-        int base = 0;
-        if (lane == leader) base = atomicAdd(&ns, __popcll(act));
-        sx[__shfl(base, leader) + __popcll(act & ((1ull << lane) - 1ull))] = x;
+    __syncthreads();
+    // blur: horizontal over rows y0 - 3 .. y0 + 18, then vertical
+    for (int i = tid; i < (kOrbTY + 6) * kOrbTX; i += 256) {
+        const uint8_t *r = img + (i / kOrbTX + 1) * kOrbLX + i % kOrbTX + 1;
+        int s = 0;
+#pragma unroll
+        for (int t = 0; t < 7; t++) s += mcs::kOrbBlur[t] * r[t];
+        hb[i] = (uint16_t)s;
+    }
+    // FAST on the tile and a one-pixel ring (positions x0 - 1 .., y0 - 1 ..)
+    const int lo = mcs::kOrbEdge - 1;
+    for (int i = tid; i < kOrbSY * kOrbSX; i += 256) {
+        const int yy = y0 - 1 + i / kOrbSX, xx = x0 - 1 + i % kOrbSX;
+        uint8_t v = 0;
+        if (xx >= lo && yy >= lo && xx < w - lo && yy < h - lo) {
+            const int s = mcs::orb_fast_score(
+                img + (i / kOrbSX + kOrbHalo - 1) * kOrbLX + i % kOrbSX + kOrbHalo - 1, kOrbLX);
+            v = s > p.threshold ? (uint8_t)s : 0;
+        }
+        sc[i] = v;
+    }
+    __syncthreads();
+    uint8_t *blur = p.blur + p.off[l];
+    for (int i = tid; i < kOrbTY * kOrbTX; i += 256) {
+        const int yy = y0 + i / kOrbTX, xx = x0 + i % kOrbTX;
+        if (yy >= h || xx >= w) continue;
+        const uint16_t *c = hb + (i / kOrbTX) * kOrbTX + i % kOrbTX;
+        int s = 0;
+#pragma unroll
+        for (int t = 0; t < 7; t++) s += mcs::kOrbBlur[t] * (int)c[t * kOrbTX];
+        blur[(int64_t)yy * w + xx] = (uint8_t)((s + 32768) >> 16);
+    }
+    // 3x3 NMS of the tile's pixels; survivors (packed y << 16 | x) compacted in LDS
+    const int e = mcs::kOrbEdge;
+    for (int i = tid; i < kOrbTY * kOrbTX; i += 256) {
+        const int yy = y0 + i / kOrbTX, xx = x0 + i % kOrbTX;
+        bool keep = xx >= e && yy >= e && xx < w - e && yy < h - e;
+        if (keep) {
+            const uint8_t *s = sc + (i / kOrbTX + 1) * kOrbSX + i % kOrbTX + 1;
+            const int c = s[0];
+            keep = c != 0;
+#pragma unroll
+            for (int dy = -1; dy <= 1; dy++)
+#pragma unroll
+                for (int dx = -1; dx <= 1; dx++)
+                    if (dx || dy) keep = keep && c > s[dy * kOrbSX + dx];
+        }
+        if (keep) {
+            const unsigned long long act = __ballot(1);
+            const int lane = __lane_id(), leader = __ffsll((long long)act) - 1;
+            int base = 0;
+            if (lane == leader) base = atomicAdd(&ns, __popcll(act));
+            sx[__shfl(base, leader) + __popcll(act & ((1ull << lane) - 1ull))] = i;
+        }
     }
     __syncthreads();
     const int n = ns;
-    if ((int)threadIdx.x >= n) return;
-    const int xs = sx[threadIdx.x];
-    const double r = mcs::orb_harris(a.img + (int64_t)y * a.w + xs, a.w);
-    // one atomic per wave: the lanes take consecutive slots (their order is irrelevant: the
-    // host ranks each level's candidates)
-    const unsigned long long act = __ballot(1);
-    const int lane = __lane_id(), leader = __ffsll((long long)act) - 1;
-    int base = 0;
-    if (lane == leader) base = atomicAdd(a.ncand, __popcll(act));
-    const int i = __shfl(base, leader) + __popcll(act & ((1ull << lane) - 1ull));
-    if (i < a.cap) {
-        a.cand[i].x = xs;
-        a.cand[i].y = y;
-        a.cand[i].response = r;
+    for (int j0 = 0; j0 < n; j0 += 256) {
+        const int j = j0 + tid;
+        if (j >= n) break;
+        const int i = sx[j];
+        const double r = mcs::orb_harris(
+            img + (i / kOrbTX + kOrbHalo) * kOrbLX + i % kOrbTX + kOrbHalo, kOrbLX);
+        const unsigned long long act = __ballot(1);
+        const int lane = __lane_id(), leader = __ffsll((long long)act) - 1;
+        int base = 0;
+        if (lane == leader) base = atomicAdd(p.ncand + l, __popcll(act));
+        const int q = __shfl(base, leader) + __popcll(act & ((1ull << lane) - 1ull));
+        if (q < p.cap[l]) {
+            mcs::OrbCand *cand = p.cand + p.coff[l];
+            cand[q].x = x0 + i % kOrbTX;
+            cand[q].y = y0 + i / kOrbTX;
+            cand[q].response = r;
+        }
     }
 }
-
-// Level of this block (KOrbPyrArgs), its pixel (x, y) and its per-level view.
-__device__ __forceinline__ mcs::KOrbLevelArgs orb_level(const mcs::KOrbPyrArgs &p, int &x, int &y)
-{
-    const int b = blockIdx.x;
-    int l = 0;
-    for (int k = 1; k < p.nlevels; k++) l += b >= p.bstart[k] ? 1 : 0;
-    const int bx = (p.w[l] + 255) >> 8, loc = b - p.bstart[l];
-    y = loc / bx;
-    x = (loc - y * bx) * 256 + (int)threadIdx.x;
-    mcs::KOrbLevelArgs a;
-    a.img = p.img + p.off[l];
-    a.hblur = p.hblur + p.off[l];
-    a.blur = p.blur + p.off[l];
-    a.score = p.score + p.off[l];
-    a.cand = p.cand + p.coff[l];
-    a.ncand = p.ncand + l;
-    a.w = p.w[l];
-    a.h = p.h[l];
-    a.threshold = p.threshold;
-    a.cap = p.cap[l];
-    return a;
-}
-
-#define MCS_ORB_PYR_KERNEL(NAME)                                                               \
-    extern "C" __global__ __launch_bounds__(256) void mcs_orb_##NAME(const mcs::KOrbPyrArgs p) \
-    {                                                                                          \
-        int x, y;                                                                              \
-        const mcs::KOrbLevelArgs a = orb_level(p, x, y);                                       \
-        orb_##NAME(a, x, y);                                                                   \
-    }
-MCS_ORB_PYR_KERNEL(blur_h)
-MCS_ORB_PYR_KERNEL(blur_v)
-MCS_ORB_PYR_KERNEL(fast)
-MCS_ORB_PYR_KERNEL(nms)
 
 // grid (nlevels), block kOrbSelThreads: the level's candidates ranked in LDS by a bitonic sort
 // (response descending, then y, then x: the host ranking's total order; (y, x) packed as

@@ -68,23 +68,12 @@ struct OrbCand {
     int x, y;
     double response;
 };
-struct KOrbLevelArgs {
-    const uint8_t *img;    // level image (w x h, dense)
-    uint16_t *hblur;       // horizontal blur pass
-    uint8_t *blur;         // blurred level
-    uint8_t *score;        // FAST scores of corners (0 elsewhere)
-    OrbCand *cand;         // NMS survivors with their Harris response
-    int *ncand;
-    int w, h, threshold, cap;
-};
-// All levels of one frame in one launch: grid (bstart[nlevels]) blocks of 256 threads, level l
-// owning blocks [bstart[l], bstart[l + 1]), one block per 256-pixel row segment.  Level buffers
-// are the bases + off[l] (pixels) and cand + coff[l] (candidates).
+// All levels of one frame in one launch (mcs_orb_level): grid (bstart[nlevels]) blocks of 256
+// threads, level l owning blocks [bstart[l], bstart[l + 1]), one block per 64 x 16 tile (row-major
+// over the level).  Level buffers are the bases + off[l] (pixels) and cand + coff[l].
 struct KOrbPyrArgs {
     const uint8_t *img;
-    uint16_t *hblur;
     uint8_t *blur;
-    uint8_t *score;
     OrbCand *cand;
     int *ncand;                 // [nlevels]
     int64_t off[12];
