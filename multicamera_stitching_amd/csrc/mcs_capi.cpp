@@ -84,7 +84,7 @@ using mcs::rt::Api;
 struct Kernels {
     bool loaded = false;
     hipFunction_t prepare[5][2] = {};     // [channels][interp]
-    hipFunction_t stream[5] = {};         // [channels]
+    hipFunction_t stream[5][2] = {};      // [channels][buffer-resource DMA]
     hipFunction_t direct[5][2][2] = {};   // [channels][interp][32-bit offsets]
     hipFunction_t footprint[2] = {};
     hipFunction_t resize[5] = {};         // [channels]
@@ -115,7 +115,9 @@ int kernels(const Api *A, int device, const Kernels **out)
         int rc = MCS_OK;
         for (int c = 1; c <= 4 && rc == MCS_OK; c++) {
             snprintf(name, sizeof(name), "mcs_stream_c%d", c);
-            rc = fn(name, &k.stream[c]);
+            rc = fn(name, &k.stream[c][0]);
+            snprintf(name, sizeof(name), "mcs_stream_c%d_b32", c);
+            if (rc == MCS_OK) rc = fn(name, &k.stream[c][1]);
             snprintf(name, sizeof(name), "mcs_resize_c%d", c);
             if (rc == MCS_OK) rc = fn(name, &k.resize[c]);
             snprintf(name, sizeof(name), "mcs_mb_levels_c%d", c);
@@ -204,6 +206,29 @@ bool offset_base(const mcs_plan *p, const mcs::KParams &kp, const uint8_t **base
     const bool off32 = !g_force_off64 && hi - lo < (uintptr_t(1) << 32);
     *base = off32 ? (const uint8_t *)lo : nullptr;
     return off32;
+}
+
+// The streaming kernel's DMA base: when every byte of every capture of every used camera lies in
+// [base, base + 4 GiB) the footprint rows are read through one buffer resource with 32-bit
+// offsets (mcs_stream_c*_b32).  Captures are fstride = cam_fstride[0] apart (the stream kernel's
+// layout).
+bool stream_base(const mcs_plan *p, const mcs::KParams &kp, int n_frames, const uint8_t **base)
+{
+    bool need[MCS_MAX_CAMS];
+    need_mask(p->fd, need);
+    uintptr_t lo = UINTPTR_MAX, hi = 0;
+    const uintptr_t span = (uintptr_t)(n_frames > 0 ? n_frames - 1 : 0) * kp.cam_fstride[0];
+    for (int i = 0; i < p->fd.n_cams; i++) {
+        if (!need[i]) continue;
+        const uintptr_t a = (uintptr_t)kp.cams[i];
+        const uintptr_t e = a + span + (uintptr_t)p->fd.cam_w[i] * p->fd.cam_h[i] * p->fd.channels;
+        lo = a < lo ? a : lo;
+        hi = e > hi ? e : hi;
+    }
+    static const bool off = getenv("MCS_STREAM_B32") && strcmp(getenv("MCS_STREAM_B32"), "0") == 0;
+    const bool b32 = !off && !g_force_off64 && lo <= hi && hi - lo < (uintptr_t(1) << 32);
+    *base = b32 ? (const uint8_t *)lo : kp.base;
+    return b32;
 }
 
 int launch_args(const Api *A, hipFunction_t f, unsigned gx, unsigned gy, unsigned bx,
@@ -624,6 +649,7 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
     {
         mcs::KStreamArgs args;
         args.P = P;
+        const bool b32 = stream_base(p, P, n_frames, &args.P.base);
         args.tiles = p->d_tiles;
         args.desc = p->d_desc;
         args.n_frames = n_frames;
@@ -634,7 +660,8 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
         // 1-D grid dealt over the 8 XCDs; the kernel maps block -> tile (XCD-contiguous bands)
         const unsigned n_tiles = (unsigned)(p->gx * p->gy);
         const unsigned grid = 8u * ((n_tiles + 7u) / 8u);
-        HIP_TRY(A->hipModuleLaunchKernel(k->stream[p->fd.channels], grid, 1, 1, mcs::kWave,
+        HIP_TRY(A->hipModuleLaunchKernel(k->stream[p->fd.channels][b32 ? 1 : 0], grid, 1, 1,
+                                         mcs::kWave,
                                          mcs::kWavesPerBlock, 1,
                                          mcs::lds_stream_bytes(p->fd.channels), s, nullptr, cfg));
     }

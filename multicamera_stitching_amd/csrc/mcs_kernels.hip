@@ -613,26 +613,32 @@ __device__ __forceinline__ void prepare_tile(const KParams &P, TileHdr *tiles, u
 __device__ __forceinline__ int uni(const int &v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // The LDS-DMA jobs of one wave: its footprint rows (j = wave, wave + 8, ...), resolved once per
-// block into scalar registers (compile-time indexed), so a capture costs one address add and one
-// global_load_lds_dwordx4 per row.  Per row: the frame-0 source address of its first 16-byte
-// chunk and one packed word, LDS offset (bits 0-15) | 16-byte chunks (16-23).  Every chunk lies
-// inside its camera frame (TileHdr::last_shift).
+// block into scalar registers (compile-time indexed), so a capture costs one 32-bit add and one
+// LDS-DMA instruction per row.  Per row: the byte offset of its first 16-byte chunk in frame 0
+// and one packed word, LDS offset (bits 0-15) | 16-byte chunks (16-23).  Every chunk lies inside
+// its camera frame (TileHdr::last_shift).
+//   BUF (every byte of every capture of every used camera within 4 GiB of P.base): offsets from
+//   P.base, read through one buffer resource (buffer_load_dwordx4 ... offen lds), the capture's
+//   offset f * fstride in the instruction's scalar offset -- no per-row 64-bit address math;
+//   otherwise 64-bit frame-0 addresses for global_load_lds_dwordx4.
+template <bool BUF>
 struct WaveJobs {
-    const uint8_t *src[kJobsPerWave];
+    typedef typename std::conditional<BUF, uint32_t, const uint8_t *>::type src_t;
+    src_t src[kJobsPerWave];
     uint32_t w[kJobsPerWave];
     int n;
 };
 
-template <int CN>
-__device__ __forceinline__ WaveJobs wave_jobs(const KParams &P, const TileHdr &h, int wave)
+template <int CN, bool BUF>
+__device__ __forceinline__ WaveJobs<BUF> wave_jobs(const KParams &P, const TileHdr &h, int wave)
 {
-    WaveJobs J;
+    WaveJobs<BUF> J;
     const int njobs = uni(h.njobs);
     J.n = 0;
 #pragma unroll
     for (int jj = 0; jj < kJobsPerWave; jj++) {
         const int j = wave + jj * kWavesPerBlock;
-        J.src[jj] = nullptr;
+        J.src[jj] = 0;
         J.w[jj] = 0;
         if (j < njobs) {
             int k = 0;
@@ -643,7 +649,12 @@ __device__ __forceinline__ WaveJobs wave_jobs(const KParams &P, const TileHdr &h
             const int64_t pitch = (int64_t)P.cam_w[c] * CN;
             const int r = uni(h.rmin[k]) + row;
             const int e = r == P.cam_h[c] - 1 ? (uni(h.last_shift) >> (8 * k)) & 255 : 0;
-            J.src[jj] = P.cams[c] + (int64_t)r * pitch + uni(h.cal[k]) - e;
+            const int64_t in_frame = (int64_t)r * pitch + uni(h.cal[k]) - e;
+            if constexpr (BUF)
+                J.src[jj] = (uint32_t)((uint64_t)(uintptr_t)P.cams[c] -
+                                       (uint64_t)(uintptr_t)P.base + (uint64_t)in_frame);
+            else
+                J.src[jj] = P.cams[c] + in_frame;
             J.w[jj] = (uint32_t)(uni(h.base[k]) + row * stride) | ((uint32_t)(stride >> 4) << 16);
             J.n = jj + 1;
         }
@@ -652,19 +663,26 @@ __device__ __forceinline__ WaveJobs wave_jobs(const KParams &P, const TileHdr &h
 }
 
 // Issues capture f's footprint rows into `slot`: one LDS-DMA wave instruction per row (lane =
-// 16-byte chunk).
-__device__ __forceinline__ void stage_capture(const WaveJobs &J, uint8_t *slot, int64_t foff,
-                                              int lane)
+// 16-byte chunk).  foff = f * fstride (fits 32 bits in BUF mode).
+template <bool BUF>
+__device__ __forceinline__ void stage_capture(const WaveJobs<BUF> &J, __amdgpu_buffer_rsrc_t rs,
+                                              uint8_t *slot, int64_t foff, int lane)
 {
 #pragma unroll
     for (int jj = 0; jj < kJobsPerWave; jj++) {
         if (jj < J.n) {
             const uint32_t w = J.w[jj];
             // LDS destination: wave-uniform row base (M0); the hardware adds 16 * lane
-            if (lane < (int)(w >> 16))
-                __builtin_amdgcn_global_load_lds(J.src[jj] + foff + 16 * lane,
-                                                 ((lds_u8 *)slot) + (w & 0xffffu), 16, 0,
-                                                 MCS_DMA_AUX);
+            if (lane < (int)(w >> 16)) {
+                if constexpr (BUF)
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                        rs, ((lds_u8 *)slot) + (w & 0xffffu), 16, J.src[jj] + 16 * lane,
+                        (int)(uint32_t)foff, 0, MCS_DMA_AUX);
+                else
+                    __builtin_amdgcn_global_load_lds(J.src[jj] + foff + 16 * lane,
+                                                     ((lds_u8 *)slot) + (w & 0xffffu), 16, 0,
+                                                     MCS_DMA_AUX);
+            }
         }
     }
 }
@@ -698,7 +716,7 @@ __device__ __forceinline__ void wait_vmcnt_le(int n)
 // [x * per, (x+1) * per), walked row-major; vertically adjacent tiles, whose footprints overlap
 // by a few source rows, then run at about the same time on the same L2.  (Placement affects
 // speed only.)
-template <int CN>
+template <int CN, bool BUF>
 __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *tiles,
                                             const uint32_t *desc, int n_frames, uint8_t *smem)
 {
@@ -734,7 +752,11 @@ __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *til
             d[4 * i + 3] = v.w;
         }
     }
-    const WaveJobs J = wave_jobs<CN>(P, h, wave);
+    const WaveJobs<BUF> J = wave_jobs<CN, BUF>(P, h, wave);
+    // (BUF: raw buffer over [P.base, P.base + 4 GiB); no range clamping needed, every chunk is
+    // inside a frame)
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(BUF ? P.base : P.out), 0, 0xffffffff, 0x00020000);
     const int ring = uni(h.ring), buf_bytes = uni(h.buf_bytes), njobs = uni(h.njobs);
     const int d_min = njobs / kWavesPerBlock;
     const int waitn = min((ring - 2) * d_min, 15);
@@ -742,7 +764,7 @@ __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *til
     const bool wide = npx == kPx && (((uintptr_t)dst | (uintptr_t)P.out_fstride) & 3) == 0;
     const int64_t fstride = P.cam_fstride[0];
     for (int q = 0; q < ring - 1 && q < n_frames; q++)
-        stage_capture(J, ring0 + q * buf_bytes, (int64_t)q * fstride, lane);
+        stage_capture<BUF>(J, rs, ring0 + q * buf_bytes, (int64_t)q * fstride, lane);
     wait_vmcnt_le(0);
     __builtin_amdgcn_s_barrier();
     // Steady state: waitn = DMA instructions this wave has certainly issued after those of
@@ -755,7 +777,8 @@ __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *til
     for (int f = 0; f < n_frames; f++) {
         const int ahead = f + ring - 1;
         const bool full = ahead < n_frames;
-        if (full) stage_capture(J, ring0 + slot_a * buf_bytes, (int64_t)ahead * fstride, lane);
+        if (full)
+            stage_capture<BUF>(J, rs, ring0 + slot_a * buf_bytes, (int64_t)ahead * fstride, lane);
         const uint8_t *b = ring0 + slot_f * buf_bytes;
         if (live) {
             uint32_t rr[kPx * CN];
@@ -924,12 +947,12 @@ __device__ __forceinline__ void resize_px(const KResizeArgs &a)
 #else
 #define MCS_STREAM_ATTR
 #endif
-#define MCS_STREAM_ENTRY(CN)                                                                   \
-    extern "C" __global__ __launch_bounds__(512) MCS_STREAM_ATTR void mcs_stream_c##CN(        \
+#define MCS_STREAM_ENTRY(CN, SUF, BUF)                                                         \
+    extern "C" __global__ __launch_bounds__(512) MCS_STREAM_ATTR void mcs_stream_c##CN##SUF(   \
         const mcs::KParams P, const mcs::TileHdr *tiles, const uint32_t *desc, int n_frames)  \
     {                                                                                          \
         extern __shared__ __attribute__((aligned(16))) uint8_t smem[];                         \
-        mcs::stream_tile<CN>(P, tiles, desc, n_frames, smem);                                  \
+        mcs::stream_tile<CN, BUF>(P, tiles, desc, n_frames, smem);                             \
     }
 #define MCS_DIRECT_ENTRY(CN, IN, O32)                                                          \
     extern "C" __global__ __launch_bounds__(512) void mcs_direct_c##CN##_i##IN##_o##O32(       \
@@ -940,7 +963,8 @@ __device__ __forceinline__ void resize_px(const KResizeArgs &a)
 #define MCS_ENTRIES(CN)                                                                        \
     MCS_PREPARE_ENTRY(CN, 0)                                                                   \
     MCS_PREPARE_ENTRY(CN, 1)                                                                   \
-    MCS_STREAM_ENTRY(CN)                                                                       \
+    MCS_STREAM_ENTRY(CN, , false)                                                              \
+    MCS_STREAM_ENTRY(CN, _b32, true)                                                           \
     MCS_DIRECT_ENTRY(CN, 0, 32)                                                                \
     MCS_DIRECT_ENTRY(CN, 1, 32)                                                                \
     MCS_DIRECT_ENTRY(CN, 0, 64)                                                                \
