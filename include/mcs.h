@@ -153,8 +153,9 @@ int mcs_plan_describe(const mcs_plan *plan, mcs_flat_desc *out);
  * call it on first use.  stream: hipStream_t or NULL for the plan's own stream. */
 int mcs_plan_prepare(mcs_plan *plan, void *stream);
 
-/* stats[0..6] = prepared, tiles, tiles on the LDS path, tiles on the direct path, table bytes,
- * blend mode, 32-px tiles the blend kernels recompute per frame. */
+/* stats[0..7] = prepared, tiles, tiles on the LDS path, tiles on the direct path, table bytes,
+ * blend mode, 32-px tiles the blend kernels recompute per frame, the most owners any multi-band
+ * tile blends (<= 8; more in one 64 x 64 neighbourhood fails with MCS_E_UNSUPPORTED). */
 int mcs_plan_stats(const mcs_plan *plan, int64_t *stats, int n);
 
 /* Blend mode of the plan (MCS_BLEND_*; default NONE = the reference's paste).  Changing it drops

@@ -94,7 +94,7 @@ struct Kernels {
     hipFunction_t feather[5][2] = {};     // [channels][interp]
     hipFunction_t mb_prep[5][2] = {};     // [channels][interp]
     hipFunction_t mb_levels[5] = {};      // [channels]
-    hipFunction_t mb_blend[5][2] = {};    // [channels][<= 2 owners : <= 4]
+    hipFunction_t mb_blend[5][3] = {};    // [channels][<= 2 owners, <= 4, <= 8]
     hipFunction_t mb_bands[5][2] = {};    // [channels][reaches the bottom / right edge]
     hipFunction_t mb_bdesc[5][2] = {};    // [channels][interp]
 };
@@ -130,6 +130,8 @@ int kernels(const Api *A, int device, const Kernels **out)
             if (rc == MCS_OK) rc = fn(name, &k.mb_blend[c][0]);
             snprintf(name, sizeof(name), "mcs_mb_blend_c%d_s4", c);
             if (rc == MCS_OK) rc = fn(name, &k.mb_blend[c][1]);
+            snprintf(name, sizeof(name), "mcs_mb_blend_c%d_s8", c);
+            if (rc == MCS_OK) rc = fn(name, &k.mb_blend[c][2]);
             for (int i = 0; i < 2 && rc == MCS_OK; i++) {
                 snprintf(name, sizeof(name), "mcs_prepare_c%d_i%d", c, i);
                 rc = fn(name, &k.prepare[c][i]);
@@ -688,7 +690,9 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
                 m.f0 = f0;
                 m.nf = nf;
                 if (rc == MCS_OK)
-                    rc = launch_args(A, k->mb_blend[p->fd.channels][p->mb_slots <= 2 ? 0 : 1],
+                    rc = launch_args(A,
+                                     k->mb_blend[p->fd.channels]
+                                                [p->mb_slots <= 2 ? 0 : (p->mb_slots <= 4 ? 1 : 2)],
                                      (unsigned)p->n_blend,
                                      (unsigned)nf, mcs::kMbBlThreads, 1, &m, sizeof(m), s);
             }
@@ -1410,11 +1414,11 @@ int mcs_plan_stats(const mcs_plan *p, int64_t *stats, int n)
 {
     if (!p || !stats) return mcs::fail(MCS_E_INVALID, "NULL plan/stats");
     const int64_t tiles = (int64_t)p->gx * p->gy;
-    const int64_t v[7] = {p->prepared ? 1 : 0, tiles, tiles - p->n_fallback, p->n_fallback,
+    const int64_t v[8] = {p->prepared ? 1 : 0, tiles, tiles - p->n_fallback, p->n_fallback,
                           tiles * (int64_t)(sizeof(mcs::TileHdr) +
                                             mcs::kTilePx * mcs::kDescWords * 4),
-                          p->blend, p->n_blend};
-    for (int i = 0; i < n; i++) stats[i] = i < 7 ? v[i] : 0;
+                          p->blend, p->n_blend, p->mb_slots};
+    for (int i = 0; i < n; i++) stats[i] = i < 8 ? v[i] : 0;
     return MCS_OK;
 }
 

@@ -1049,6 +1049,12 @@ extern "C" __global__ __launch_bounds__(256) void mcs_blend_classify(const mcs::
     {                                                                                          \
         __shared__ mcs::MbBlLds<CN, 4> lds;                                                    \
         mcs::mb_blend<CN, 4>(a, lds);                                                          \
+    }                                                                                          \
+    extern "C" __global__ __launch_bounds__(256) void mcs_mb_blend_c##CN##_s8(                \
+        const mcs::KMbArgs a)                                                                  \
+    {                                                                                          \
+        __shared__ mcs::MbBlLds<CN, 8> lds;                                                    \
+        mcs::mb_blend<CN, 8>(a, lds);                                                          \
     }
 MCS_MB_ENTRY(1)
 MCS_MB_ENTRY(2)

@@ -139,7 +139,8 @@ constexpr int kResizeBlock = 256;
 constexpr int kBlendTileW = 32;
 constexpr int kBlendTileH = MCS_BLEND_TILE_H;
 constexpr int kBlendHalo = 16;
-constexpr int kBlendSlots = 4;
+// most owners in one multi-band neighbourhood (blend kernels for <= 2, <= 4 and <= 8)
+constexpr int kBlendSlots = 8;
 constexpr int kBlendNone = 255;
 // multi-band kernels (mcs_blend.h): prep once per plan, then per chunk of captures levels + blend
 constexpr int kMbPrepThreads = 256;
