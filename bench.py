@@ -291,7 +291,7 @@ def main():
             "roofline": {
                 "bound": "hbm",
                 "kernel": "mcs_stream_c%d%s (one launch)" % (
-                    C, {"multiband": " + mcs_mb_levels_c%d + mcs_mb_blend_c%d" % (C, C),
+                    C, {"multiband": " + mcs_mb_bands(_br)_c%d + mcs_mb_blend_c%d" % (C, C),
                         "feather": " + mcs_feather_c%d_i1" % C, "none": "",
                         "seam": ""}[args.blend]),
                 "achieved": round(achieved, 1),

@@ -289,6 +289,7 @@ int prepare_bands(const Api *A, mcs_plan *p, const Kernels *k, hipStream_t s)
     const int gyb = (H + mcs::kBlendTileH - 1) / mcs::kBlendTileH;
     const mcs::KParams &P = p->kp;
     for (int c = 0; c <= P.n_stages; c++) {
+        if (c == 0 && P.cam0_w == 0) continue;     // (cylindrical plans: no slot-0 camera)
         const int64_t w = c == 0 ? P.cam0_w : P.st[c - 1].src_w;
         const int64_t h = c == 0 ? P.cam0_h : P.st[c - 1].src_h;
         if ((h - 1) * w * C < 16) return MCS_OK;   // (mb_levels' guarded window loads)

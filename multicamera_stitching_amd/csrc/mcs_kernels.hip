@@ -947,6 +947,11 @@ __device__ __forceinline__ void resize_px(const KResizeArgs &a)
 #else
 #define MCS_STREAM_ATTR
 #endif
+#ifdef MCS_MB_BL_WPE   // experiment knob: occupancy target of the multi-band blend kernel
+#define MCS_MB_BL_ATTR __attribute__((amdgpu_waves_per_eu(MCS_MB_BL_WPE)))
+#else
+#define MCS_MB_BL_ATTR
+#endif
 #define MCS_STREAM_ENTRY(CN, SUF, BUF)                                                         \
     extern "C" __global__ __launch_bounds__(512) MCS_STREAM_ATTR void mcs_stream_c##CN##SUF(   \
         const mcs::KParams P, const mcs::TileHdr *tiles, const uint32_t *desc, int n_frames)  \
@@ -1038,19 +1043,22 @@ extern "C" __global__ __launch_bounds__(256) void mcs_blend_classify(const mcs::
     {                                                                                          \
         mcs::mb_bands<CN, mcs::kMbBandFrames, true>(a);                                        \
     }                                                                                          \
-    extern "C" __global__ __launch_bounds__(256) void mcs_mb_blend_c##CN##_s2(                \
+    extern "C" __global__ __launch_bounds__(MCS_MB_BL_THREADS) MCS_MB_BL_ATTR void             \
+        mcs_mb_blend_c##CN##_s2(                                                               \
         const mcs::KMbArgs a)                                                                  \
     {                                                                                          \
         __shared__ mcs::MbBlLds<CN, 2> lds;                                                    \
         mcs::mb_blend<CN, 2>(a, lds);                                                          \
     }                                                                                          \
-    extern "C" __global__ __launch_bounds__(256) void mcs_mb_blend_c##CN##_s4(                \
+    extern "C" __global__ __launch_bounds__(MCS_MB_BL_THREADS) MCS_MB_BL_ATTR void             \
+        mcs_mb_blend_c##CN##_s4(                                                               \
         const mcs::KMbArgs a)                                                                  \
     {                                                                                          \
         __shared__ mcs::MbBlLds<CN, 4> lds;                                                    \
         mcs::mb_blend<CN, 4>(a, lds);                                                          \
     }                                                                                          \
-    extern "C" __global__ __launch_bounds__(256) void mcs_mb_blend_c##CN##_s8(                \
+    extern "C" __global__ __launch_bounds__(MCS_MB_BL_THREADS) MCS_MB_BL_ATTR void             \
+        mcs_mb_blend_c##CN##_s8(                                                               \
         const mcs::KMbArgs a)                                                                  \
     {                                                                                          \
         __shared__ mcs::MbBlLds<CN, 8> lds;                                                    \

@@ -153,7 +153,10 @@ constexpr int kMbLvThreads = MCS_MB_LV_THREADS;
 #endif
 constexpr int kMbLvFrames = MCS_MB_LV_FRAMES;   // captures per levels block (sample windows held
                                                 // in registers)
-constexpr int kMbBlThreads = 256;
+#ifndef MCS_MB_BL_THREADS
+#define MCS_MB_BL_THREADS 256
+#endif
+constexpr int kMbBlThreads = MCS_MB_BL_THREADS;
 constexpr int64_t kMbScratchBytes = 1ll << 30;    // level scratch budget per plan (<= 64 captures)
 // The pyramid arrays a tile holds, per axis (tile side T): level 0 [O - 14, O + T + 10]
 // (T + 25), level 1 [O/2 - 6, O/2 + T/2 + 4] (T/2 + 11), level 2 [O/4 - 2, O/4 + T/4 + 1]

@@ -13,15 +13,28 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PMC = os.environ.get("MCS_PMC_DIR", os.path.join(ROOT, "gpurun_out", "pmc"))
 
 
+def _window_start(rows):
+    """First dispatch of the bench's own launches in one pass: after the last plan prepare
+    (mcs_prepare_* / mcs_cyl_prepare_*).  Earlier stitch dispatches belong to the Stitcher's
+    calibration (its own small plans) and are not bench launches."""
+    last = -1
+    for r in rows:
+        if "prepare" in r["Kernel_Name"]:
+            last = max(last, int(r["Dispatch_Id"]))
+    return last + 1
+
+
 def family_counters(prefix, totals=False):
-    """Per-dispatch averages of every counter over the dispatches of kernels named prefix*
-    (totals=True: (sum over the dispatches, dispatches per pass))."""
+    """Per-dispatch averages of every counter over the bench-launch dispatches of kernels named
+    prefix* (totals=True: (sum over the dispatches, dispatches per pass))."""
     vals = defaultdict(lambda: defaultdict(float))     # (pass, dispatch) -> counter -> value
     for f in sorted(glob.glob(os.path.join(PMC, "pass*", "**", "*counter_collection.csv"),
                               recursive=True)):
         p = f.split(os.sep)[len(PMC.split(os.sep))]
-        for r in csv.DictReader(open(f)):
-            if not r["Kernel_Name"].startswith(prefix):
+        rows = list(csv.DictReader(open(f)))
+        start = _window_start(rows)
+        for r in rows:
+            if not r["Kernel_Name"].startswith(prefix) or int(r["Dispatch_Id"]) < start:
                 continue
             vals[(p, int(r["Dispatch_Id"]))][r["Counter_Name"]] += float(r["Counter_Value"])
     per_counter = defaultdict(list)
@@ -93,6 +106,6 @@ def main(prefixes=("mcs_stream_c3",), workload=None, out=None):
 if __name__ == "__main__":
     wl = sys.argv[1] if len(sys.argv) > 1 else "4x1920x1080x3-linear-super0-F64-multiband"
     kernels = (sys.argv[2].split(",") if len(sys.argv) > 2
-               else ["mcs_stream_c3", "mcs_mb_levels_c3", "mcs_mb_blend_c3"])
+               else ["mcs_stream_c3", "mcs_mb_bands", "mcs_mb_levels_c3", "mcs_mb_blend_c3"])
     out = sys.argv[3] if len(sys.argv) > 3 else os.path.join(ROOT, "profiles", "pmc_latest.json")
     main(prefixes=kernels, workload=wl, out=out)
