@@ -1332,22 +1332,23 @@ __device__ __forceinline__ void mb_bands(const KMbBandArgs &a)
             }
         }
     };
-    // Pipeline over rows: at row r the windows of rows r + 1 and r + 2 and the descriptor of row
-    // r + 3 are in flight, three buffers each indexed by row % 3.  The 12-row body makes every
-    // buffer and accumulator index a compile-time constant, so no register copy ever reads an
-    // in-flight load (such a copy makes the compiler drain all loads at the loop's back edge).
-    uint64_t dq[3];
-    uint2 wq0[3][FR], wq1[3][FR];
-    dq[0] = dsc[0];
-    dq[1] = dsc[kMbBandLanes];
-    dq[2] = dsc[2 * kMbBandLanes];
-    load_win(dq[0], wq0[0], wq1[0]);
-    load_win(dq[1], wq0[1], wq1[1]);
+    // Pipeline over rows: at row r the windows of rows r + 1 .. r + A and the descriptor of row
+    // r + A + 1 are in flight (A = kMbBandAhead), A + 1 buffers each indexed by row % (A + 1).
+    // The 12-row body makes every buffer and accumulator index a compile-time constant, so no
+    // register copy ever reads an in-flight load (such a copy makes the compiler drain all loads
+    // at the loop's back edge).
+    constexpr int NB = kMbBandBufs, A = kMbBandAhead;
+    uint64_t dq[NB];
+    uint2 wq0[NB][FR], wq1[NB][FR];
+#pragma unroll
+    for (int i = 0; i < NB; i++) dq[i] = dsc[i * kMbBandLanes];
+#pragma unroll
+    for (int i = 0; i < A; i++) load_win(dq[i], wq0[i], wq1[i]);
     for (int r12 = 0; r12 < kMbBandRows; r12 += 12) {
         static_for<12>([&](auto PHc) {
             constexpr int ph = decltype(PHc)::value;
             const int r = r12 + ph;
-            constexpr int b0 = ph % 3, b2 = (ph + 2) % 3;
+            constexpr int b0 = ph % NB, bA = (ph + A) % NB;
             uint32_t wa, wb;
             const uint32_t meta = (uint32_t)(dq[b0] >> 32), dd = (meta >> 12) & 7u;
             mb_weights(meta, wa, wb);
@@ -1360,10 +1361,10 @@ __device__ __forceinline__ void mb_bands(const KMbBandArgs &a)
                     v[f] |= mb_tap<CN>(wq0[b0][f], wq1[b0][f], wa, wb, c, dd) << (8 * c);
             }
             // the previous row's finished entries (after this row's window wait), then the loads:
-            // windows of row r + 2 (its descriptor arrived a row ago), descriptor of row r + 3
+            // windows of row r + A (its descriptor arrived a row ago), descriptor of row r + A + 1
             flush();
-            load_win(dq[b2], wq0[b2], wq1[b2]);
-            dq[b0] = dsc[(r + 3) * kMbBandLanes];
+            load_win(dq[bA], wq0[bA], wq1[bA]);
+            dq[b0] = dsc[(r + NB) * kMbBandLanes];
             // level-0 row r = 2k + (ph & 1), k % 3 = K3; level-1 row k - 2 = 2m + P2, m % 3 = M3
             constexpr int K3 = (ph / 2) % 3;
             constexpr int q = ph / 2 - 2, P2 = q & 1, M3 = ((q - P2) / 2 + 3) % 3;
@@ -1427,6 +1428,9 @@ __device__ __forceinline__ void mb_blend_tile(const KMbArgs &a, const MbGeo &G, 
     auto ir = [&](int cx, int cy) {   // the R1 region (g1, m1, d1, r1)
         return (int)__umul24((unsigned)ix2<IN>(cy, G.YR, kMbNRY), kMbNRX) + ix2<IN>(cx, G.XR, kMbNRX);
     };
+#if defined(MCS_MB_BL_SKIP) && MCS_MB_BL_SKIP >= 3
+    return;
+#endif
     // B2 = sum m2 g2 / (sum m2 * 65536)
     for (int e = tid; e < kMbN2X * kMbN2Y; e += nt) {
         // (integer sums in double: every product < 2^41, every sum < 2^43 -- exact)
@@ -1444,6 +1448,9 @@ __device__ __forceinline__ void mb_blend_tile(const KMbArgs &a, const MbGeo &G, 
             L.b2[k][e] = den ? num[k] / ((double)den * 65536.0) : 0.0;
     }
     __syncthreads();
+#if defined(MCS_MB_BL_SKIP) && MCS_MB_BL_SKIP >= 2
+    return;
+#endif
     // R1 = B1 + up(B2), B1 = sum m1 (16384 g1 - E(g2)) / (sum m1 * 4194304)
     const int n_r1 = t_d2[kMbN2X * kMbN2Y + 1];
     const uint16_t *t_r1 =
@@ -1499,6 +1506,9 @@ __device__ __forceinline__ void mb_blend_tile(const KMbArgs &a, const MbGeo &G, 
         }
     }
     __syncthreads();
+#if defined(MCS_MB_BL_SKIP) && MCS_MB_BL_SKIP >= 1
+    return;
+#endif
     // R0 = L0_owner / 16384 + up(R1) over the tile's own pixels; L0 = 16384 g0 - E(g1), g0 = the
     // owner sample already in the mosaic
 #pragma unroll

@@ -219,7 +219,15 @@ constexpr int kMbBandLanes = 64;
 // rows feed no stored entry), and descriptor rows for the 3-row lookahead past it, so that no
 // load in the loop needs a guard
 constexpr int kMbBandRows = (kMbUsedY + 11) / 12 * 12;
-constexpr int kMbBandDescRows = kMbBandRows + 3;
+// rows of window loads the band pass keeps in flight ahead of the row it computes (+1 buffer;
+// the buffer count divides the 12-row body)
+#ifndef MCS_MB_BAND_AHEAD
+#define MCS_MB_BAND_AHEAD 2
+#endif
+constexpr int kMbBandAhead = MCS_MB_BAND_AHEAD;
+constexpr int kMbBandBufs = kMbBandAhead + 1;
+static_assert(12 % kMbBandBufs == 0, "band pass: buffers must divide the 12-row body");
+constexpr int kMbBandDescRows = kMbBandRows + kMbBandBufs;
 constexpr int kMbBandStride = 52;  // window step: consecutive windows' level-2 outputs abut
 #ifndef MCS_MB_BAND_FRAMES
 #define MCS_MB_BAND_FRAMES 2
