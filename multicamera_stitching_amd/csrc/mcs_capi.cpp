@@ -35,6 +35,11 @@ struct mcs_plan {
     // second side stream: the multi-band level pyramids (concurrent with both of the above)
     hipStream_t side2 = nullptr;
     hipEvent_t ev_join2 = nullptr;
+    // multi-band: the streaming tiles under mixed blend pixels run first (d_order[0, n_early)),
+    // then the multi-band blend starts on side2 (ev_early) beside the rest of the streaming tiles
+    hipEvent_t ev_early = nullptr;
+    int *d_order = nullptr;
+    int n_early = 0;
     // host path with frames off their calibrated size: upload buffers for the resize pre-pass
     uint8_t *d_raw[MCS_MAX_CAMS] = {};
     size_t raw_bytes[MCS_MAX_CAMS] = {};
@@ -375,6 +380,31 @@ int prepare_bands(const Api *A, mcs_plan *p, const Kernels *k, hipStream_t s)
         for (const mcs::MbBand &b : bands)
             fprintf(stderr, "band slot %d row %d c0 %d\n", b.slot, b.row, b.c0);
     if (bands.empty()) return MCS_OK;
+    {
+        // streaming tiles under the blend tiles that have mixed pixels: launched first, so the
+        // blend (which overwrites those pixels) can run beside the other streaming tiles
+        std::vector<char> early((size_t)p->gx * p->gy, 0);
+        for (int i = 0; i < n; i++) {
+            if (cnt[(size_t)i * mcs::kMbTabCounts] == 0) continue;
+            const int t = list[1 + 2 * i];
+            const int X0 = (t % p->gxb) * mcs::kBlendTileW, Y0 = (t / p->gxb) * mcs::kBlendTileH;
+            const int x1 = std::min(X0 + mcs::kBlendTileW, W) - 1;
+            const int y1 = std::min(Y0 + mcs::kBlendTileH, H) - 1;
+            for (int ty = Y0 / mcs::kTileH; ty <= y1 / mcs::kTileH; ty++)
+                for (int tx = X0 / mcs::kTileW; tx <= x1 / mcs::kTileW; tx++)
+                    early[(size_t)ty * p->gx + tx] = 1;
+        }
+        std::vector<int> order;
+        order.reserve(early.size());
+        for (size_t t = 0; t < early.size(); t++)
+            if (early[t]) order.push_back((int)t);
+        p->n_early = (int)order.size();
+        for (size_t t = 0; t < early.size(); t++)
+            if (!early[t]) order.push_back((int)t);
+        HIP_TRY(A->hipMalloc((void **)&p->d_order, order.size() * sizeof(int)));
+        HIP_TRY(A->hipMemcpyAsync(p->d_order, order.data(), order.size() * sizeof(int),
+                                  hipMemcpyHostToDevice, s));
+    }
     // bands whose rows or columns reach past the bottom / right mosaic edge: the _br kernel
     auto br = [&](const mcs::MbBand &b) {
         return b.row * mcs::kBlendTileH - mcs::kBlendHalo + mcs::kMbFirst + mcs::kMbUsedY > H ||
@@ -489,8 +519,10 @@ void release_tables(const Api *A, mcs_plan *p)
                     (void *)p->d_owner, (void *)p->d_binfo, (void *)p->d_blist,
                     (void *)p->d_mbdesc, (void *)p->d_mbtab, (void *)p->d_mbfoot, (void *)p->d_mbg1,
                     (void *)p->d_mbg2, (void *)p->d_bands, (void *)p->d_tile_bt,
-                    (void *)p->d_bdesc})
+                    (void *)p->d_bdesc, (void *)p->d_order})
         if (q) (void)A->hipFree(q);
+    p->d_order = nullptr;
+    p->n_early = 0;
     p->d_bands = nullptr;
     p->d_tile_bt = nullptr;
     p->d_bdesc = nullptr;
@@ -643,30 +675,63 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
                                          0, p->side, nullptr, cfg));
         HIP_TRY(A->hipEventRecord(p->ev_join, p->side));
     }
+    // split (multi-band, one scratch chunk): streaming tiles under mixed pixels first, then the
+    // blend on side2 (after the band pass, those tiles and the direct-gather tiles) beside the
+    // remaining streaming tiles.  MCS_MB_SPLIT=0 (experiments): the blend after everything.
+    static const bool split_on = !getenv("MCS_MB_SPLIT") || strcmp(getenv("MCS_MB_SPLIT"), "0");
+    const bool split = mb && split_on && p->d_order && p->n_early > 0 && n_frames <= p->mb_chunk;
     if (mb) {
         HIP_TRY(A->hipStreamWaitEvent(p->side2, p->ev_fork, 0));
         const int rc = launch_mb_levels(A, p, k, m, 0, std::min(p->mb_chunk, n_frames), p->side2);
         if (rc) return rc;
-        HIP_TRY(A->hipEventRecord(p->ev_join2, p->side2));
+        if (!split) HIP_TRY(A->hipEventRecord(p->ev_join2, p->side2));
     }
-    {
-        mcs::KStreamArgs args;
-        args.P = P;
-        const bool b32 = stream_base(p, P, n_frames, &args.P.base);
-        args.tiles = p->d_tiles;
-        args.desc = p->d_desc;
-        args.n_frames = n_frames;
-        args.pad_ = 0;
+    mcs::KStreamArgs args;
+    args.P = P;
+    const bool b32 = stream_base(p, P, n_frames, &args.P.base);
+    args.tiles = p->d_tiles;
+    args.desc = p->d_desc;
+    args.n_frames = n_frames;
+    args.pad_ = 0;
+    args.pad2_ = 0;
+    // 1-D grid dealt over the 8 XCDs; the kernel maps block -> tile (XCD-contiguous bands)
+    auto stream_launch = [&](const int *order, int n_tiles) -> int {
+        args.order = order;
+        args.n_order = n_tiles;
         size_t sz = sizeof(args);
         void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, (void *)&args, HIP_LAUNCH_PARAM_BUFFER_SIZE,
                        &sz, HIP_LAUNCH_PARAM_END};
-        // 1-D grid dealt over the 8 XCDs; the kernel maps block -> tile (XCD-contiguous bands)
-        const unsigned n_tiles = (unsigned)(p->gx * p->gy);
-        const unsigned grid = 8u * ((n_tiles + 7u) / 8u);
+        const unsigned grid = 8u * (((unsigned)n_tiles + 7u) / 8u);
         HIP_TRY(A->hipModuleLaunchKernel(k->stream[p->fd.channels][b32 ? 1 : 0], grid, 1, 1,
-                                         mcs::kWave,
-                                         mcs::kWavesPerBlock, 1,
+                                         mcs::kWave, mcs::kWavesPerBlock, 1,
                                          mcs::lds_stream_bytes(p->fd.channels), s, nullptr, cfg));
+        return MCS_OK;
+    };
+    const int n_tiles = p->gx * p->gy;
+    if (split) {
+        int rc = stream_launch(p->d_order, p->n_early);
+        if (rc) return rc;
+        HIP_TRY(A->hipEventRecord(p->ev_early, s));
+        HIP_TRY(A->hipStreamWaitEvent(p->side2, p->ev_early, 0));
+        if (p->n_fallback > 0) HIP_TRY(A->hipStreamWaitEvent(p->side2, p->ev_join, 0));
+        m.f0 = 0;
+        m.nf = n_frames;
+        rc = launch_args(A, k->mb_blend[p->fd.channels][p->mb_slots <= 2 ? 0 : (p->mb_slots <= 4 ? 1 : 2)],
+                         (unsigned)p->n_blend, (unsigned)n_frames, mcs::kMbBlThreads, 1, &m,
+                         sizeof(m), p->side2);
+        if (rc) return rc;
+        HIP_TRY(A->hipEventRecord(p->ev_join2, p->side2));
+        if (n_tiles > p->n_early) {
+            rc = stream_launch(p->d_order + p->n_early, n_tiles - p->n_early);
+            if (rc) return rc;
+        }
+        if (p->n_fallback > 0) HIP_TRY(A->hipStreamWaitEvent(s, p->ev_join, 0));
+        HIP_TRY(A->hipStreamWaitEvent(s, p->ev_join2, 0));
+        return MCS_OK;
+    }
+    {
+        const int rc = stream_launch(nullptr, n_tiles);
+        if (rc) return rc;
     }
     if (p->n_fallback > 0) HIP_TRY(A->hipStreamWaitEvent(s, p->ev_join, 0));
     if (mb) HIP_TRY(A->hipStreamWaitEvent(s, p->ev_join2, 0));
@@ -716,6 +781,7 @@ int ensure_side(const Api *A, mcs_plan *p)
     }
     if (mb && !p->side2) {
         HIP_TRY(A->hipEventCreateWithFlags(&p->ev_join2, hipEventDisableTiming));
+        HIP_TRY(A->hipEventCreateWithFlags(&p->ev_early, hipEventDisableTiming));
         HIP_TRY(A->hipStreamCreateWithFlags(&p->side2, hipStreamNonBlocking));
     }
     return MCS_OK;
@@ -1041,6 +1107,7 @@ int mcs_plan_destroy(mcs_plan *p)
             if (p->ev_fork) (void)A->hipEventDestroy(p->ev_fork);
             if (p->ev_join) (void)A->hipEventDestroy(p->ev_join);
             if (p->ev_join2) (void)A->hipEventDestroy(p->ev_join2);
+            if (p->ev_early) (void)A->hipEventDestroy(p->ev_early);
         }
     }
     delete p;

@@ -711,21 +711,24 @@ __device__ __forceinline__ void wait_vmcnt_le(int n)
     }
 }
 
-// grid (8 * ceil(tiles / 8)), block (64, 8).  XCD-aware tile order: workgroups are dealt
-// round-robin over the 8 XCDs (b % 8 share one), so XCD x gets the contiguous band of tiles
-// [x * per, (x+1) * per), walked row-major; vertically adjacent tiles, whose footprints overlap
+// grid (8 * ceil(n_order / 8)), block (64, 8); the launch streams tiles order[0, n_order) (or
+// tiles 0 .. n_order - 1).  XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs
+// (b % 8 share one), so XCD x gets the contiguous band of list entries [x * per, (x+1) * per),
+// walked in list (row-major) order; vertically adjacent tiles, whose footprints overlap
 // by a few source rows, then run at about the same time on the same L2.  (Placement affects
 // speed only.)
 template <int CN, bool BUF>
 __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *tiles,
-                                            const uint32_t *desc, int n_frames, uint8_t *smem)
+                                            const uint32_t *desc, int n_frames, const int *order,
+                                            int n_order, uint8_t *smem)
 {
     const int lane = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(threadIdx.y);
     const int tid = wave * kWave + lane;
-    const int gx = (P.out_w + kTileW - 1) / kTileW, gy = (P.out_h + kTileH - 1) / kTileH;
-    const int n_tiles = gx * gy, per = (n_tiles + 7) >> 3;
-    const int tile = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
-    if (tile >= n_tiles) return;
+    const int gx = (P.out_w + kTileW - 1) / kTileW;
+    const int per = (n_order + 7) >> 3;
+    const int idx = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+    if (idx >= n_order) return;
+    const int tile = order ? __builtin_amdgcn_readfirstlane(order[idx]) : idx;
     const int bx = tile % gx, by = tile / gx;
     // the tile header, copied once into LDS (the kernel also stores to global memory, so the
     // compiler cannot serve `tiles` from the scalar cache)
@@ -954,10 +957,11 @@ __device__ __forceinline__ void resize_px(const KResizeArgs &a)
 #endif
 #define MCS_STREAM_ENTRY(CN, SUF, BUF)                                                         \
     extern "C" __global__ __launch_bounds__(512) MCS_STREAM_ATTR void mcs_stream_c##CN##SUF(   \
-        const mcs::KParams P, const mcs::TileHdr *tiles, const uint32_t *desc, int n_frames)  \
+        const mcs::KParams P, const mcs::TileHdr *tiles, const uint32_t *desc, int n_frames,  \
+        const int *order, int n_order)                                                         \
     {                                                                                          \
         extern __shared__ __attribute__((aligned(16))) uint8_t smem[];                         \
-        mcs::stream_tile<CN, BUF>(P, tiles, desc, n_frames, smem);                             \
+        mcs::stream_tile<CN, BUF>(P, tiles, desc, n_frames, order, n_order, smem);             \
     }
 #define MCS_DIRECT_ENTRY(CN, IN, O32)                                                          \
     extern "C" __global__ __launch_bounds__(512) void mcs_direct_c##CN##_i##IN##_o##O32(       \

@@ -110,6 +110,9 @@ struct KStreamArgs {
     const uint32_t *desc;
     int n_frames;
     int pad_;
+    const int *order;              // tiles to stream (NULL: all, in grid order)
+    int n_order;                   // tiles in this launch
+    int pad2_;
 };
 struct KDirectArgs {
     KParams P;

@@ -1,0 +1,15 @@
+# multi-band launch split (streaming tiles under mixed pixels first, blend beside the rest):
+# parity of the blend / stream paths, then C2 and C4 bench lines with MCS_MB_SPLIT=1 / 0 alternating
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+timeout -k 10 500 python -u -m pytest tests/test_gpu_blend.py tests/test_gpu_cylinder.py tests/test_gpu_parity.py tests/test_gpu_stream.py tests/test_gpu_ingest.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_split.log 2>&1 || { tail -30 gpurun_out/pytest_split.log; exit 1; }
+tail -1 gpurun_out/pytest_split.log
+for i in 1 2; do
+  for v in 1 0; do
+    for r in chain cylinder; do
+      MCS_MB_SPLIT=$v timeout -k 10 200 python bench.py --rig $r --no-cpu-baseline > gpurun_out/split_$v.log 2>&1 || { tail -20 gpurun_out/split_$v.log; exit 1; }
+      tail -1 gpurun_out/split_$v.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$r SPLIT=$v', d['value'], 'launch', d['kernels']['launch_ms'])"
+    done
+  done
+done
