@@ -27,6 +27,8 @@ namespace rt {
       (void *, size_t, const void *, size_t, size_t, size_t, hipMemcpyKind, hipStream_t))      \
     X(hipMemsetAsync, hipError_t, (void *, int, size_t, hipStream_t))                         \
     X(hipStreamCreateWithFlags, hipError_t, (hipStream_t *, unsigned int))                    \
+    X(hipStreamCreateWithPriority, hipError_t, (hipStream_t *, unsigned int, int))            \
+    X(hipDeviceGetStreamPriorityRange, hipError_t, (int *, int *))                             \
     X(hipStreamDestroy, hipError_t, (hipStream_t))                                             \
     X(hipStreamSynchronize, hipError_t, (hipStream_t))                                         \
     X(hipEventCreate, hipError_t, (hipEvent_t *))                                              \
