@@ -72,22 +72,24 @@ def derived(avg):
     return res
 
 
-def main(prefixes=("mcs_stream_c3",), workload=None, out=None):
-    """Launches = the dispatches of the first family (one per stitch launch; the PMC runs use
-    bench.py --no-paste-ref so only the measured plan dispatches); HBM bytes per launch = every
-    family's FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE over its dispatches, / launches."""
+def main(prefixes=("mcs_stream_c3",), workload=None, out=None, launches=None):
+    """Launches = the bench launches of each counter pass (tools/gpu_pmc.sh: --steps 3 --warmup 1
+    = 4, $MCS_PMC_LAUNCHES overrides; the PMC runs use bench.py --no-paste-ref so only the
+    measured plan dispatches, and a multi-band launch streams its tiles in two dispatches); HBM
+    bytes per launch = every family's FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE over its
+    dispatches, / launches."""
+    if launches is None:
+        launches = int(os.environ.get("MCS_PMC_LAUNCHES", "4"))
     sys.path.insert(0, ROOT)
     from multicamera_stitching_amd import _capi
     # the kernels these counters belong to: bench.py reports "traffic" only for this build
     res = {"kernels": list(prefixes), "workload": workload, "build_id": _capi.build_id(),
            "per_kernel": {}}
     total = 0
-    launches = None
+    res["launches_per_pass"] = launches
     for pre in prefixes:
         avg = family_counters(pre)
         tot, n = family_counters(pre, totals=True)
-        if launches is None:
-            launches = max(n, 1)
         d = derived(avg)
         d["counters_per_dispatch"] = avg
         d["dispatches_per_launch"] = n / launches
