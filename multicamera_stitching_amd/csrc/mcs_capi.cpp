@@ -100,7 +100,7 @@ struct Kernels {
     hipFunction_t mb_prep[5][2] = {};     // [channels][interp]
     hipFunction_t mb_levels[5] = {};      // [channels]
     hipFunction_t mb_blend[5][3] = {};    // [channels][<= 2 owners, <= 4, <= 8]
-    hipFunction_t mb_bands[5][2] = {};    // [channels][reaches the bottom / right edge]
+    hipFunction_t mb_bands[5][3] = {};    // [channels][interior, bottom / right edge, both]
     hipFunction_t mb_bdesc[5][2] = {};    // [channels][interp]
 };
 Kernels g_k[kMaxDevices];
@@ -131,6 +131,8 @@ int kernels(const Api *A, int device, const Kernels **out)
             if (rc == MCS_OK) rc = fn(name, &k.mb_bands[c][0]);
             snprintf(name, sizeof(name), "mcs_mb_bands_br_c%d", c);
             if (rc == MCS_OK) rc = fn(name, &k.mb_bands[c][1]);
+            snprintf(name, sizeof(name), "mcs_mb_bands_all_c%d", c);
+            if (rc == MCS_OK) rc = fn(name, &k.mb_bands[c][2]);
             snprintf(name, sizeof(name), "mcs_mb_blend_c%d_s2", c);
             if (rc == MCS_OK) rc = fn(name, &k.mb_blend[c][0]);
             snprintf(name, sizeof(name), "mcs_mb_blend_c%d_s4", c);
@@ -278,6 +280,8 @@ void band_args(const mcs_plan *p, const mcs::KParams &P, mcs::KMbBandArgs &a)
     a.nf = 0;
     a.gxb = p->gxb;
     a.band0 = 0;
+    a.n_in = p->n_bands_in;
+    a.pad_ = 0;
 }
 
 // The band pass of a multi-band plan (after mb_prep): per (owner slot, blend-tile row) the
@@ -620,6 +624,14 @@ int launch_mb_levels(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KMb
         b.f0 = f0;
         b.nf = nf;
         const unsigned gy = (unsigned)((nf + mcs::kMbBandFrames - 1) / mcs::kMbBandFrames);
+        // interior and edge bands in ONE launch (blocks below n_in interior): the edge bands run
+        // beside the interior ones instead of after them.  MCS_MB_BANDS_FUSED=0 (experiments):
+        // two launches.
+        static const bool fused =
+            !getenv("MCS_MB_BANDS_FUSED") || strcmp(getenv("MCS_MB_BANDS_FUSED"), "0") != 0;
+        if (fused && p->n_bands_in > 0 && p->n_bands > p->n_bands_in)
+            return launch_args(A, k->mb_bands[p->fd.channels][2], (unsigned)p->n_bands, gy,
+                               mcs::kMbBandLanes, 1, &b, sizeof(b), s);
         int rc = MCS_OK;
         if (p->n_bands_in > 0)
             rc = launch_args(A, k->mb_bands[p->fd.channels][0], (unsigned)p->n_bands_in, gy,

@@ -1047,6 +1047,12 @@ extern "C" __global__ __launch_bounds__(256) void mcs_blend_classify(const mcs::
     {                                                                                          \
         mcs::mb_bands<CN, mcs::kMbBandFrames, true>(a);                                        \
     }                                                                                          \
+    extern "C" __global__ __launch_bounds__(64) void mcs_mb_bands_all_c##CN(                   \
+        const mcs::KMbBandArgs a)                                                              \
+    {                                                                                          \
+        if ((int)blockIdx.x < a.n_in) mcs::mb_bands<CN, mcs::kMbBandFrames, false>(a);         \
+        else mcs::mb_bands<CN, mcs::kMbBandFrames, true>(a);                                   \
+    }                                                                                          \
     extern "C" __global__ __launch_bounds__(MCS_MB_BL_THREADS) MCS_MB_BL_ATTR void             \
         mcs_mb_blend_c##CN##_s2(                                                               \
         const mcs::KMbArgs a)                                                                  \

@@ -247,6 +247,8 @@ struct KMbBandArgs {
     int slots, chunk, f0, nf;
     int gxb;                       // blend tiles per mosaic row
     int band0;                     // first band of this launch
+    int n_in;                      // mcs_mb_bands_all: blocks below n_in take the interior path
+    int pad_;
 };
 struct KBlendArgs {
     KParams P;
