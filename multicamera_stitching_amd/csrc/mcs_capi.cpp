@@ -707,7 +707,7 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
     args.pad_ = 0;
     args.pad2_ = 0;
     // 1-D grid dealt over the 8 XCDs; the kernel maps block -> tile (XCD-contiguous bands)
-    auto stream_launch = [&](const int *order, int n_tiles) -> int {
+    auto stream_launch = [&](const int *order, int n_tiles, unsigned lds) -> int {
         args.order = order;
         args.n_order = n_tiles;
         size_t sz = sizeof(args);
@@ -716,12 +716,17 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
         const unsigned grid = 8u * (((unsigned)n_tiles + 7u) / 8u);
         HIP_TRY(A->hipModuleLaunchKernel(k->stream[p->fd.channels][b32 ? 1 : 0], grid, 1, 1,
                                          mcs::kWave, mcs::kWavesPerBlock, 1,
-                                         mcs::lds_stream_bytes(p->fd.channels), s, nullptr, cfg));
+                                         lds, s, nullptr, cfg));
         return MCS_OK;
     };
+    const unsigned lds = (unsigned)mcs::lds_stream_bytes(p->fd.channels);
+    // MCS_STREAM_LDS_LATE (experiments): LDS reserved per block of the late streaming launch, to
+    // leave room on each CU for the multi-band kernels beside it
+    static const unsigned lds_late =
+        getenv("MCS_STREAM_LDS_LATE") ? (unsigned)atoi(getenv("MCS_STREAM_LDS_LATE")) : 0u;
     const int n_tiles = p->gx * p->gy;
     if (split) {
-        int rc = stream_launch(p->d_order, p->n_early);
+        int rc = stream_launch(p->d_order, p->n_early, lds);
         if (rc) return rc;
         HIP_TRY(A->hipEventRecord(p->ev_early, s));
         HIP_TRY(A->hipStreamWaitEvent(p->side2, p->ev_early, 0));
@@ -734,7 +739,8 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
         if (rc) return rc;
         HIP_TRY(A->hipEventRecord(p->ev_join2, p->side2));
         if (n_tiles > p->n_early) {
-            rc = stream_launch(p->d_order + p->n_early, n_tiles - p->n_early);
+            rc = stream_launch(p->d_order + p->n_early, n_tiles - p->n_early,
+                               std::max(lds, lds_late));
             if (rc) return rc;
         }
         if (p->n_fallback > 0) HIP_TRY(A->hipStreamWaitEvent(s, p->ev_join, 0));
@@ -742,7 +748,7 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
         return MCS_OK;
     }
     {
-        const int rc = stream_launch(nullptr, n_tiles);
+        const int rc = stream_launch(nullptr, n_tiles, lds);
         if (rc) return rc;
     }
     if (p->n_fallback > 0) HIP_TRY(A->hipStreamWaitEvent(s, p->ev_join, 0));
