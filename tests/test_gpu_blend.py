@@ -72,6 +72,30 @@ def test_multiband_c2_full_size_batch():
         assert _diff(got[f].reshape(want.shape), want) == 0
 
 
+@pytest.mark.parametrize("F", [64, 70])
+def test_multiband_batch_split_and_chunked(F):
+    """A multi-band device batch of F captures: F <= 64 takes the split launch (streaming tiles
+    under mixed pixels first, the blend beside the rest), F > 64 the chunked launch (levels +
+    blend per 64-capture chunk of the scratch after the streaming kernel) -- every capture equal
+    to the restatement."""
+    import torch
+    plan, cams = _world_plan(3, 160, 140, 3, seed=12)   # (>= 128 px: the band pass)
+    plan.set_blend(MODES["multiband"])
+    shots = [[np.roll(c, 3 * f, axis=1) for c in cams] for f in range(F)]
+    dev = [torch.from_numpy(np.stack([shots[f][i] for f in range(F)])).cuda()
+           for i in range(len(cams))]
+    pitch = (plan.out_w * 3 + 63) // 64 * 64
+    out = torch.zeros((F, plan.out_h, pitch), dtype=torch.uint8, device="cuda")
+    plan.stitch_device([d.data_ptr() for d in dev], [d[0].numel() for d in dev],
+                       out.data_ptr(), pitch, out[0].numel(), F, 0)
+    torch.cuda.synchronize()
+    got = out[:, :, :plan.out_w * 3].cpu().numpy()
+    assert plan.stats()["blend_tiles"] > 0
+    for f in (0, 1, F // 2, F - 2, F - 1):
+        want = oracle.blend_stitch(plan.describe(), shots[f], MODES["multiband"])
+        assert _diff(got[f].reshape(want.shape), want) == 0, f
+
+
 def test_blend_mode_switch_back_to_paste():
     plan, cams = _world_plan(3, 120, 80, 3, seed=9)
     paste = plan.stitch_host(cams)
