@@ -607,6 +607,9 @@ __device__ __forceinline__ void prepare_tile(const KParams &P, TileHdr *tiles, u
 #ifndef MCS_DMA_AUX
 #define MCS_DMA_AUX 0
 #endif
+#ifndef MCS_DESC_NT
+#define MCS_DESC_NT 0
+#endif
 #ifndef MCS_STORE_NT
 #define MCS_STORE_NT 1
 #endif
@@ -751,7 +754,13 @@ __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *til
             desc + ((int64_t)tile * kTilePx + (int64_t)tid * kPx) * kDescWords);
 #pragma unroll
         for (int i = 0; i < kPx * kDescWords / 4; i++) {
+#if MCS_DESC_NT
+            typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+            const v4u t = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(s4) + i);
+            const uint4 v = make_uint4(t.x, t.y, t.z, t.w);
+#else
             const uint4 v = s4[i];
+#endif
             d[4 * i] = v.x;
             d[4 * i + 1] = v.y;
             d[4 * i + 2] = v.z;
