@@ -201,7 +201,7 @@ def main():
 
     mpix_per_launch = F * out_w * out_h / 1e6
     value = shard.job_rate(mpix_per_launch, args.steps, elapsed, world)
-    frame0 = d_out[0, :, :out_w * C].reshape(out_h, out_w, C).cpu().numpy() if rank == 0 else None
+    frame0 = d_out[0, :, :out_w * C].reshape(out_h, out_w, C).cpu().numpy()
 
     # the same launch with the reference's paste (cylinder: the hard seam) and no blend pass:
     # the blend's share of the time
@@ -250,13 +250,21 @@ def main():
     except (OSError, ValueError):
         pass
 
+    # parity on EVERY rank (outside the timed region): this rank's capture 0 (read back above,
+    # before the paste-only launch reuses d_out) against the CPU restatement fed the same camera
+    # frames; the line reports the max over ranks
+    runner = oracle_runner(st, args, interp, plan, blend, (rig_cams, geo) if cyl else None)
+    host = host_cpus()
+    shift = [(rank * F) % c.shape[0] for c in cams]
+    max_abs = check_frame0(runner, [np.roll(c, s, axis=0) for c, s in zip(cams, shift)], frame0,
+                           max(1, host["usable"] // world))
+    max_abs = shard.max_abs_over_ranks(max_abs, device=dev)
+
     result = None
     if rank == 0:
         cpu = None
-        max_abs = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu, max_abs = cpu_baseline(st, cams, frame0, args, interp, out_w, out_h, plan, blend,
-                                        (rig_cams, geo) if cyl else None)
+            cpu = cpu_baseline(runner, cams, args, out_w, out_h, host)
         result = {
             "metric": ("stitched MPix/sec (8-cam 360 cylindrical rig)" if cyl else
                        "stitched MPix/sec (4-cam 1080p rig)"),
@@ -379,6 +387,11 @@ def stub_main(args, world, rank):
     elapsed = shard.timed_loop(step, args.steps, args.warmup, lambda: None)
     mine = elapsed
     elapsed = shard.max_over_ranks([elapsed], device=dev)[0]
+    # every rank checks its own output against an independent restatement (numpy), max over
+    # ranks -- the same reduction as the GPU path's per-rank oracle check
+    want = np.roll(src.numpy(), rank + 1)
+    max_abs = int(np.abs(d_out.view(-1).numpy().astype(np.int16) - want.astype(np.int16)).max())
+    max_abs = shard.max_abs_over_ranks(max_abs, device=dev)
     mpix = F * out_w * out_h / 1e6
     gather = None
     if world > 1 and args.gather != "none":
@@ -393,7 +406,7 @@ def stub_main(args, world, rank):
                   "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
                   "rank0_seconds": mine, "max_seconds": elapsed,
                   "mpix_per_step_per_rank": mpix, "higher_is_better": True, "scaling": "weak",
-                  "gather": gather, "config": {"workload": "stub"}}
+                  "max_abs_diff": max_abs, "gather": gather, "config": {"workload": "stub"}}
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.barrier()
@@ -414,53 +427,154 @@ def describe_workload(args, cyl):
             f"homographies, {args.interp} warpPerspective + {what}")
 
 
-def cpu_baseline(st, cams, frame0, args, interp, out_w, out_h, plan, blend, cyl=None):
-    """The same workload on host cores (oracle/, C restatement), bounded sample.  Paste: the
-    reference-structured cascade (per-stage warp into full canvases + paste, StitcherClass.py);
-    blend modes: the flattened restatement of the blend (orc_blend.c)."""
+def host_cpus() -> dict:
+    """The host's CPUs as this process sees them: nproc (every CPU of the machine), the affinity
+    set, the cgroup quota, and `usable` = the cores this process may actually run on at once
+    (the CPU baseline's thread count), plus the lscpu model name."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = nproc
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(period)
+    except (OSError, ValueError):
+        pass
+    usable = aff if quota is None else max(1, min(aff, int(quota + 0.5)))
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.lower().startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"nproc": nproc, "affinity": aff, "cgroup_quota_cpus": quota, "usable": usable,
+            "model": model}
+
+
+def oracle_runner(st, args, interp, plan, blend, cyl=None):
+    """The workload's CPU restatement (oracle/, test infrastructure) as run(cams) -> mosaic, plus
+    the reference-structured cascade (paste only) and the flattened gather, for the baseline.
+    Returns {"workload": (run, what), "cascade": ..., "flat": ...} (None where not defined)."""
     from oracle import oracle
-    threads = min(16, os.cpu_count() or 1)
-    oracle.set_threads(threads)
-    if blend == 0:
+    out = {"cascade": None, "flat": None}
+    if st is not None:
         stages = [dict(H=np.asarray(sb.cachedAH), canvas_w=sb.ABSize[0], canvas_h=sb.ABSize[1],
                        bx=sb.Bpts[0][0], by=sb.Bpts[0][1], super_mode=sb.super_mode,
                        x_limits=sb.x_limits, y_limits=sb.y_limits) for sb in st.stitchers]
-
-        def run():
-            return oracle.cascade_stitch(stages, cams, interp)
-        what = "cascaded per-stage warpPerspective+paste"
+        out["cascade"] = (lambda cams: oracle.cascade_stitch(stages, cams, interp),
+                          "reference-structured cascade: per-stage warpPerspective into the full "
+                          "stage canvas + overwrite paste + crop (StitcherClass.py:114-136,"
+                          "211-256), mcs_oracle.c")
+    if blend == 0:
+        out["workload"] = out["cascade"]
+        if st is not None:
+            flat = plan.describe()
+            out["flat"] = (lambda cams: oracle.flat_stitch(flat, cams, interp),
+                           "flattened single-pass gather (mcs_oracle.c orc_flat_stitch)")
     elif cyl is not None:
         rig_cams, g = cyl
-
-        def run():
-            return oracle.blend_stitch_cyl(rig_cams, g["out_w"], g["out_h"], g["f_cyl"], g["u0"],
-                                           g["v0"], cams, blend, interp)
-        what = ({1: "feather", 2: "3-level multi-band", 3: "seam"}[blend] +
-                " cylindrical panorama (orc_blend.c)")
+        out["workload"] = (
+            lambda cams: oracle.blend_stitch_cyl(rig_cams, g["out_w"], g["out_h"], g["f_cyl"],
+                                                 g["u0"], g["v0"], cams, blend, interp),
+            {1: "feather", 2: "3-level multi-band", 3: "seam"}[blend] +
+            " cylindrical panorama (orc_blend.c)")
     else:
         flat = plan.describe()
+        out["workload"] = (lambda cams: oracle.blend_stitch(flat, cams, blend, interp),
+                           {1: "feather", 2: "3-level multi-band", 3: "seam"}[blend] +
+                           " blend (orc_blend.c)")
+    return out
 
-        def run():
-            return oracle.blend_stitch(flat, cams, blend, interp)
-        what = {1: "feather", 2: "3-level multi-band", 3: "seam"}[blend] + " blend (orc_blend.c)"
-    want = run()
-    max_abs = int(np.abs(want.astype(np.int16) - frame0.astype(np.int16)).max())
+
+def check_frame0(runner, cams, frame0, threads) -> int:
+    """max |GPU - CPU restatement| over one capture (the portable, test-pinned oracle build)."""
+    from oracle import oracle
+    oracle.set_threads(threads)
+    want = runner["workload"][0](cams)
+    return int(np.abs(want.astype(np.int16) - frame0.astype(np.int16)).max())
+
+
+def _time_line(run, cams, threads, seconds, mpix, what, max_n=5000):
+    from oracle import oracle
+    oracle.set_threads(threads)
     n = 0
     t0 = time.perf_counter()
     while True:
-        run()
+        run(cams)
         n += 1
         dt = time.perf_counter() - t0
-        if dt >= args.cpu_seconds or n >= 5000:
+        if dt >= seconds or n >= max_n:
             break
+    return {"what": what, "threads": threads, "value": round(n * mpix / dt, 3), "unit": "MPix/s",
+            "captures": n, "seconds": round(dt, 2)}
+
+
+def cpu_baseline(runner, cams, args, out_w, out_h, host):
+    """The same workload on the GPU box's own host cores (oracle/, C restatement):
+    built -O3 -march=native here (the portable build if that fails), a bounded sample per line:
+    the workload at every usable core (the headline) and at 1 thread, the reference-structured
+    cascade (paste) at every usable core and at 1 thread, and the flattened gather."""
+    import tempfile
+    from oracle import oracle
+    mpix = out_w * out_h / 1e6
+    build = "-O3 -march=native"
+    path = None
+    try:
+        path = oracle.build_native(os.path.join(tempfile.mkdtemp(prefix="mcs_orc_"),
+                                                "liboracle_native.so"))
+    except Exception as e:   # (a missing compiler on the host: the portable build, said so)
+        build = f"-O3 -march=x86-64-v2 (native build failed: {type(e).__name__})"
+    n_all = host["usable"]
+    sec = args.cpu_seconds
+    lines = []
+    ctx = oracle.library(path) if path else _null_ctx()
+    with ctx:
+        run, what = runner["workload"]
+        native_exact = None
+        if path:
+            want = runner["workload"][0](cams)
+            with oracle.library(os.path.join(os.path.dirname(oracle.__file__), "liboracle.so")):
+                native_exact = bool(np.array_equal(want, run(cams)))
+        head = _time_line(run, cams, n_all, sec, mpix, what)
+        lines.append(head)
+        lines.append(_time_line(run, cams, 1, sec / 2, mpix, what))
+        if runner["cascade"] is not None and runner["cascade"] is not runner["workload"]:
+            lines.append(_time_line(*runner["cascade"][:1], cams, n_all, sec / 2, mpix,
+                                    runner["cascade"][1]))
+            lines.append(_time_line(*runner["cascade"][:1], cams, 1, sec / 2, mpix,
+                                    runner["cascade"][1]))
+        elif runner["cascade"] is not None:
+            lines.append(_time_line(*runner["cascade"][:1], cams, 1, sec / 2, mpix,
+                                    runner["cascade"][1]))
+        if runner["flat"] is not None:
+            lines.append(_time_line(*runner["flat"][:1], cams, n_all, sec / 2, mpix,
+                                    runner["flat"][1]))
     return {
-        "value": round(n * out_w * out_h / 1e6 / dt, 3),
+        "value": head["value"],
         "unit": "MPix/s",
-        "cores": threads,
+        "cores": n_all,
         "kind": "port",
-        "sample": f"{n} captures of the same rig through the {what} C restatement, "
-                  f"{dt:.1f} s, OpenMP {threads} threads",
-    }, max_abs
+        "sample": f"{head['captures']} captures of the same rig through the {what} C "
+                  f"restatement, {head['seconds']} s, OpenMP {n_all} threads "
+                  f"(every core this process may use), built {build}",
+        "build": build,
+        "native_equals_portable": native_exact,
+        "host": host,
+        "lines": lines,
+    }
+
+
+class _null_ctx:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *exc):
+        return False
 
 
 if __name__ == "__main__":

@@ -153,16 +153,18 @@ int mcs_plan_describe(const mcs_plan *plan, mcs_flat_desc *out);
  * call it on first use.  stream: hipStream_t or NULL for the plan's own stream. */
 int mcs_plan_prepare(mcs_plan *plan, void *stream);
 
-/* stats[0..7] = prepared, tiles, tiles on the LDS path, tiles on the direct path, table bytes,
- * blend mode, 32-px tiles the blend kernels recompute per frame, the most owners any multi-band
- * tile blends (<= 8; more in one 64 x 64 neighbourhood fails with MCS_E_UNSUPPORTED). */
+/* stats[0..8] = prepared, tiles, tiles on the LDS path, tiles on the direct path, table bytes,
+ * blend mode, 32 x 64 tiles the blend kernels recompute per frame, the most owners any
+ * multi-band tile blends (<= 8), multi-band tiles degraded to the feather rule (their
+ * neighbourhood -- the tile grown by 16 px -- holds more than 8 owners). */
 int mcs_plan_stats(const mcs_plan *plan, int64_t *stats, int n);
 
 /* Blend mode of the plan (MCS_BLEND_*; default NONE = the reference's paste).  Changing it drops
  * the prepared tables (rebuilt by mcs_plan_prepare or the next stitch).  FEATHER / MULTIBAND
- * replace the reference's paste with the blends of SURVEY.md 8 NS-2 / NS-1; MULTIBAND supports
- * up to 4 cameras meeting within 16 px (else MCS_E_UNSUPPORTED at prepare).  Cylindrical plans
- * refuse NONE. */
+ * replace the reference's paste with the blends of SURVEY.md 8 NS-2 / NS-1.  MULTIBAND blends up
+ * to 8 owners per 32 x 64 tile neighbourhood (the tile grown by 16 px); a tile with more takes
+ * the FEATHER rule instead, on the GPU (counted in mcs_plan_stats[8]; oracle/orc_blend.c "dense
+ * seams").  Cylindrical plans refuse NONE. */
 int mcs_plan_set_blend(mcs_plan *plan, int mode);
 
 /* Seams.  MCS_SEAM_DISTANCE: the owner is the covering camera farthest from

@@ -218,7 +218,7 @@ class Stitcher(_Transient, Debugger):
         cams = [images_dic[label] for label in self.img_labels]
         if all(sb.cachedAH is None for sb in self.stitchers):
             return cams[0]   # every stage returns its B unchanged (:255-256)
-        return _run_chain(self, self.stitchers, cams)
+        return _run_chain(self, self.stitchers, cams, images_dic[self.img_labels[-1]])
 
     # ------------------------------------------------------------------ persistence
     def save_stitcher(self, save_path):
@@ -298,7 +298,7 @@ class StitcherBase(_Transient, Debugger):
             return imageB
         if draw_descriptors:
             _warn_draw(self)
-        return _run_chain(self, [self], [imageB, imageA])
+        return _run_chain(self, [self], [imageB, imageA], imageB)
 
     def calibrate(self, images, ratio=0.75, reprojThresh=4.0, xoffset=10, yoffset=10,
                   homography=None, use_features=True):
@@ -431,12 +431,32 @@ def _conform_cameras(owner, chain, cams):
     return cams, cam0_hw, sizes
 
 
-def _run_chain(owner, chain, cams):
+def _run_chain(owner, chain, cams, fallback):
+    """One GPU stitch of the chain.  The reference never raises on an expected failure: it logs
+    and returns a fallback image (:126-128 the last camera's image, :255-256 B).  A failure of
+    the GPU path (a C-ABI status, e.g. a device allocation that fails) is logged the same way and
+    `fallback` is returned -- the caller's thread (Qt GUI / worker) gets an image, never an
+    exception, and the log says why.  (There is no CPU stitch behind it: a missing libmcs.so
+    fails at import.)"""
     cams, cam0_hw, sizes = _conform_cameras(owner, chain, cams)
     cache = owner._cache()
     with cache.lock:
-        plan = _get_plan(owner, chain, cam0_hw, _channels(cams[0]))
-        return plan.stitch_host(cams, sizes)
+        try:
+            plan = _get_plan(owner, chain, cam0_hw, _channels(cams[0]))
+            out = plan.stitch_host(cams, sizes)
+            if not getattr(plan, "_dense_logged", False):
+                plan._dense_logged = True
+                dense = plan.stats().get("mb_degraded_tiles", 0)
+                if dense:
+                    owner.debugger(DEBUG_LEVEL_0, "[STITCHER] multi-band: {} tiles have more than "
+                                   "8 cameras meeting within 16 px; they take the feather "
+                                   "blend".format(dense), log_type="warn")
+            return out
+        except _capi.McsError as e:
+            cache.key = cache.plan = None     # rebuilt on the next call
+            owner.debugger(DEBUG_LEVEL_0, "[STITCHER] GPU stitch failed ({}); returning the "
+                           "fallback image".format(e), log_type="err")
+            return fallback
 
 
 def _stage_out_shape(sb, imageB):

@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import hashlib
 import os
+import struct
 import subprocess
 import sys
 
@@ -48,6 +49,42 @@ HOST_FLAGS = [
 ]
 
 
+def _elf_sections(path: str) -> dict:
+    """{name: bytes} of an ELF64 little-endian file's sections (NOBITS sections: b"")."""
+    with open(path, "rb") as f:
+        b = f.read()
+    if b[:4] != b"\x7fELF" or b[4] != 2 or b[5] != 1:
+        raise ValueError(f"{path}: not an ELF64 little-endian object")
+    shoff, = struct.unpack_from("<Q", b, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", b, 0x3A)
+    hdrs = [struct.unpack_from("<IIQQQQIIQQ", b, shoff + i * shentsize) for i in range(shnum)]
+    names = hdrs[shstrndx]
+    strtab = b[names[4]:names[4] + names[5]]
+    out = {}
+    for h in hdrs:
+        name = strtab[h[0]:strtab.index(b"\0", h[0])].decode()
+        out[name] = b"" if h[1] == 8 else b[h[4]:h[4] + h[5]]
+    return out
+
+
+# The sections that define what runs: machine code, kernel descriptors (.rodata) and the kernel
+# metadata note (names, argument layout, register and LDS counts).  The symbol/string tables are
+# left out: they carry names derived from the output path, so a rebuild of the same sources at
+# another path keeps its id.
+CODE_SECTIONS = (".text", ".rodata", ".note")
+
+
+def code_id(paths) -> str:
+    """16-hex build id of code objects, from their code sections only (see CODE_SECTIONS)."""
+    digest = hashlib.sha256()
+    for p in paths:
+        secs = _elf_sections(p)
+        for name in CODE_SECTIONS:
+            data = secs.get(name, b"")
+            digest.update(name.encode() + struct.pack("<Q", len(data)) + data)
+    return digest.hexdigest()[:16]
+
+
 def _stale() -> bool:
     if not (os.path.exists(LIB) and os.path.exists(HSACO)):
         return True
@@ -80,11 +117,7 @@ def _build_to(LIB: str, HSACO: str, defines, verbose: bool) -> str:
               os.path.join(CSRC, src)], verbose)
         os.replace(out + ".tmp", out)
         objs[name] = out
-    digest = hashlib.sha256()
-    for name in sorted(objs):
-        with open(objs[name], "rb") as f:
-            digest.update(f.read())
-    build_id = digest.hexdigest()[:16]
+    build_id = code_id([objs[name] for name in sorted(objs)])
     blob = LIB + ".blob.S"
     with open(blob, "w") as f:
         f.write("    .section .rodata\n")

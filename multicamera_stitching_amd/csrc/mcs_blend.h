@@ -189,12 +189,16 @@ __device__ __forceinline__ void blend_owner_tile(const KParams &P, uint8_t *owne
 }
 
 // grid (tiles), block 256: appends (tile, slot mask) to list[1 + 2i] for the tiles the mode
-// recomputes; list[0] = count.  multiband: the owners in the tile's 64 x 64 neighbourhood
-// (clipped to the mosaic: reflected positions land inside it), when there are two or more;
-// more than kBlendSlots owners in one neighbourhood is counted in overflow[0] (prepare fails);
-// overflow[1] = the most owners any listed tile has.
+// recomputes; list[0] = count.  multiband: the owners in the tile's neighbourhood (the tile grown
+// by kBlendHalo, clipped to the mosaic: reflected positions land inside it), when there are two
+// or more.  A neighbourhood with more than kBlendSlots owners (more than the blend kernels hold)
+// degrades its tile to the feather rule (orc_blend.c "dense seams"): the tile goes to list2 with
+// its feather slot set (none when no pixel has two cameras at positive distance: the owner
+// sample the streaming kernel writes IS the feather value there), counted in overflow[0];
+// overflow[1] = the most owners any multi-band-listed tile has.
 __device__ __forceinline__ void blend_classify(const KParams &P, int mode, const uint8_t *owner,
-                                               const uint32_t *info, int *list, int *overflow)
+                                               const uint32_t *info, int *list, int *overflow,
+                                               int *list2)
 {
     __shared__ uint32_t s_mask;
     const int gx = (P.out_w + kBlendTileW - 1) / kBlendTileW;
@@ -220,8 +224,17 @@ __device__ __forceinline__ void blend_classify(const KParams &P, int mode, const
         mask = s_mask;
         if (__popc(mask) < 2) mask = 0;
     }
+    if (threadIdx.x == 0 && mode == MCS_BLEND_MULTIBAND && __popc(mask) > kBlendSlots) {
+        atomicAdd(overflow, 1);
+        const uint32_t fea = info[2 * t + 1];
+        if (fea) {
+            const int i = atomicAdd(&list2[0], 1);
+            list2[1 + 2 * i] = t;
+            list2[2 + 2 * i] = (int)fea;
+        }
+        return;
+    }
     if (threadIdx.x == 0 && mask) {
-        if (mode == MCS_BLEND_MULTIBAND && __popc(mask) > kBlendSlots) atomicAdd(overflow, 1);
         atomicMax(overflow + 1, __popc(mask));
         const int i = atomicAdd(&list[0], 1);
         list[1 + 2 * i] = t;

@@ -46,6 +46,10 @@ struct mcs_plan {
     // blended modes (mcs_plan_set_blend): owner map, 32-px tile info, per-frame tile list
     int blend = MCS_BLEND_NONE;
     int n_blend = 0, mb_slots = 0;
+    // multi-band: tiles degraded to the feather rule (d_blist + 2 * blend tiles + 3: count, then
+    // (tile, feather mask) pairs)
+    int n_dense = 0, n_degraded = 0;
+    int *d_dense = nullptr;
     uint8_t *d_owner = nullptr;
     uint32_t *d_binfo = nullptr;
     int *d_blist = nullptr;
@@ -484,30 +488,32 @@ int prepare_blend(const Api *A, mcs_plan *p, const Kernels *k, hipStream_t s)
     const size_t nt = (size_t)bx * by;
     HIP_TRY(A->hipMalloc((void **)&p->d_owner, (size_t)W * H));
     HIP_TRY(A->hipMalloc((void **)&p->d_binfo, nt * 2 * sizeof(uint32_t)));
-    HIP_TRY(A->hipMalloc((void **)&p->d_blist, (2 * nt + 3) * sizeof(int)));
-    HIP_TRY(A->hipMemsetAsync(p->d_blist, 0, (2 * nt + 3) * sizeof(int), s));
+    HIP_TRY(A->hipMalloc((void **)&p->d_blist, (4 * nt + 4) * sizeof(int)));
+    HIP_TRY(A->hipMemsetAsync(p->d_blist, 0, (4 * nt + 4) * sizeof(int), s));
     mcs::KBlendPrepArgs a;
     a.P = p->kp;
     a.owner = p->d_owner;
     a.info = p->d_binfo;
     a.list = p->d_blist;
     a.overflow = p->d_blist + 2 * nt + 1;
+    a.list2 = p->d_blist + 2 * nt + 3;
     a.mode = p->blend;
     a.pad_ = 0;
     int rc = launch_args(A, k->blend_owner[p->fd.interp], bx, by, 256, 1, &a, sizeof(a), s);
     if (rc == MCS_OK) rc = launch_args(A, k->blend_classify, (unsigned)nt, 1, 256, 1, &a,
                                        sizeof(a), s);
     if (rc) return rc;
-    int n = 0, tail[2] = {0, 0};
+    int n = 0, tail[3] = {0, 0, 0};
     HIP_TRY(A->hipMemcpyAsync(&n, p->d_blist, sizeof(int), hipMemcpyDeviceToHost, s));
-    HIP_TRY(A->hipMemcpyAsync(tail, p->d_blist + 2 * nt + 1, 2 * sizeof(int),
+    HIP_TRY(A->hipMemcpyAsync(tail, p->d_blist + 2 * nt + 1, 3 * sizeof(int),
                               hipMemcpyDeviceToHost, s));
     HIP_TRY(A->hipStreamSynchronize(s));
-    const int overflow = tail[0];
+    // tail[0]: multi-band tiles with more than kBlendSlots owners (degraded to the feather rule),
+    // tail[2]: those of them with pixels to feather (listed in d_dense)
     p->mb_slots = tail[1];
-    if (overflow)
-        return mcs::fail(MCS_E_UNSUPPORTED, "multi-band: %d tiles have more than %d cameras "
-                         "meeting within %d px", overflow, mcs::kBlendSlots, mcs::kBlendHalo);
+    p->n_degraded = p->blend == MCS_BLEND_MULTIBAND ? tail[0] : 0;
+    p->n_dense = tail[2];
+    p->d_dense = p->d_blist + 2 * nt + 3;
     p->n_blend = n;
     if (p->blend == MCS_BLEND_MULTIBAND && n > 0) return prepare_multiband(A, p, k, s);
     return MCS_OK;
@@ -543,6 +549,8 @@ void release_tables(const Api *A, mcs_plan *p)
     p->d_owner = nullptr;
     p->d_binfo = nullptr;
     p->d_blist = nullptr;
+    p->d_dense = nullptr;
+    p->n_dense = p->n_degraded = 0;
     p->prepared = false;
     p->n_fallback = p->n_blend = 0;
 }
@@ -653,6 +661,22 @@ int launch_mb_levels(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KMb
     return MCS_OK;
 }
 
+// Multi-band tiles degraded to the feather rule (more than kBlendSlots owners in their
+// neighbourhood): the feather kernel over d_dense, on stream s after the mosaic is written.
+int launch_dense(const Api *A, const mcs_plan *p, const Kernels *k, const mcs::KParams &P,
+                 int n_frames, hipStream_t s)
+{
+    if (p->blend != MCS_BLEND_MULTIBAND || p->n_dense <= 0) return MCS_OK;
+    mcs::KBlendArgs b;
+    b.P = P;
+    b.owner = p->d_owner;
+    b.list = p->d_dense;
+    b.n_frames = n_frames;
+    b.pad_ = 0;
+    return launch_args(A, k->feather[p->fd.channels][p->fd.interp], p->n_dense, n_frames, 256, 1,
+                       &b, sizeof(b), s);
+}
+
 // One launch (stream over all tiles, + direct over the fallback tiles, + the blend passes) for
 // n_frames captures that share one frame stride.  Work that does not read the mosaic -- the
 // direct-gather tiles and the first multi-band chunk's level pyramids -- runs on two side streams,
@@ -745,7 +769,7 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
         }
         if (p->n_fallback > 0) HIP_TRY(A->hipStreamWaitEvent(s, p->ev_join, 0));
         HIP_TRY(A->hipStreamWaitEvent(s, p->ev_join2, 0));
-        return MCS_OK;
+        return launch_dense(A, p, k, P, n_frames, s);
     }
     {
         const int rc = stream_launch(nullptr, n_tiles, lds);
@@ -783,7 +807,7 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
         }
         if (rc) return rc;
     }
-    return MCS_OK;
+    return launch_dense(A, p, k, P, n_frames, s);
 }
 
 // Side streams + fork/join events for the direct-gather tiles and the multi-band levels (created
@@ -1111,17 +1135,9 @@ int mcs_plan_destroy(mcs_plan *p)
             if (p->d_out) (void)A->hipFree(p->d_out);
             for (int i = 0; i < MCS_MAX_CAMS; i++)
                 if (p->d_raw[i]) (void)A->hipFree(p->d_raw[i]);
-            if (p->d_tiles) (void)A->hipFree(p->d_tiles);
-            if (p->d_desc) (void)A->hipFree(p->d_desc);
-            if (p->d_fallback) (void)A->hipFree(p->d_fallback);
-            if (p->d_owner) (void)A->hipFree(p->d_owner);
-            if (p->d_binfo) (void)A->hipFree(p->d_binfo);
-            if (p->d_blist) (void)A->hipFree(p->d_blist);
-            if (p->d_mbdesc) (void)A->hipFree(p->d_mbdesc);
-            if (p->d_mbtab) (void)A->hipFree(p->d_mbtab);
-            if (p->d_mbfoot) (void)A->hipFree(p->d_mbfoot);
-            if (p->d_mbg1) (void)A->hipFree(p->d_mbg1);
-            if (p->d_mbg2) (void)A->hipFree(p->d_mbg2);
+            // every prepared table (stream, blend, multi-band, band pass, launch order): one list,
+            // shared with the blend-mode change
+            release_tables(A, p);
             if (p->d_cyl) (void)A->hipFree(p->d_cyl);
             if (p->d_seam) (void)A->hipFree(p->d_seam);
             if (p->d_map) (void)A->hipFree(p->d_map);
@@ -1508,11 +1524,11 @@ int mcs_plan_stats(const mcs_plan *p, int64_t *stats, int n)
 {
     if (!p || !stats) return mcs::fail(MCS_E_INVALID, "NULL plan/stats");
     const int64_t tiles = (int64_t)p->gx * p->gy;
-    const int64_t v[8] = {p->prepared ? 1 : 0, tiles, tiles - p->n_fallback, p->n_fallback,
+    const int64_t v[9] = {p->prepared ? 1 : 0, tiles, tiles - p->n_fallback, p->n_fallback,
                           tiles * (int64_t)(sizeof(mcs::TileHdr) +
                                             mcs::kTilePx * mcs::kDescWords * 4),
-                          p->blend, p->n_blend, p->mb_slots};
-    for (int i = 0; i < n; i++) stats[i] = i < 8 ? v[i] : 0;
+                          p->blend, p->n_blend, p->mb_slots, p->n_degraded};
+    for (int i = 0; i < n; i++) stats[i] = i < 9 ? v[i] : 0;
     return MCS_OK;
 }
 

@@ -132,7 +132,10 @@ extern "C" {
 
 const char *mcs_rccl_library(void)
 {
+    // only a caller with a bound runtime triggers the one-time bind (the search for the librccl
+    // beside the HIP runtime needs it; a failed bind is cached for the life of the process)
     const mcs::rt::Api *A = mcs::rt::api();
+    if (!A) return "";
     (void)rccl(A);
     return g_rccl_name.c_str();
 }

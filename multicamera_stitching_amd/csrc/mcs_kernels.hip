@@ -282,14 +282,15 @@ __device__ __forceinline__ void put_px(OutWords &w, int p, uint32_t v)
 //
 // Every pixel -- bilinear inside the image, bilinear on its border, a paste copy, a nearest
 // sample, or outside everything -- is expressed in ONE form: two row windows of 2*CN bytes
-// (row 0 at off0, row 1 at off1) and 15-bit weights packed as u16 pairs W0 = (w00, w01),
-// W1 = (w10, w11), so that per channel k
-//     out_k = dot2(row1_k, W1, dot2(row0_k, W0, 16384)) >> 15            (v_dot2_u32_u16)
-// which is remapBilinear's sum(p * w) + 2^14 >> 15 exactly.  A copy is W0 = (32768, 0),
-// W1 = 0; a pixel outside every camera has W0 = W1 = 0; taps outside the image get weight 0
-// and their window is moved onto valid bytes (so nothing outside a frame is ever read, see
-// place_window()).  No per-pixel branching remains in the frame loop except the rare
-// "window would end past the frame" case (last pixels of a frame), flagged in `slow`.
+// (row 0 at off0, row 1 at off1) and remapBilinear's 15-bit weights stored DOUBLED as u16 pairs
+// W0 = (w2x(w00), w2x(w01)), W1 = (w2x(w10), w2x(w11)) (w2x above), so that per channel k
+//     s_k = dot2(row1_k, W1, dot2(row0_k, W0, 32768))                    (v_dot2_u32_u16)
+// carries remapBilinear's (sum(p * w) + 2^14) >> 15 exactly in its byte 2 (pack_b2 extracts
+// it).  A copy is W0 = (65535, 0), W1 = 0; a pixel outside every camera has W0 = W1 = 0; taps
+// outside the image get weight 0 and their window is moved onto valid bytes (so nothing outside
+// a frame is ever read, see place_cols()).  No per-pixel branching remains in the frame loop
+// except the rare "window would end past the frame" case (last pixels of a frame), flagged in
+// `shift`.
 template <bool OFF32>
 struct Desc {
     typedef typename std::conditional<OFF32, uint32_t, uint64_t>::type off_t;
@@ -613,6 +614,18 @@ __device__ __forceinline__ void prepare_tile(const KParams &P, TileHdr *tiles, u
 #ifndef MCS_STORE_NT
 #define MCS_STORE_NT 1
 #endif
+// Decomposition knobs (variant builds only, never the product): MCS_EXP_NOCOMPUTE stores a
+// constant instead of reading LDS windows (memory-only time), MCS_EXP_NODMA stages only the
+// first ring of captures (compute + stores), MCS_EXP_NOSTORE skips the mosaic stores.
+#ifndef MCS_EXP_NOCOMPUTE
+#define MCS_EXP_NOCOMPUTE 0
+#endif
+#ifndef MCS_EXP_NODMA
+#define MCS_EXP_NODMA 0
+#endif
+#ifndef MCS_EXP_NOSTORE
+#define MCS_EXP_NOSTORE 0
+#endif
 
 
 // Block-uniform value read from LDS (broadcast read + readfirstlane -> SGPR).
@@ -791,11 +804,18 @@ __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *til
     int slot_f = 0, slot_a = ring - 1;     // slots of capture f and of capture f + ring - 1
     for (int f = 0; f < n_frames; f++) {
         const int ahead = f + ring - 1;
-        const bool full = ahead < n_frames;
+        const bool full = ahead < n_frames && !MCS_EXP_NODMA;
         if (full)
             stage_capture<BUF>(J, rs, ring0 + slot_a * buf_bytes, (int64_t)ahead * fstride, lane);
         const uint8_t *b = ring0 + slot_f * buf_bytes;
-        if (live) {
+        if (live && !MCS_EXP_NOSTORE) {
+#if MCS_EXP_NOCOMPUTE
+            OutWords w;
+            w.w0 = d[0] ^ (uint32_t)f;
+            w.w1 = d[1];
+            w.w2 = d[2];
+            w.w3 = d[3];
+#else
             uint32_t rr[kPx * CN];
 #pragma unroll
             for (int p = 0; p < kPx; p++) {
@@ -808,6 +828,7 @@ __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *til
                                                d[p * kDescWords + 2], k);
             }
             const OutWords w = pack_words<CN>(rr);
+#endif
             uint8_t *o = dst + (int64_t)f * P.out_fstride;
             if (wide) {
                 uint32_t *o32 = reinterpret_cast<uint32_t *>(o);
@@ -1021,7 +1042,7 @@ MCS_SEAM_ENTRY(4, 0)
 MCS_SEAM_ENTRY(4, 1)
 extern "C" __global__ __launch_bounds__(256) void mcs_blend_classify(const mcs::KBlendPrepArgs a)
 {
-    mcs::blend_classify(a.P, a.mode, a.owner, a.info, a.list, a.overflow);
+    mcs::blend_classify(a.P, a.mode, a.owner, a.info, a.list, a.overflow, a.list2);
 }
 #define MCS_BLEND_ENTRY(CN, IN)                                                                \
     extern "C" __global__ __launch_bounds__(256) void mcs_feather_c##CN##_i##IN(               \

@@ -135,7 +135,8 @@ constexpr int kResizeBlock = 256;
 
 // Blended modes (mcs_blend.h): 32 x 64 output tiles (tall: the seams of a horizontal rig run
 // vertically, so a tall tile shares its pyramid rows), 16-px pyramid halo, <= 4 owners per
-// multi-band neighbourhood, owner map byte 255 = no camera.
+// multi-band neighbourhood (more: the tile takes the feather rule), owner map byte 255 = no
+// camera.
 #ifndef MCS_BLEND_TILE_H
 #define MCS_BLEND_TILE_H 64
 #endif
@@ -190,6 +191,9 @@ struct KBlendPrepArgs {
     uint32_t *info;
     int *list;
     int *overflow;
+    // multi-band: tiles whose neighbourhood holds more than kBlendSlots owners take the feather
+    // rule instead (list2[0] = count, then (tile, feather slot mask) pairs); overflow[0] counts them
+    int *list2;
     int mode, pad_;
 };
 struct KMbArgs {

@@ -109,13 +109,35 @@ def job_rate(units_per_step_per_rank: float, steps: int, seconds_max: float, wor
     return world * units_per_step_per_rank * steps / seconds_max
 
 
-def checksum(t) -> int:
-    """Order-sensitive 63-bit checksum of a u8 tensor's bytes (position-weighted sum), computed
-    where the tensor lives; used to verify gathered mosaics against their producers."""
+CHECKSUM_CHUNK = 1 << 24     # bytes per slice: 64 MB of int32 temporaries, whatever the batch
+
+
+def checksum(t, chunk: int = CHECKSUM_CHUNK) -> int:
+    """Order-sensitive 63-bit checksum of a u8 tensor's bytes, computed where the tensor lives;
+    used to verify gathered mosaics against their producers.
+
+    sum_i byte_i * ((i + 1) mod 65521) mod 2^63, taken slice by slice: per slice of `chunk` bytes
+    the products (< 2^24) in int32 and their int64 sum, so a 1.3 GB batch needs 2 x 64 MB of
+    temporaries instead of 10 GB of int64 ones."""
     import torch
-    flat = t.reshape(-1).to(torch.int64)
-    w = torch.arange(1, flat.numel() + 1, device=flat.device, dtype=torch.int64) % 65521
-    return int((flat * w).sum().item()) & ((1 << 63) - 1)
+    flat = t.reshape(-1)
+    n = flat.numel()
+    base = torch.arange(min(chunk, max(n, 1)), device=flat.device, dtype=torch.int32)
+    total = 0
+    for o in range(0, n, chunk):
+        m = min(chunk, n - o)
+        w = base[:m] + ((o + 1) % 65521)
+        w = torch.remainder(w, 65521)
+        total += int((flat[o:o + m].to(torch.int32) * w).sum(dtype=torch.int64).item())
+    return total & ((1 << 63) - 1)
+
+
+def max_abs_over_ranks(mine, device=None):
+    """Max over ranks of each rank's own max |product - oracle| (None where a rank did not
+    check; None overall when no rank did)."""
+    v = -1.0 if mine is None else float(mine)
+    got = max_over_ranks([v], device=device)[0]
+    return None if got < 0 else int(got)
 
 
 def gather_and_verify(local, dst: int = 0, bufs=None, device=None):

@@ -41,60 +41,91 @@ def build():
     subprocess.check_call(["make", "-s", "-C", _HERE])
 
 
+def build_native(out_path: str, timeout: float = 180.0) -> str:
+    """The same restatement built `-O3 -march=native` for the host running this (bench.py's CPU
+    baseline: SURVEY.md 8d).  Returns out_path; raises on a failed build."""
+    subprocess.run(["make", "-s", "-B", "-C", _HERE, "MARCH=native", "OUT=" + out_path],
+                   check=True, timeout=timeout, capture_output=True)
+    return out_path
+
+
+class library:
+    """Context manager: the oracle functions use the library at `path` (e.g. build_native's)
+    inside the block, the portable liboracle.so again after it."""
+
+    def __init__(self, path: str):
+        self.path = path
+
+    def __enter__(self):
+        global _lib
+        self.saved = _lib
+        _lib = _load(self.path)
+        return _lib
+
+    def __exit__(self, *exc):
+        global _lib
+        _lib = self.saved
+        return False
+
+
 def lib():
     global _lib
     if _lib is None:
         if not os.path.exists(_SO):
             build()
-        L = ctypes.CDLL(_SO)
-        P = ctypes.c_void_p
-        L.orc_invert3x3.argtypes = [P, P]
-        L.orc_invert3x3.restype = ctypes.c_int
-        L.orc_warp_perspective.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_long,
-                                           ctypes.c_int, P, ctypes.c_int, ctypes.c_int,
-                                           ctypes.c_long, P, ctypes.c_int, ctypes.c_int]
-        L.orc_cascade_out_size.argtypes = [P, ctypes.c_int, P, P]
-        L.orc_cascade_stitch.argtypes = [P, ctypes.c_int, P, P, P, ctypes.c_int, ctypes.c_int, P]
-        L.orc_flat_stitch.argtypes = [ctypes.c_int, P, P, P, P, P, P, P, P, ctypes.c_int,
-                                      ctypes.c_int, P, ctypes.c_int, ctypes.c_int]
-        L.orc_map_pixel.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                    P, P]
-        L.orc_bilinear_weights.argtypes = [ctypes.c_int, ctypes.c_int, P]
-        L.orc_num_threads.restype = ctypes.c_int
-        L.orc_set_num_threads.argtypes = [ctypes.c_int]
-        L.orc_resize_linear.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_long,
-                                        ctypes.c_int, P, ctypes.c_int, ctypes.c_int, ctypes.c_long]
-        L.orc_resize_linear.restype = ctypes.c_int
-        L.orc_resize_axis.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P]
-        L.orc_hamming_knn2.argtypes = [P, ctypes.c_int, P, ctypes.c_int, P, P]
-        L.orc_hamming_knn2.restype = None
-        L.orc_blend_stitch.argtypes = [ctypes.c_int, P, P, P, P, P, P, P, P, ctypes.c_int,
-                                       ctypes.c_int, ctypes.c_int, P, ctypes.c_int, ctypes.c_int,
-                                       P, ctypes.c_int, P]
-        L.orc_blend_stitch.restype = ctypes.c_int
-        L.orc_blend_stitch_cyl.argtypes = [ctypes.c_int, P, P, P, P, ctypes.c_double,
-                                           ctypes.c_double, ctypes.c_double, P, P, P,
-                                           ctypes.c_int, ctypes.c_int, ctypes.c_int, P,
-                                           ctypes.c_int, ctypes.c_int, P, ctypes.c_int, P]
-        L.orc_blend_stitch_cyl.restype = ctypes.c_int
-        L.orc_ransac_homography.argtypes = [P, ctypes.c_int, ctypes.c_double, ctypes.c_int,
-                                            ctypes.c_uint32, P, P, P]
-        L.orc_ransac_homography.restype = ctypes.c_int
-        L.orc_homography_refine.argtypes = [P, ctypes.c_int, P, P]
-        L.orc_homography_refine.restype = None
-        L.orc_orb_detect.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                     ctypes.c_float, ctypes.c_int, P, P, P, P, P, P]
-        L.orc_orb_detect.restype = ctypes.c_int
-        L.orc_seam_graphcut.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P,
-                                        ctypes.c_int]
-        L.orc_seam_graphcut.restype = ctypes.c_int
-        L.orc_undistort.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P,
-                                    ctypes.c_int, P]
-        L.orc_undistort.restype = ctypes.c_int
-        L.orc_l2_knn2.argtypes = [P, ctypes.c_int, P, ctypes.c_int, ctypes.c_int, P, P]
-        L.orc_l2_knn2.restype = ctypes.c_int
-        _lib = L
+        _lib = _load(_SO)
     return _lib
+
+
+def _load(path: str):
+    L = ctypes.CDLL(path)
+    P = ctypes.c_void_p
+    L.orc_invert3x3.argtypes = [P, P]
+    L.orc_invert3x3.restype = ctypes.c_int
+    L.orc_warp_perspective.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_long,
+                                       ctypes.c_int, P, ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_long, P, ctypes.c_int, ctypes.c_int]
+    L.orc_cascade_out_size.argtypes = [P, ctypes.c_int, P, P]
+    L.orc_cascade_stitch.argtypes = [P, ctypes.c_int, P, P, P, ctypes.c_int, ctypes.c_int, P]
+    L.orc_flat_stitch.argtypes = [ctypes.c_int, P, P, P, P, P, P, P, P, ctypes.c_int,
+                                  ctypes.c_int, P, ctypes.c_int, ctypes.c_int]
+    L.orc_map_pixel.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                P, P]
+    L.orc_bilinear_weights.argtypes = [ctypes.c_int, ctypes.c_int, P]
+    L.orc_num_threads.restype = ctypes.c_int
+    L.orc_set_num_threads.argtypes = [ctypes.c_int]
+    L.orc_resize_linear.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_long,
+                                    ctypes.c_int, P, ctypes.c_int, ctypes.c_int, ctypes.c_long]
+    L.orc_resize_linear.restype = ctypes.c_int
+    L.orc_resize_axis.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P]
+    L.orc_hamming_knn2.argtypes = [P, ctypes.c_int, P, ctypes.c_int, P, P]
+    L.orc_hamming_knn2.restype = None
+    L.orc_blend_stitch.argtypes = [ctypes.c_int, P, P, P, P, P, P, P, P, ctypes.c_int,
+                                   ctypes.c_int, ctypes.c_int, P, ctypes.c_int, ctypes.c_int,
+                                   P, ctypes.c_int, P]
+    L.orc_blend_stitch.restype = ctypes.c_int
+    L.orc_blend_stitch_cyl.argtypes = [ctypes.c_int, P, P, P, P, ctypes.c_double,
+                                       ctypes.c_double, ctypes.c_double, P, P, P,
+                                       ctypes.c_int, ctypes.c_int, ctypes.c_int, P,
+                                       ctypes.c_int, ctypes.c_int, P, ctypes.c_int, P]
+    L.orc_blend_stitch_cyl.restype = ctypes.c_int
+    L.orc_ransac_homography.argtypes = [P, ctypes.c_int, ctypes.c_double, ctypes.c_int,
+                                        ctypes.c_uint32, P, P, P]
+    L.orc_ransac_homography.restype = ctypes.c_int
+    L.orc_homography_refine.argtypes = [P, ctypes.c_int, P, P]
+    L.orc_homography_refine.restype = None
+    L.orc_orb_detect.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                 ctypes.c_float, ctypes.c_int, P, P, P, P, P, P]
+    L.orc_orb_detect.restype = ctypes.c_int
+    L.orc_seam_graphcut.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P,
+                                    ctypes.c_int]
+    L.orc_seam_graphcut.restype = ctypes.c_int
+    L.orc_undistort.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P,
+                                ctypes.c_int, P]
+    L.orc_undistort.restype = ctypes.c_int
+    L.orc_l2_knn2.argtypes = [P, ctypes.c_int, P, ctypes.c_int, ctypes.c_int, P, P]
+    L.orc_l2_knn2.restype = ctypes.c_int
+    return L
 
 
 def _p(a):

@@ -32,6 +32,11 @@
  *   collapse R1 = B1 + up(B2), R0 = B0 + up(R1), up in double: acc += (uy * ux) * R over the
  *            taps in the order listed (rows outer), then acc / 64;
  *   out = clamp(floor(R0 + 0.5), 0, 255) where an owner exists, else 0.
+ *   Dense seams: the mosaic is cut into 32 x 64 blend tiles (columns x rows); a tile whose
+ *   neighbourhood (the tile grown by 16 px on every side, clipped to the mosaic) holds more than
+ *   8 distinct owners takes the FEATHER rule below for its own pixels instead (the GPU's blend
+ *   kernels hold at most 8 owners; the pyramids of every other tile are unaffected, they depend
+ *   on the samples and the owner map only).
  * SEAM: out = I_owner (the seam without blending), 0 where no slot covers p.
  * Graph-cut seams (seam_k >= 0, orc_seam.c): the owner is the seam label's camera when it
  *   covers p (d >= 0), else the distance owner above.
@@ -187,6 +192,63 @@ static int seam_labels(const geo_t *geo, int S, const int *scam, const uint8_t *
     return rc;
 }
 
+/* FEATHER at pixel p: (sum_s d_s I_s + D / 2) / D over the slots at positive distance. */
+static void feather_px(int S, long npx, int cn, const uint8_t *owner, const int32_t *dist,
+                       const uint8_t *g0, long p, uint8_t *d)
+{
+    if (owner[p] == 255) {
+        memset(d, 0, (size_t)cn);
+        return;
+    }
+    int64_t den = 0;
+    for (int s = 0; s < S; s++)
+        if (dist[(long)s * npx + p] > 0) den += dist[(long)s * npx + p];
+    for (int k = 0; k < cn; k++) {
+        if (den == 0) {
+            d[k] = g0[((long)owner[p] * npx + p) * cn + k];
+            continue;
+        }
+        int64_t num = 0;
+        for (int s = 0; s < S; s++) {
+            const int32_t ds = dist[(long)s * npx + p];
+            if (ds > 0) num += (int64_t)ds * g0[((long)s * npx + p) * cn + k];
+        }
+        d[k] = (uint8_t)((num + den / 2) / den);
+    }
+}
+
+/* Multi-band blend tiles (32 x 64) whose 16-px neighbourhood holds more than 8 owners: 1. */
+#define ORC_MB_TILE_W 32
+#define ORC_MB_TILE_H 64
+#define ORC_MB_HALO 16
+#define ORC_MB_MAX_OWNERS 8
+static uint8_t *dense_tiles(const uint8_t *owner, int ow, int oh, int *gx_out)
+{
+    const int gx = (ow + ORC_MB_TILE_W - 1) / ORC_MB_TILE_W;
+    const int gy = (oh + ORC_MB_TILE_H - 1) / ORC_MB_TILE_H;
+    uint8_t *dense = (uint8_t *)calloc((size_t)gx * gy, 1);
+    if (!dense) return NULL;
+#pragma omp parallel for schedule(static)
+    for (int t = 0; t < gx * gy; t++) {
+        const int tx = t % gx, ty = t / gx;
+        int x0 = tx * ORC_MB_TILE_W - ORC_MB_HALO, x1 = tx * ORC_MB_TILE_W + ORC_MB_TILE_W + ORC_MB_HALO;
+        int y0 = ty * ORC_MB_TILE_H - ORC_MB_HALO, y1 = ty * ORC_MB_TILE_H + ORC_MB_TILE_H + ORC_MB_HALO;
+        if (x0 < 0) x0 = 0;
+        if (y0 < 0) y0 = 0;
+        if (x1 > ow) x1 = ow;
+        if (y1 > oh) y1 = oh;
+        uint32_t m = 0;
+        for (int y = y0; y < y1; y++)
+            for (int x = x0; x < x1; x++) {
+                const int o = owner[(long)y * ow + x];
+                if (o != 255) m |= 1u << o;
+            }
+        dense[t] = __builtin_popcount(m) > ORC_MB_MAX_OWNERS;
+    }
+    *gx_out = gx;
+    return dense;
+}
+
 static int blend_core(const geo_t *geo, int S, const int *scam, const uint8_t *const *cams,
                       const int *cw, const int *ch, int cn, int interp, int mode, uint8_t *out,
                       int ow, int oh, uint8_t *owner_out, int seam_k, uint8_t *seam_lab)
@@ -237,28 +299,7 @@ static int blend_core(const geo_t *geo, int S, const int *scam, const uint8_t *c
         }
     } else if (mode == ORC_BLEND_FEATHER) {
 #pragma omp parallel for schedule(static)
-        for (long p = 0; p < npx; p++) {
-            uint8_t *d = out + p * cn;
-            if (owner[p] == 255) {
-                memset(d, 0, (size_t)cn);
-                continue;
-            }
-            int64_t den = 0;
-            for (int s = 0; s < S; s++)
-                if (dist[(long)s * npx + p] > 0) den += dist[(long)s * npx + p];
-            for (int k = 0; k < cn; k++) {
-                if (den == 0) {
-                    d[k] = g0[((long)owner[p] * npx + p) * cn + k];
-                    continue;
-                }
-                int64_t num = 0;
-                for (int s = 0; s < S; s++) {
-                    const int32_t ds = dist[(long)s * npx + p];
-                    if (ds > 0) num += (int64_t)ds * g0[((long)s * npx + p) * cn + k];
-                }
-                d[k] = (uint8_t)((num + den / 2) / den);
-            }
-        }
+        for (long p = 0; p < npx; p++) feather_px(S, npx, cn, owner, dist, g0, p, out + p * cn);
     } else if (mode == ORC_BLEND_MULTIBAND) {
         const int w1 = (ow + 1) / 2, h1 = (oh + 1) / 2, w2 = (w1 + 1) / 2, h2 = (h1 + 1) / 2;
         const long n1 = (long)w1 * h1, n2 = (long)w2 * h2;
@@ -307,11 +348,21 @@ static int blend_core(const geo_t *geo, int S, const int *scam, const uint8_t *c
                 r1[q * cn + k] = b1 + expand_d(b2, w2, h2, cn, y, x, k);
             }
         }
+        int gxd = 0;
+        uint8_t *dense = dense_tiles(owner, ow, oh, &gxd);
+        if (!dense) {
+            rc = -1;
+            goto done;
+        }
 #pragma omp parallel for schedule(static)
         for (long p = 0; p < npx; p++) {
             const int y = (int)(p / ow), x = (int)(p % ow);
             uint8_t *d = out + p * cn;
             const int s = owner[p];
+            if (dense[(long)(y / ORC_MB_TILE_H) * gxd + x / ORC_MB_TILE_W]) {
+                feather_px(S, npx, cn, owner, dist, g0, p, d);
+                continue;
+            }
             for (int k = 0; k < cn; k++) {
                 if (s == 255) {
                     d[k] = 0;
@@ -324,6 +375,7 @@ static int blend_core(const geo_t *geo, int S, const int *scam, const uint8_t *c
                 d[k] = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
             }
         }
+        free(dense);
     done:
         free(t0); free(g1); free(g2); free(m0); free(m1); free(m2); free(b2); free(r1);
     } else {

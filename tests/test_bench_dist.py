@@ -36,6 +36,8 @@ def test_bench_gpus2_spawns_two_ranks():
     assert abs(res["value"] - want) <= 1e-5 * want + 1e-6
     assert res["max_seconds"] >= res["rank0_seconds"]
     assert res["gather"] == {"verified": True, "ranks": 2, "bytes_into_rank0": 4 * 32 * 48 * 3}
+    # every rank checked its own output; the line carries the max over ranks, a number
+    assert res["max_abs_diff"] == 0
 
 
 def test_bench_gpus1_stub_single_process():

@@ -63,3 +63,19 @@ def test_gloo_world2_sharding_reduce_gather():
     assert t == [1.5, 3.0]
     assert flat == list(range(10))
     assert shapes == [[4, 6, 3], [4, 6, 3]]
+
+
+def test_checksum_chunked_equals_definition():
+    """shard.checksum slice by slice (int32 products, int64 sums) = the position-weighted sum
+    sum_i b_i ((i + 1) mod 65521) mod 2^63, for slice sizes that do and do not divide the data."""
+    import numpy as np
+    import torch
+    from multicamera_stitching_amd import shard
+    rng = np.random.default_rng(3)
+    a = rng.integers(0, 256, size=200_003, dtype=np.uint8)
+    w = (np.arange(1, a.size + 1, dtype=np.int64) % 65521)
+    want = int((a.astype(np.int64) * w).sum()) & ((1 << 63) - 1)
+    t = torch.from_numpy(a)
+    for chunk in (1 << 24, 65536, 1000, 7):
+        assert shard.checksum(t, chunk=chunk) == want
+    assert shard.checksum(t.reshape(-1)[:0]) == 0
