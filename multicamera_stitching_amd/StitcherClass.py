@@ -187,9 +187,11 @@ class Stitcher(_Transient, Debugger):
             self.stitchers[idx].calibrate(images=images, ratio=0.75, reprojThresh=3.0,
                                           xoffset=0, yoffset=0, homography=H,
                                           use_features=homographies is None)
-            if homographies is None or callable(homographies):
+            if homographies is None or (callable(homographies) and
+                                        getattr(homographies, "needs_pixels", True)):
                 # the next stage's B is the real mosaic so far: the reference's features, or a
-                # callable that may estimate its H from imageB's pixels, see it
+                # callable that may estimate its H from imageB's pixels, see it (a callable that
+                # declares needs_pixels = False gets B's shape only, like a list)
                 img_result = self.stitchers[idx].stitch(images=images)
             else:
                 # a list of matrices needs only the next stage's B shape: no pixels, no GPU work

@@ -1150,8 +1150,17 @@ __device__ __forceinline__ void mb_target(const KMbBandArgs &a, int s, int row, 
 // the reduces computed there are the reflected entries (reflect-101 about 0 commutes with the
 // 2x decimation).  At the bottom / right edges it does not (for even level sizes), so BR units
 // give level 2 the reflected level-1 rows (a history of four) and columns (source lanes).
+// This block's band of the launch (KMbBandArgs::xcd), -1 past the launch's bands.
+__device__ __forceinline__ int mb_band_of_block(const KMbBandArgs &a)
+{
+    if (a.xcd <= 0) return (int)blockIdx.x;
+    const int per = (a.xcd + 7) >> 3;
+    const int i = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+    return i < a.xcd ? i : -1;
+}
+
 template <int CN, int FR, bool BR>
-__device__ __forceinline__ void mb_bands(const KMbBandArgs &a)
+__device__ __forceinline__ void mb_bands(const KMbBandArgs &a, int bl)
 {
     typedef __attribute__((address_space(1))) const uint8_t gu8;
     struct __attribute__((packed)) U2 {
@@ -1161,7 +1170,7 @@ __device__ __forceinline__ void mb_bands(const KMbBandArgs &a)
     typedef __attribute__((address_space(1))) uint2 g2u;
     const KParams &P = a.P;
     const int l = threadIdx.x;
-    const int bi = a.band0 + blockIdx.x;
+    const int bi = a.band0 + bl;
     const MbBand B = a.bands[bi];
     const int fl0 = blockIdx.y * FR;
     if (fl0 >= a.nf) return;

@@ -28,6 +28,7 @@ struct mcs_plan {
     int gx = 0, gy = 0, n_fallback = 0;
     mcs::TileHdr *d_tiles = nullptr;
     uint32_t *d_desc = nullptr;
+    uint32_t *d_desc4 = nullptr;      // compact per-pixel words (the streaming kernel reads these)
     int *d_fallback = nullptr;
     // side stream for the direct-gather tiles, forked from / joined to the caller's stream
     hipStream_t side = nullptr;
@@ -285,7 +286,42 @@ void band_args(const mcs_plan *p, const mcs::KParams &P, mcs::KMbBandArgs &a)
     a.gxb = p->gxb;
     a.band0 = 0;
     a.n_in = p->n_bands_in;
-    a.pad_ = 0;
+    a.xcd = 0;
+}
+
+// Grid width of a band launch of n bands (XCD-contiguous mapping: padded to a multiple of 8).
+// MCS_MB_BAND_XCD=0 / 1: the mapping (KMbBandArgs::xcd).
+unsigned band_grid(mcs::KMbBandArgs &b, int n)
+{
+    static const bool xcd = getenv("MCS_MB_BAND_XCD") && strcmp(getenv("MCS_MB_BAND_XCD"), "0");
+    b.xcd = xcd ? n : 0;
+    return xcd ? 8u * (((unsigned)n + 7u) / 8u) : (unsigned)n;
+}
+
+// Order of the streaming tiles in a launch list.  stream_tile deals a list to the 8 XCDs in
+// contiguous slices (XCD x: entries [x * per, (x + 1) * per)), each walked in list order, so the
+// order decides which tiles share an XCD's L2 at the same time.  MCS_STREAM_ORDER=0: row-major
+// (an XCD holds a band of whole tile rows: horizontal neighbours together, vertical ones only
+// at the band's concurrent rows); 1 (experiment): 8 vertical strips of ceil(gx / 8) tile
+// columns, each walked row by row (an XCD's resident blocks are ~16 vertically adjacent rows of
+// its strip).  Measured (same box, two alternations): strips are slower -- paste launch 0.610 ->
+// 0.627-0.639 ms, multi-band 0.972 -> 0.977 ms: the 16-byte chunk rounding at both ends of every
+// footprint row makes horizontal neighbours share more L2 lines than vertical ones share rows.
+int stream_order_mode()
+{
+    static const int mode = getenv("MCS_STREAM_ORDER") ? atoi(getenv("MCS_STREAM_ORDER")) : 0;
+    return mode;
+}
+
+void order_tiles(const mcs_plan *p, std::vector<int> &v)
+{
+    if (stream_order_mode() != 1) return;   // (lists are built row-major)
+    const int sw = (p->gx + 7) / 8;
+    std::stable_sort(v.begin(), v.end(), [&](int a, int b) {
+        const int ax = a % p->gx, ay = a / p->gx, bx = b % p->gx, by = b / p->gx;
+        if (ax / sw != bx / sw) return ax / sw < bx / sw;
+        return ay != by ? ay < by : ax < bx;
+    });
 }
 
 // The band pass of a multi-band plan (after mb_prep): per (owner slot, blend-tile row) the
@@ -402,13 +438,14 @@ int prepare_bands(const Api *A, mcs_plan *p, const Kernels *k, hipStream_t s)
                 for (int tx = X0 / mcs::kTileW; tx <= x1 / mcs::kTileW; tx++)
                     early[(size_t)ty * p->gx + tx] = 1;
         }
-        std::vector<int> order;
+        std::vector<int> order, late;
         order.reserve(early.size());
         for (size_t t = 0; t < early.size(); t++)
-            if (early[t]) order.push_back((int)t);
+            (early[t] ? order : late).push_back((int)t);
         p->n_early = (int)order.size();
-        for (size_t t = 0; t < early.size(); t++)
-            if (!early[t]) order.push_back((int)t);
+        order_tiles(p, order);
+        order_tiles(p, late);
+        order.insert(order.end(), late.begin(), late.end());
         HIP_TRY(A->hipMalloc((void **)&p->d_order, order.size() * sizeof(int)));
         HIP_TRY(A->hipMemcpyAsync(p->d_order, order.data(), order.size() * sizeof(int),
                                   hipMemcpyHostToDevice, s));
@@ -525,7 +562,8 @@ void release_tables(const Api *A, mcs_plan *p)
     if (p->stream) (void)A->hipStreamSynchronize(p->stream);
     if (p->side) (void)A->hipStreamSynchronize(p->side);
     if (p->side2) (void)A->hipStreamSynchronize(p->side2);
-    for (void *q : {(void *)p->d_tiles, (void *)p->d_desc, (void *)p->d_fallback,
+    for (void *q : {(void *)p->d_tiles, (void *)p->d_desc, (void *)p->d_desc4,
+                    (void *)p->d_fallback,
                     (void *)p->d_owner, (void *)p->d_binfo, (void *)p->d_blist,
                     (void *)p->d_mbdesc, (void *)p->d_mbtab, (void *)p->d_mbfoot, (void *)p->d_mbg1,
                     (void *)p->d_mbg2, (void *)p->d_bands, (void *)p->d_tile_bt,
@@ -545,6 +583,7 @@ void release_tables(const Api *A, mcs_plan *p)
     p->mb_chunk = 0;
     p->d_tiles = nullptr;
     p->d_desc = nullptr;
+    p->d_desc4 = nullptr;
     p->d_fallback = nullptr;
     p->d_owner = nullptr;
     p->d_binfo = nullptr;
@@ -597,12 +636,14 @@ int prepare(const Api *A, mcs_plan *p, hipStream_t s)
     }
     HIP_TRY(A->hipMalloc((void **)&p->d_tiles, tiles * sizeof(mcs::TileHdr)));
     HIP_TRY(A->hipMalloc((void **)&p->d_desc, tiles * mcs::kTilePx * mcs::kDescWords * 4));
+    HIP_TRY(A->hipMalloc((void **)&p->d_desc4, tiles * mcs::kTilePx * 4));
     HIP_TRY(A->hipMalloc((void **)&p->d_fallback, (tiles + 1) * sizeof(int)));
     HIP_TRY(A->hipMemsetAsync(p->d_fallback, 0, sizeof(int), s));
     mcs::KPrepareArgs args;
     args.P = p->kp;
     args.tiles = p->d_tiles;
     args.desc = p->d_desc;
+    args.desc4 = p->d_desc4;
     args.fallback = p->d_fallback;
     size_t sz = sizeof(args);
     void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, (void *)&args, HIP_LAUNCH_PARAM_BUFFER_SIZE,
@@ -613,6 +654,17 @@ int prepare(const Api *A, mcs_plan *p, hipStream_t s)
     HIP_TRY(A->hipMemcpyAsync(&nf, p->d_fallback, sizeof(int), hipMemcpyDeviceToHost, s));
     HIP_TRY(A->hipStreamSynchronize(s));
     p->n_fallback = nf;
+    if (!p->d_order && stream_order_mode() != 0) {
+        // one launch list of every tile (the multi-band split builds its own, early tiles first)
+        std::vector<int> order(tiles);
+        for (size_t t = 0; t < tiles; t++) order[t] = (int)t;
+        order_tiles(p, order);
+        HIP_TRY(A->hipMalloc((void **)&p->d_order, order.size() * sizeof(int)));
+        HIP_TRY(A->hipMemcpyAsync(p->d_order, order.data(), order.size() * sizeof(int),
+                                  hipMemcpyHostToDevice, s));
+        HIP_TRY(A->hipStreamSynchronize(s));
+        p->n_early = 0;
+    }
     p->prepared = true;
     return MCS_OK;
 }
@@ -637,18 +689,23 @@ int launch_mb_levels(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KMb
         // two launches.
         static const bool fused =
             !getenv("MCS_MB_BANDS_FUSED") || strcmp(getenv("MCS_MB_BANDS_FUSED"), "0") != 0;
-        if (fused && p->n_bands_in > 0 && p->n_bands > p->n_bands_in)
-            return launch_args(A, k->mb_bands[p->fd.channels][2], (unsigned)p->n_bands, gy,
-                               mcs::kMbBandLanes, 1, &b, sizeof(b), s);
+        if (fused && p->n_bands_in > 0 && p->n_bands > p->n_bands_in) {
+            const unsigned gx = band_grid(b, p->n_bands);
+            return launch_args(A, k->mb_bands[p->fd.channels][2], gx, gy, mcs::kMbBandLanes, 1,
+                               &b, sizeof(b), s);
+        }
         int rc = MCS_OK;
-        if (p->n_bands_in > 0)
-            rc = launch_args(A, k->mb_bands[p->fd.channels][0], (unsigned)p->n_bands_in, gy,
-                             mcs::kMbBandLanes, 1, &b, sizeof(b), s);
-        b.band0 = p->n_bands_in;
-        if (rc == MCS_OK && p->n_bands > p->n_bands_in)
-            rc = launch_args(A, k->mb_bands[p->fd.channels][1],
-                             (unsigned)(p->n_bands - p->n_bands_in), gy, mcs::kMbBandLanes, 1, &b,
+        if (p->n_bands_in > 0) {
+            const unsigned gx = band_grid(b, p->n_bands_in);
+            rc = launch_args(A, k->mb_bands[p->fd.channels][0], gx, gy, mcs::kMbBandLanes, 1, &b,
                              sizeof(b), s);
+        }
+        b.band0 = p->n_bands_in;
+        if (rc == MCS_OK && p->n_bands > p->n_bands_in) {
+            const unsigned gx = band_grid(b, p->n_bands - p->n_bands_in);
+            rc = launch_args(A, k->mb_bands[p->fd.channels][1], gx, gy, mcs::kMbBandLanes, 1, &b,
+                             sizeof(b), s);
+        }
         return rc;
     }
     const unsigned gz = (unsigned)((nf + mcs::kMbLvFrames - 1) / mcs::kMbLvFrames);
@@ -727,6 +784,7 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
     const bool b32 = stream_base(p, P, n_frames, &args.P.base);
     args.tiles = p->d_tiles;
     args.desc = p->d_desc;
+    args.desc4 = p->d_desc4;
     args.n_frames = n_frames;
     args.pad_ = 0;
     args.pad2_ = 0;
@@ -772,7 +830,8 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
         return launch_dense(A, p, k, P, n_frames, s);
     }
     {
-        const int rc = stream_launch(nullptr, n_tiles, lds);
+        // (d_order: the tile order of prepare / prepare_bands; NULL: row-major grid order)
+        const int rc = stream_launch(p->d_order, n_tiles, lds);
         if (rc) return rc;
     }
     if (p->n_fallback > 0) HIP_TRY(A->hipStreamWaitEvent(s, p->ev_join, 0));
@@ -1526,7 +1585,7 @@ int mcs_plan_stats(const mcs_plan *p, int64_t *stats, int n)
     const int64_t tiles = (int64_t)p->gx * p->gy;
     const int64_t v[9] = {p->prepared ? 1 : 0, tiles, tiles - p->n_fallback, p->n_fallback,
                           tiles * (int64_t)(sizeof(mcs::TileHdr) +
-                                            mcs::kTilePx * mcs::kDescWords * 4),
+                                            mcs::kTilePx * (mcs::kDescWords + 1) * 4),
                           p->blend, p->n_blend, p->mb_slots, p->n_degraded};
     for (int i = 0; i < n; i++) stats[i] = i < 9 ? v[i] : 0;
     return MCS_OK;

@@ -334,6 +334,9 @@ __device__ __forceinline__ int place_cols(int sx, int sw, uint32_t wl, uint32_t 
 struct Geo {
     int cam, r0, c0, r1, c1;
     uint32_t w0, w1;
+    int fx, fy;                  // the bilinear fraction (1/32 px)
+    bool plain;                  // all four taps in the image (or fy = 0 and both row-0 taps):
+                                 // the weights follow from (fx, fy), row 1 = row 0 + 1, c1 = c0
 };
 
 template <int CN, int INTERP>
@@ -378,6 +381,9 @@ __device__ __forceinline__ Geo describe_geo(const KParams &P, int x, int y)
     g.r1 = y1_in ? sy + 1 : 0;
     g.w0 = w2x(a0) | (w2x(b0) << 16);
     g.w1 = w2x(a1) | (w2x(b1) << 16);
+    g.fx = fx;
+    g.fy = fy;
+    g.plain = sx >= 0 && sx + 1 < sw && y0_in && (y1_in || fy == 0);
     if (g.w0 == 0u) {            // no live tap in row 0: reuse row 1's window
         g.r0 = g.r1;
         g.c0 = g.c1;
@@ -495,7 +501,7 @@ struct FootprintLds {
 
 template <int CN, int INTERP>
 __device__ __forceinline__ void prepare_tile(const KParams &P, TileHdr *tiles, uint32_t *desc,
-                                             int *fallback)
+                                             uint32_t *desc4, int *fallback)
 {
     __shared__ FootprintLds fl;
     __shared__ TileHdr th;
@@ -578,7 +584,7 @@ __device__ __forceinline__ void prepare_tile(const KParams &P, TileHdr *tiles, u
         if (!th.fits) fallback[1 + atomicAdd(&fallback[0], 1)] = tile;
     }
     __syncthreads();
-    uint32_t d[kPx * kDescWords];
+    uint32_t d[kPx * kDescWords], cw[kPx];
 #pragma unroll
     for (int p = 0; p < kPx; p++) {
         int k = 0;
@@ -589,11 +595,25 @@ __device__ __forceinline__ void prepare_tile(const KParams &P, TileHdr *tiles, u
                                  (g[p].r0 == last ? e : 0));
         uint32_t a1 = (uint32_t)(bs + (g[p].r1 - rm) * st + (g[p].c1 - ca) +
                                  (g[p].r1 == last ? e : 0));
-        if ((g[p].w0 | g[p].w1) == 0u || !th.fits) a0 = a1 = 0u;
+        const bool zero = (g[p].w0 | g[p].w1) == 0u || !th.fits;
+        if (zero) a0 = a1 = 0u;
         d[p * kDescWords + 0] = (a0 & 0xffffu) | (a1 << 16);
         d[p * kDescWords + 1] = g[p].w0;
         d[p * kDescWords + 2] = g[p].w1;
+        // compact form (kCw*): a plain bilinear pixel is its row-0 window, (fx, fy) and its
+        // camera's footprint slot; row 1 is one footprint row further (plus the last-row shift
+        // when row 1 is the frame's last row)
+        if (zero)
+            cw[p] = kCwZero;
+        else if (!g[p].plain)
+            cw[p] = kCwFull;
+        else
+            cw[p] = (a0 & 0xffffu) | ((uint32_t)g[p].fx << 16) | ((uint32_t)g[p].fy << 21) |
+                    ((uint32_t)k << 26) | (g[p].fy == 0 ? kCwOneRow : 0u) |
+                    (g[p].fy != 0 && g[p].r1 == last && e ? kCwLastRow1 : 0u);
     }
+    reinterpret_cast<uint4 *>(desc4)[(int64_t)tile * (kTilePx / kPx) + tid] =
+        make_uint4(cw[0], cw[1], cw[2], cw[3]);
     uint4 *o = reinterpret_cast<uint4 *>(desc + ((int64_t)tile * kTilePx + (int64_t)tid * kPx) *
                                                     kDescWords);
 #pragma unroll
@@ -607,9 +627,6 @@ __device__ __forceinline__ void prepare_tile(const KParams &P, TileHdr *tiles, u
 // 0.978 -> 0.951 ms).
 #ifndef MCS_DMA_AUX
 #define MCS_DMA_AUX 0
-#endif
-#ifndef MCS_DESC_NT
-#define MCS_DESC_NT 0
 #endif
 #ifndef MCS_STORE_NT
 #define MCS_STORE_NT 1
@@ -738,8 +755,9 @@ __device__ __forceinline__ void wait_vmcnt_le(int n)
 // speed only.)
 template <int CN, bool BUF>
 __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *tiles,
-                                            const uint32_t *desc, int n_frames, const int *order,
-                                            int n_order, uint8_t *smem)
+                                            const uint32_t *desc, const uint32_t *desc4,
+                                            int n_frames, const int *order, int n_order,
+                                            uint8_t *smem)
 {
     const int lane = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(threadIdx.y);
     const int tid = wave * kWave + lane;
@@ -761,23 +779,37 @@ __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *til
     tile_pixel(bx, by, lane, wave, xg, y);
     const bool live = xg < P.out_w && y < P.out_h;
     const int npx = live ? min(kPx, P.out_w - xg) : 0;
+    // the lane's 4 pixel descriptors: one 16-byte load of their compact words (4 B per pixel
+    // per launch instead of 12), expanded here; pixels off the plain bilinear form (frame edges)
+    // read their full 12-byte form
     uint32_t d[kPx * kDescWords];
     {
-        const uint4 *s4 = reinterpret_cast<const uint4 *>(
-            desc + ((int64_t)tile * kTilePx + (int64_t)tid * kPx) * kDescWords);
+        const uint4 c4 = reinterpret_cast<const uint4 *>(desc4)[(int64_t)tile * (kTilePx / kPx) +
+                                                                 tid];
+        const uint32_t cw[kPx] = {c4.x, c4.y, c4.z, c4.w};
+        const uint32_t *full = desc + ((int64_t)tile * kTilePx + (int64_t)tid * kPx) * kDescWords;
 #pragma unroll
-        for (int i = 0; i < kPx * kDescWords / 4; i++) {
-#if MCS_DESC_NT
-            typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-            const v4u t = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(s4) + i);
-            const uint4 v = make_uint4(t.x, t.y, t.z, t.w);
-#else
-            const uint4 v = s4[i];
-#endif
-            d[4 * i] = v.x;
-            d[4 * i + 1] = v.y;
-            d[4 * i + 2] = v.z;
-            d[4 * i + 3] = v.w;
+        for (int p = 0; p < kPx; p++) {
+            const uint32_t w = cw[p];
+            uint32_t d0, d1, d2;
+            if (w & kCwFull) {
+                d0 = full[p * kDescWords];
+                d1 = full[p * kDescWords + 1];
+                d2 = full[p * kDescWords + 2];
+            } else {
+                const uint32_t a0 = w & 0xffffu, fx = (w >> 16) & 31u, fy = (w >> 21) & 31u;
+                const int k = (int)((w >> 26) & 3u);
+                const uint32_t e = (w & kCwLastRow1) ? ((uint32_t)h.last_shift >> (8 * k)) & 255u
+                                                     : 0u;
+                const uint32_t a1 = (w & kCwOneRow) ? a0 : a0 + (uint32_t)h.stride[k] + e;
+                d0 = a0 | (a1 << 16);
+                d1 = w2x((32u - fx) * (32u - fy) * 32u) | (w2x(fx * (32u - fy) * 32u) << 16);
+                d2 = w2x((32u - fx) * fy * 32u) | (w2x(fx * fy * 32u) << 16);
+                if (w & kCwZero) d0 = d1 = d2 = 0u;
+            }
+            d[p * kDescWords] = d0;
+            d[p * kDescWords + 1] = d1;
+            d[p * kDescWords + 2] = d2;
         }
     }
     const WaveJobs<BUF> J = wave_jobs<CN, BUF>(P, h, wave);
@@ -974,9 +1006,10 @@ __device__ __forceinline__ void resize_px(const KResizeArgs &a)
 // (ceil(out_w/256), out_h).
 #define MCS_PREPARE_ENTRY(CN, IN)                                                              \
     extern "C" __global__ __launch_bounds__(512) void mcs_prepare_c##CN##_i##IN(               \
-        const mcs::KParams P, mcs::TileHdr *tiles, uint32_t *desc, int *fallback)              \
+        const mcs::KParams P, mcs::TileHdr *tiles, uint32_t *desc, uint32_t *desc4,            \
+        int *fallback)                                                                         \
     {                                                                                          \
-        mcs::prepare_tile<CN, IN>(P, tiles, desc, fallback);                                   \
+        mcs::prepare_tile<CN, IN>(P, tiles, desc, desc4, fallback);                            \
     }
 #ifdef MCS_STREAM_WAVES_PER_EU   // experiment knob: occupancy target of the streaming kernel
 #define MCS_STREAM_ATTR __attribute__((amdgpu_waves_per_eu(MCS_STREAM_WAVES_PER_EU)))
@@ -990,11 +1023,11 @@ __device__ __forceinline__ void resize_px(const KResizeArgs &a)
 #endif
 #define MCS_STREAM_ENTRY(CN, SUF, BUF)                                                         \
     extern "C" __global__ __launch_bounds__(512) MCS_STREAM_ATTR void mcs_stream_c##CN##SUF(   \
-        const mcs::KParams P, const mcs::TileHdr *tiles, const uint32_t *desc, int n_frames,  \
-        const int *order, int n_order)                                                         \
+        const mcs::KParams P, const mcs::TileHdr *tiles, const uint32_t *desc,                \
+        const uint32_t *desc4, int n_frames, const int *order, int n_order)                    \
     {                                                                                          \
         extern __shared__ __attribute__((aligned(16))) uint8_t smem[];                         \
-        mcs::stream_tile<CN, BUF>(P, tiles, desc, n_frames, order, n_order, smem);             \
+        mcs::stream_tile<CN, BUF>(P, tiles, desc, desc4, n_frames, order, n_order, smem);      \
     }
 #define MCS_DIRECT_ENTRY(CN, IN, O32)                                                          \
     extern "C" __global__ __launch_bounds__(512) void mcs_direct_c##CN##_i##IN##_o##O32(       \
@@ -1073,18 +1106,22 @@ extern "C" __global__ __launch_bounds__(256) void mcs_blend_classify(const mcs::
     extern "C" __global__ __launch_bounds__(64) void mcs_mb_bands_c##CN(                       \
         const mcs::KMbBandArgs a)                                                              \
     {                                                                                          \
-        mcs::mb_bands<CN, mcs::kMbBandFrames, false>(a);                                       \
+        const int bl = mcs::mb_band_of_block(a);                                               \
+        if (bl >= 0) mcs::mb_bands<CN, mcs::kMbBandFrames, false>(a, bl);                      \
     }                                                                                          \
     extern "C" __global__ __launch_bounds__(64) void mcs_mb_bands_br_c##CN(                    \
         const mcs::KMbBandArgs a)                                                              \
     {                                                                                          \
-        mcs::mb_bands<CN, mcs::kMbBandFrames, true>(a);                                        \
+        const int bl = mcs::mb_band_of_block(a);                                               \
+        if (bl >= 0) mcs::mb_bands<CN, mcs::kMbBandFrames, true>(a, bl);                       \
     }                                                                                          \
     extern "C" __global__ __launch_bounds__(64) void mcs_mb_bands_all_c##CN(                   \
         const mcs::KMbBandArgs a)                                                              \
     {                                                                                          \
-        if ((int)blockIdx.x < a.n_in) mcs::mb_bands<CN, mcs::kMbBandFrames, false>(a);         \
-        else mcs::mb_bands<CN, mcs::kMbBandFrames, true>(a);                                   \
+        const int bl = mcs::mb_band_of_block(a);                                               \
+        if (bl < 0) return;                                                                    \
+        if (bl < a.n_in) mcs::mb_bands<CN, mcs::kMbBandFrames, false>(a, bl);                  \
+        else mcs::mb_bands<CN, mcs::kMbBandFrames, true>(a, bl);                               \
     }                                                                                          \
     extern "C" __global__ __launch_bounds__(MCS_MB_BL_THREADS) MCS_MB_BL_ATTR void             \
         mcs_mb_blend_c##CN##_s2(                                                               \

@@ -84,6 +84,14 @@ constexpr int kTileH = kWavesPerBlock * kRowsPerWave;
 constexpr int kTileCams = 4;       // cameras one LDS tile may draw from
 constexpr int kTilePx = kTileW * kTileH;
 constexpr int kDescWords = 3;
+// Compact per-pixel word the streaming kernel loads (4 B instead of 12): bits 0-15 the row-0
+// window's LDS address, 16-20 fx, 21-25 fy, 26-27 the camera's footprint slot in the tile header;
+// flags below.  A "plain" pixel (all taps in the image) has the weights of (fx, fy) and its row-1
+// window one footprint row further; other pixels (frame edges) read the full 12-byte form.
+constexpr uint32_t kCwLastRow1 = 1u << 28;   // row 1 is the frame's last row (+ its DMA shift)
+constexpr uint32_t kCwZero = 1u << 29;       // no live tap (no camera): output 0
+constexpr uint32_t kCwFull = 1u << 30;       // read the full form
+constexpr uint32_t kCwOneRow = 1u << 31;     // fy = 0: row 1 unused (= row 0)
 struct TileHdr {
     int fits;                      // 1: LDS path, 0: listed for the direct-gather launch
     int ncam, njobs, ring, buf_bytes;
@@ -102,12 +110,14 @@ struct KPrepareArgs {
     KParams P;
     TileHdr *tiles;
     uint32_t *desc;
+    uint32_t *desc4;               // compact words (kCw*), 4 per lane
     int *fallback;                 // [0] = count, then tile indices
 };
 struct KStreamArgs {
     KParams P;
     const TileHdr *tiles;
     const uint32_t *desc;
+    const uint32_t *desc4;
     int n_frames;
     int pad_;
     const int *order;              // tiles to stream (NULL: all, in grid order)
@@ -251,8 +261,13 @@ struct KMbBandArgs {
     int slots, chunk, f0, nf;
     int gxb;                       // blend tiles per mosaic row
     int band0;                     // first band of this launch
-    int n_in;                      // mcs_mb_bands_all: blocks below n_in take the interior path
-    int pad_;
+    int n_in;                      // mcs_mb_bands_all: bands below n_in take the interior path
+    // band -> block mapping: 0 = block x is band x (consecutive bands round-robin over the 8
+    // XCDs); n > 0 = XCD-contiguous: the launch's n bands are dealt to the XCDs in contiguous
+    // slices (block b -> band (b % 8) * ceil(n / 8) + b / 8; the grid is padded to a multiple
+    // of 8), so vertically adjacent bands of one owner -- which share 25 of their 89 source
+    // rows -- run on one XCD's L2
+    int xcd;
 };
 struct KBlendArgs {
     KParams P;

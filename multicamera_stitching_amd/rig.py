@@ -74,6 +74,7 @@ def homography_provider(C, chain_getter):
     def provide(idx, stitcher_base, imageB, imageA):
         chain = chain_getter()
         return stage_homography(C, idx, chain[:idx])
+    provide.needs_pixels = False    # the rig's H follow from the camera models and the chain
     return provide
 
 

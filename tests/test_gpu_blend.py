@@ -137,12 +137,13 @@ def test_multiband_more_than_eight_owners_degrades_to_feather(n, w, step):
     assert _diff(got.reshape(want.shape), want) == 0
     st = plan.stats()
     assert st["mb_degraded_tiles"] > 0 and st["mb_owners"] <= 8
-    # the degraded tiles really are feathered: where they are, the mosaic equals the feather
-    # mosaic, and somewhere else it does not
+    # the degraded tiles really are feathered (their pixels equal the feather mosaic's; the CPU
+    # test test_blend_dense_cpu.py checks which tiles), the others are not
     plan.set_blend(MODES["feather"])
     fea = oracle.blend_stitch(plan.describe(), cams, MODES["feather"])
     assert _diff(plan.stitch_host(cams).reshape(fea.shape), fea) == 0
-    assert (want == fea).all(axis=-1).mean() > 0.5
+    same = (want == fea).all(axis=-1).mean()
+    assert 0.2 < same < 1.0, same
 
 
 def test_dropin_dense_rig_multiband_does_not_raise(monkeypatch):

@@ -9,3 +9,9 @@ BLENDS=none bash tools/gpu_var_bench.sh main nocomp nodma nostore > gpurun_out/d
 cat gpurun_out/decomp.txt
 timeout -k 10 120 python tools/copy_bw.py > gpurun_out/copy_bw.json 2>&1 || exit 1
 cat gpurun_out/copy_bw.json gpurun_out/host.txt
+# tail / prologue share: the paste launch at 64, 128 and 256 captures per launch
+for F in 128 256; do
+  timeout -k 10 200 python bench.py --blend none --frames $F --no-cpu-baseline > gpurun_out/frames_$F.log 2>&1 || exit 1
+  tail -1 gpurun_out/frames_$F.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('F=$F', d['value'], 'ms', d['ms_per_step'], d['kernels'])"
+done
+timeout -k 10 400 python -u -m pytest tests/test_gpu_blend.py -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_blend.log 2>&1; tail -3 gpurun_out/pytest_blend.log
