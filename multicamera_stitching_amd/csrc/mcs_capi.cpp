@@ -40,7 +40,8 @@ struct mcs_plan {
     // then the multi-band blend starts on side2 (ev_early) beside the rest of the streaming tiles
     hipEvent_t ev_early = nullptr;
     int *d_order = nullptr;
-    int n_early = 0;
+    int n_early = 0;              // launch-list items of the early launch (multi-band split)
+    int n_list = 0;               // items of the whole list (d_order; 0: none, grid order)
     // host path with frames off their calibrated size: upload buffers for the resize pre-pass
     uint8_t *d_raw[MCS_MAX_CAMS] = {};
     size_t raw_bytes[MCS_MAX_CAMS] = {};
@@ -324,6 +325,36 @@ void order_tiles(const mcs_plan *p, std::vector<int> &v)
     });
 }
 
+// Launch list of the streaming kernel for tiles in launch order (stream_tile deals a list to the
+// 8 XCDs in equal contiguous slices, each walked in order): per slice, the last
+// MCS_STREAM_TAIL tiles (default 96 = the slice's XCD's resident blocks: 32 CUs x 3) become
+// 4 items of a quarter of the captures each, ordered part by part, so the blocks that start last
+// on an XCD finish a quarter as long after the others; slices padded to one length with -1.
+std::vector<int> launch_list(const std::vector<int> &tiles)
+{
+    static const int tail = getenv("MCS_STREAM_TAIL") ? atoi(getenv("MCS_STREAM_TAIL")) : 96;
+    const size_t n = tiles.size(), per = (n + 7) / 8;
+    std::vector<std::vector<int>> sl(8);
+    for (size_t x = 0; x < 8; x++) {
+        const size_t b = std::min(n, x * per), e = std::min(n, (x + 1) * per);
+        const size_t k = std::min(e - b, (size_t)std::max(tail, 0));
+        for (size_t i = b; i < e - k; i++) sl[x].push_back(tiles[i]);
+        for (int part = 0; part < 4 && k > 0; part++)
+            for (size_t i = e - k; i < e; i++)
+                sl[x].push_back(tiles[i] | (part << mcs::kItemPartShift) |
+                                (2 << mcs::kItemLogShift));
+    }
+    size_t len = 0;
+    for (auto &v : sl) len = std::max(len, v.size());
+    std::vector<int> out;
+    out.reserve(8 * len);
+    for (auto &v : sl) {
+        v.resize(len, -1);
+        out.insert(out.end(), v.begin(), v.end());
+    }
+    return out;
+}
+
 // The band pass of a multi-band plan (after mb_prep): per (owner slot, blend-tile row) the
 // level-1 / level-2 mosaic columns the tiles of that row read from that owner (mb_prep's per-slot
 // ranges), merged where they overlap and covered by 64-column windows kMbBandStride apart; then
@@ -438,14 +469,17 @@ int prepare_bands(const Api *A, mcs_plan *p, const Kernels *k, hipStream_t s)
                 for (int tx = X0 / mcs::kTileW; tx <= x1 / mcs::kTileW; tx++)
                     early[(size_t)ty * p->gx + tx] = 1;
         }
-        std::vector<int> order, late;
-        order.reserve(early.size());
+        std::vector<int> first, late;
         for (size_t t = 0; t < early.size(); t++)
-            (early[t] ? order : late).push_back((int)t);
-        p->n_early = (int)order.size();
-        order_tiles(p, order);
+            (early[t] ? first : late).push_back((int)t);
+        order_tiles(p, first);
         order_tiles(p, late);
-        order.insert(order.end(), late.begin(), late.end());
+        std::vector<int> order = launch_list(first);
+        p->n_early = (int)order.size();
+        const std::vector<int> rest = launch_list(late);
+        order.insert(order.end(), rest.begin(), rest.end());
+        p->n_list = (int)order.size();
+        if (p->d_order) (void)A->hipFree(p->d_order);
         HIP_TRY(A->hipMalloc((void **)&p->d_order, order.size() * sizeof(int)));
         HIP_TRY(A->hipMemcpyAsync(p->d_order, order.data(), order.size() * sizeof(int),
                                   hipMemcpyHostToDevice, s));
@@ -570,7 +604,7 @@ void release_tables(const Api *A, mcs_plan *p)
                     (void *)p->d_bdesc, (void *)p->d_order})
         if (q) (void)A->hipFree(q);
     p->d_order = nullptr;
-    p->n_early = 0;
+    p->n_early = p->n_list = 0;
     p->d_bands = nullptr;
     p->d_tile_bt = nullptr;
     p->d_bdesc = nullptr;
@@ -654,16 +688,18 @@ int prepare(const Api *A, mcs_plan *p, hipStream_t s)
     HIP_TRY(A->hipMemcpyAsync(&nf, p->d_fallback, sizeof(int), hipMemcpyDeviceToHost, s));
     HIP_TRY(A->hipStreamSynchronize(s));
     p->n_fallback = nf;
-    if (!p->d_order && stream_order_mode() != 0) {
+    if (!p->d_order) {
         // one launch list of every tile (the multi-band split builds its own, early tiles first)
-        std::vector<int> order(tiles);
-        for (size_t t = 0; t < tiles; t++) order[t] = (int)t;
-        order_tiles(p, order);
+        std::vector<int> tl(tiles);
+        for (size_t t = 0; t < tiles; t++) tl[t] = (int)t;
+        order_tiles(p, tl);
+        const std::vector<int> order = launch_list(tl);
         HIP_TRY(A->hipMalloc((void **)&p->d_order, order.size() * sizeof(int)));
         HIP_TRY(A->hipMemcpyAsync(p->d_order, order.data(), order.size() * sizeof(int),
                                   hipMemcpyHostToDevice, s));
         HIP_TRY(A->hipStreamSynchronize(s));
         p->n_early = 0;
+        p->n_list = (int)order.size();
     }
     p->prepared = true;
     return MCS_OK;
@@ -789,13 +825,13 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
     args.pad_ = 0;
     args.pad2_ = 0;
     // 1-D grid dealt over the 8 XCDs; the kernel maps block -> tile (XCD-contiguous bands)
-    auto stream_launch = [&](const int *order, int n_tiles, unsigned lds) -> int {
+    auto stream_launch = [&](const int *order, int n_items, unsigned lds) -> int {
         args.order = order;
-        args.n_order = n_tiles;
+        args.n_order = n_items;
         size_t sz = sizeof(args);
         void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, (void *)&args, HIP_LAUNCH_PARAM_BUFFER_SIZE,
                        &sz, HIP_LAUNCH_PARAM_END};
-        const unsigned grid = 8u * (((unsigned)n_tiles + 7u) / 8u);
+        const unsigned grid = 8u * (((unsigned)n_items + 7u) / 8u);
         HIP_TRY(A->hipModuleLaunchKernel(k->stream[p->fd.channels][b32 ? 1 : 0], grid, 1, 1,
                                          mcs::kWave, mcs::kWavesPerBlock, 1,
                                          lds, s, nullptr, cfg));
@@ -820,8 +856,8 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
                          sizeof(m), p->side2);
         if (rc) return rc;
         HIP_TRY(A->hipEventRecord(p->ev_join2, p->side2));
-        if (n_tiles > p->n_early) {
-            rc = stream_launch(p->d_order + p->n_early, n_tiles - p->n_early,
+        if (p->n_list > p->n_early) {
+            rc = stream_launch(p->d_order + p->n_early, p->n_list - p->n_early,
                                std::max(lds, lds_late));
             if (rc) return rc;
         }
@@ -831,7 +867,8 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
     }
     {
         // (d_order: the tile order of prepare / prepare_bands; NULL: row-major grid order)
-        const int rc = stream_launch(p->d_order, n_tiles, lds);
+        const int rc = p->d_order ? stream_launch(p->d_order, p->n_list, lds)
+                                  : stream_launch(nullptr, n_tiles, lds);
         if (rc) return rc;
     }
     if (p->n_fallback > 0) HIP_TRY(A->hipStreamWaitEvent(s, p->ev_join, 0));

@@ -765,7 +765,15 @@ __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *til
     const int per = (n_order + 7) >> 3;
     const int idx = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
     if (idx >= n_order) return;
-    const int tile = order ? __builtin_amdgcn_readfirstlane(order[idx]) : idx;
+    // launch-list item: a tile and a share of the launch's captures (kItem*); -1 = padding
+    const int item = order ? __builtin_amdgcn_readfirstlane(order[idx]) : idx;
+    if (item < 0) return;
+    const int tile = item & kItemTileMask;
+    const int f_beg = (int)(((int64_t)((item >> kItemPartShift) & 15) * n_frames) >>
+                            ((item >> kItemLogShift) & 3));
+    const int f_end = (int)(((int64_t)(((item >> kItemPartShift) & 15) + 1) * n_frames) >>
+                            ((item >> kItemLogShift) & 3));
+    if (f_beg >= f_end) return;
     const int bx = tile % gx, by = tile / gx;
     // the tile header, copied once into LDS (the kernel also stores to global memory, so the
     // compiler cannot serve `tiles` from the scalar cache)
@@ -823,8 +831,8 @@ __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *til
     uint8_t *dst = P.out + (int64_t)min(y, P.out_h - 1) * P.out_pitch + (int64_t)xg * CN;
     const bool wide = npx == kPx && (((uintptr_t)dst | (uintptr_t)P.out_fstride) & 3) == 0;
     const int64_t fstride = P.cam_fstride[0];
-    for (int q = 0; q < ring - 1 && q < n_frames; q++)
-        stage_capture<BUF>(J, rs, ring0 + q * buf_bytes, (int64_t)q * fstride, lane);
+    for (int q = 0; q < ring - 1 && f_beg + q < f_end; q++)
+        stage_capture<BUF>(J, rs, ring0 + q * buf_bytes, (int64_t)(f_beg + q) * fstride, lane);
     wait_vmcnt_le(0);
     __builtin_amdgcn_s_barrier();
     // Steady state: waitn = DMA instructions this wave has certainly issued after those of
@@ -834,9 +842,9 @@ __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *til
     // out of order with respect to each other); the barrier makes it so for the block.  Tail
     // captures wait for everything.
     int slot_f = 0, slot_a = ring - 1;     // slots of capture f and of capture f + ring - 1
-    for (int f = 0; f < n_frames; f++) {
+    for (int f = f_beg; f < f_end; f++) {
         const int ahead = f + ring - 1;
-        const bool full = ahead < n_frames && !MCS_EXP_NODMA;
+        const bool full = ahead < f_end && !MCS_EXP_NODMA;
         if (full)
             stage_capture<BUF>(J, rs, ring0 + slot_a * buf_bytes, (int64_t)ahead * fstride, lane);
         const uint8_t *b = ring0 + slot_f * buf_bytes;

@@ -84,6 +84,14 @@ constexpr int kTileH = kWavesPerBlock * kRowsPerWave;
 constexpr int kTileCams = 4;       // cameras one LDS tile may draw from
 constexpr int kTilePx = kTileW * kTileH;
 constexpr int kDescWords = 3;
+// Launch-list items of the streaming kernel: tile index | part << kItemPartShift | log2(parts) <<
+// kItemLogShift -- the tile over captures [part * n / parts, (part + 1) * n / parts) of the
+// launch's n; -1 = padding.  The tiles that start last on each XCD are split into parts so the
+// launch's drain is short (tail items of a quarter of a tile's captures).
+constexpr int kItemTileMask = (1 << 24) - 1;
+constexpr int kItemPartShift = 24;
+constexpr int kItemLogShift = 28;
+
 // Compact per-pixel word the streaming kernel loads (4 B instead of 12): bits 0-15 the row-0
 // window's LDS address, 16-20 fx, 21-25 fy, 26-27 the camera's footprint slot in the tile header;
 // flags below.  A "plain" pixel (all taps in the image) has the weights of (fx, fy) and its row-1
@@ -288,10 +296,11 @@ constexpr int kJobsPerWave = MCS_JOBS_PER_WAVE;
 constexpr int kLdsSlack = 16;      // window reads run up to 8 bytes past a row's last byte
 constexpr int kMaxRing = 6;
 // LDS of a streaming block: the tile header, then a ring of capture footprints, as many slots
-// (2..kMaxRing) as fit.  Sized per channel count to the occupancy the kernel's registers allow:
-// 3 blocks per CU for 3-4 channels (52 KiB each of the CU's 160 KiB), 4 for 1-2 channels.
+// (2..kMaxRing) as fit.  3 blocks per CU (the kernel's registers allow 3 x 8 waves) at 40 KiB
+// each leave 40 KiB of the CU's 160 KiB for a multi-band blend block beside them (same-box A/B
+// against 52 KiB: paste launch 0.612 -> 0.605 ms, multi-band 0.963 -> 0.957 ms; round 3).
 #ifndef MCS_STREAM_LDS
-#define MCS_STREAM_LDS 53248
+#define MCS_STREAM_LDS 40960
 #endif
 constexpr int lds_stream_bytes(int cn) { return cn >= 3 ? MCS_STREAM_LDS : 40960; }
 constexpr int lds_ring_bytes(int cn) { return lds_stream_bytes(cn) - (int)sizeof(TileHdr); }

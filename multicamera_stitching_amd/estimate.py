@@ -99,18 +99,35 @@ class CaptureEstimator:
         self.ratio, self.thresh, self.iters, self.seed = ratio, reproj_thresh, iters, seed
         self.super_mode, self.interp, self.device = super_mode, interp, device
         self.pool = ThreadPoolExecutor(max_workers=threads or max(1, n_cams))
+        # ORB of the NEXT capture runs on its own pool while this one's pairs are matched,
+        # estimated and stitched (features_async: a two-stage software pipeline)
+        self.fpool = ThreadPoolExecutor(max_workers=threads or max(1, n_cams))
+        self.ahead = ThreadPoolExecutor(max_workers=1)
         self.last_H = [None] * (n_cams - 1)
         self.stats = {}
 
     def close(self):
+        self.ahead.shutdown()
+        self.fpool.shutdown()
         self.pool.shutdown()
 
-    def features(self, frame_ptrs):
+    def features(self, frame_ptrs, pool=None):
         """ORB of every camera frame (device pointers, dense h x w x C, producers finished)."""
         nf, nl, sf, ft = self.orb
-        return list(self.pool.map(
+        return list((pool or self.pool).map(
             lambda p: _capi.orb_detect_device(p, self.w, self.h, self.c, nf, nl, sf, ft,
                                               self.device), frame_ptrs))
+
+    def features_async(self, frame_ptrs, ready=None):
+        """Future of features(frame_ptrs) on the look-ahead pools: `ready()` (e.g. the upload
+        event's synchronize) runs first on that thread.  The caller meanwhile runs
+        estimate_from() / stitch() of the previous capture; the frames must stay untouched until
+        the future is done."""
+        def run():
+            if ready is not None:
+                ready()
+            return self.features(frame_ptrs, self.fpool)
+        return self.ahead.submit(run)
 
     def pair_homography(self, fa, fb):
         """Camera A -> camera B (A = query, as matchKeypoints' ptsA): H or None, matches,
@@ -129,7 +146,10 @@ class CaptureEstimator:
     def estimate(self, frame_ptrs):
         """Pair homographies of one capture (camera k+1 -> camera k); a failed pair keeps the
         previous capture's estimate."""
-        feats = self.features(frame_ptrs)
+        return self.estimate_from(self.features(frame_ptrs))
+
+    def estimate_from(self, feats):
+        """estimate() from the capture's features (features / features_async)."""
         res = list(self.pool.map(lambda k: self.pair_homography(feats[k + 1], feats[k]),
                                  range(self.n_cams - 1)))
         pair_H = []

@@ -103,6 +103,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--stitch", action="store_true",
                     help="estimate -> stitch per capture (estimate.py, mcs_stitch_direct)")
+    ap.add_argument("--overlap", action="store_true",
+                    help="with --pipelined: ORB of capture f+1 beside the pairs + stitch of f")
     ap.add_argument("--pipelined", action="store_true",
                     help="with --stitch: upload capture f+1 (pinned host frames, own stream, two "
                          "device frame sets) while capture f is estimated and stitched")
@@ -273,12 +275,23 @@ def pipelined_main(args, frames, truth, W, Hh, N):
     def run(n):
         mpix = 0.0
         upload(0)
+        fut = est.features_async(ptrs[0], ev_up[0].synchronize) if args.overlap else None
         for i in range(n):
             slot = i & 1
-            if i + 1 < n:
-                upload(slot ^ 1)
-            ev_up[slot].synchronize()             # this capture's frames are on the device
-            pair_H = est.estimate(ptrs[slot])
+            if args.overlap:
+                # two-stage pipeline: the ORB of capture i+1 (its frames uploaded into the other
+                # set once that set's previous stitch is done) runs while capture i's pairs are
+                # matched, estimated and stitched
+                feats = fut.result()
+                if i + 1 < n:
+                    upload(slot ^ 1)
+                    fut = est.features_async(ptrs[slot ^ 1], ev_up[slot ^ 1].synchronize)
+                pair_H = est.estimate_from(feats)
+            else:
+                if i + 1 < n:
+                    upload(slot ^ 1)
+                ev_up[slot].synchronize()             # this capture's frames are on the device
+                pair_H = est.estimate(ptrs[slot])
             if pending[slot] is not None:         # the set's previous plan: its stitch is done
                 ev_done[slot].synchronize()
                 pending[slot].close()
