@@ -291,7 +291,8 @@ void band_args(const mcs_plan *p, const mcs::KParams &P, mcs::KMbBandArgs &a)
 }
 
 // Grid width of a band launch of n bands (XCD-contiguous mapping: padded to a multiple of 8).
-// MCS_MB_BAND_XCD=0 / 1: the mapping (KMbBandArgs::xcd).
+// MCS_MB_BAND_XCD=0 / 1: the mapping (KMbBandArgs::xcd; default 0 -- measured within noise,
+// multi-band launch 0.963 ms either way).
 unsigned band_grid(mcs::KMbBandArgs &b, int n)
 {
     static const bool xcd = getenv("MCS_MB_BAND_XCD") && strcmp(getenv("MCS_MB_BAND_XCD"), "0");
@@ -326,13 +327,15 @@ void order_tiles(const mcs_plan *p, std::vector<int> &v)
 }
 
 // Launch list of the streaming kernel for tiles in launch order (stream_tile deals a list to the
-// 8 XCDs in equal contiguous slices, each walked in order): per slice, the last
-// MCS_STREAM_TAIL tiles (default 96 = the slice's XCD's resident blocks: 32 CUs x 3) become
-// 4 items of a quarter of the captures each, ordered part by part, so the blocks that start last
-// on an XCD finish a quarter as long after the others; slices padded to one length with -1.
+// 8 XCDs in equal contiguous slices, each walked in order): per slice, the last MCS_STREAM_TAIL
+// tiles (experiment knob, default 0 = off) become 4 items of a quarter of the captures each,
+// ordered part by part, so the blocks that start last on an XCD finish a quarter as long after
+// the others; slices padded to one length with -1.  Measured (same box, two alternations): 96
+// tail tiles per XCD -- paste within noise (0.596 vs 0.596 ms), multi-band 2-3 % slower (0.947
+// -> 0.978 ms: its early list, split too, runs longer); 48 -- paste -0.8 %, multi-band +2 %.
 std::vector<int> launch_list(const std::vector<int> &tiles)
 {
-    static const int tail = getenv("MCS_STREAM_TAIL") ? atoi(getenv("MCS_STREAM_TAIL")) : 96;
+    static const int tail = getenv("MCS_STREAM_TAIL") ? atoi(getenv("MCS_STREAM_TAIL")) : 0;
     const size_t n = tiles.size(), per = (n + 7) / 8;
     std::vector<std::vector<int>> sl(8);
     for (size_t x = 0; x < 8; x++) {
