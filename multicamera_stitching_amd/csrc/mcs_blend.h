@@ -1359,20 +1359,20 @@ __device__ __forceinline__ void mb_bands(const KMbBandArgs &a, int bl)
     // The 12-row body makes every buffer and accumulator index a compile-time constant, so no
     // register copy ever reads an in-flight load (such a copy makes the compiler drain all loads
     // at the loop's back edge).
-    constexpr int NB = kMbBandBufs, A = kMbBandAhead;
-    uint64_t dq[NB];
+    constexpr int NB = kMbBandBufs, A = kMbBandAhead, ND = kMbBandDescRing;
+    uint64_t dq[ND];
     uint2 wq0[NB][FR], wq1[NB][FR];
 #pragma unroll
-    for (int i = 0; i < NB; i++) dq[i] = dsc[i * kMbBandLanes];
+    for (int i = 0; i < ND; i++) dq[i] = dsc[i * kMbBandLanes];
 #pragma unroll
     for (int i = 0; i < A; i++) load_win(dq[i], wq0[i], wq1[i]);
     for (int r12 = 0; r12 < kMbBandRows; r12 += 12) {
         static_for<12>([&](auto PHc) {
             constexpr int ph = decltype(PHc)::value;
             const int r = r12 + ph;
-            constexpr int b0 = ph % NB, bA = (ph + A) % NB;
+            constexpr int b0 = ph % NB, bA = (ph + A) % NB, d0 = ph % ND, dA = (ph + A) % ND;
             uint32_t wa, wb;
-            const uint32_t meta = (uint32_t)(dq[b0] >> 32), dd = (meta >> 12) & 7u;
+            const uint32_t meta = (uint32_t)(dq[d0] >> 32), dd = (meta >> 12) & 7u;
             mb_weights(meta, wa, wb);
             uint32_t v[FR];
 #pragma unroll
@@ -1385,8 +1385,8 @@ __device__ __forceinline__ void mb_bands(const KMbBandArgs &a, int bl)
             // the previous row's finished entries (after this row's window wait), then the loads:
             // windows of row r + A (its descriptor arrived a row ago), descriptor of row r + A + 1
             flush();
-            load_win(dq[bA], wq0[bA], wq1[bA]);
-            dq[b0] = dsc[(r + NB) * kMbBandLanes];
+            load_win(dq[dA], wq0[bA], wq1[bA]);
+            dq[d0] = dsc[(r + ND) * kMbBandLanes];
             // level-0 row r = 2k + (ph & 1), k % 3 = K3; level-1 row k - 2 = 2m + P2, m % 3 = M3
             constexpr int K3 = (ph / 2) % 3;
             constexpr int q = ph / 2 - 2, P2 = q & 1, M3 = ((q - P2) / 2 + 3) % 3;

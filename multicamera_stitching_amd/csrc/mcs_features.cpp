@@ -23,6 +23,7 @@ struct FeatureKernels {
     hipFunction_t knn2 = nullptr, knn2_finalize = nullptr;
     hipFunction_t ransac_score = nullptr, ransac_mask = nullptr;
     hipFunction_t orb_gray = nullptr, orb_level = nullptr, orb_describe = nullptr;
+    hipFunction_t orb_pyramid = nullptr;
     hipFunction_t orb_select = nullptr;
     hipFunction_t l2_prep = nullptr, l2_i8 = nullptr, l2_f32 = nullptr, l2_finalize = nullptr;
 };
@@ -81,6 +82,7 @@ int feature_kernels(const Api *A, int device, const FeatureKernels **out)
             const char *name;
             hipFunction_t *f;
         } orb[] = {{"mcs_orb_gray", &k.orb_gray},     {"mcs_orb_level", &k.orb_level},
+                   {"mcs_orb_pyramid", &k.orb_pyramid},
                    {"mcs_orb_describe", &k.orb_describe},
                    {"mcs_orb_select", &k.orb_select},
                    {"mcs_l2_prep", &k.l2_prep},       {"mcs_l2_knn2_i8", &k.l2_i8},
@@ -421,6 +423,64 @@ int mcs_ransac_homography_host(const float *src_xy, const float *dst_xy, int n, 
     return MCS_OK;
 }
 
+// Source index of destination index d in OpenCV's resize(INTER_LINEAR) (mcs_orb_pyramid's
+// pyr_axis, the same float arithmetic).
+static int pyr_src(int d, double scale, int ssize, bool is_x)
+{
+    float f = (float)((d + 0.5) * scale - 0.5);
+    int si = (int)std::floor(f);
+    if (is_x) {
+        if (si < 0) si = 0;
+        if (si >= ssize - 1) si = ssize - 1;
+    }
+    return si;
+}
+
+// mcs_orb_pyramid's arguments: last-level tiles of 32 x 16 (8 x 8 for small levels), the LDS
+// buffer size from every block's dependency regions (the kernel's top-down walk, on the host).
+// Returns the block count, 0 when the fused launch does not apply (a >= 2x level step, or
+// regions too large for LDS).
+static unsigned pyramid_args(const int *lw, const int *lh, int nlevels, const size_t *off,
+                             uint8_t *lvl, mcs::KOrbBuildArgs &a)
+{
+    std::memset(&a, 0, sizeof(a));
+    const int L = nlevels - 1;
+    for (int l = 1; l <= L; l++) {
+        if (2 * lw[l] <= lw[l - 1] || 2 * lh[l] <= lh[l - 1]) return 0;
+        a.sx[l] = 1. / ((double)lw[l] / lw[l - 1]);
+        a.sy[l] = 1. / ((double)lh[l] / lh[l - 1]);
+    }
+    for (int l = 0; l <= L; l++) {
+        a.off[l] = (int64_t)off[l];
+        a.w[l] = lw[l];
+        a.h[l] = lh[l];
+    }
+    a.lvl = lvl;
+    a.nlevels = nlevels;
+    a.tw = lw[L] >= 256 ? 32 : 8;
+    a.th = lw[L] >= 256 ? 16 : 8;
+    a.gx = (lw[L] + a.tw - 1) / a.tw;
+    const int gy = (lh[L] + a.th - 1) / a.th;
+    int mw = 1, mh = 1;
+    for (int t = 0; t < a.gx * gy; t++) {
+        int x0 = (t % a.gx) * a.tw, y0 = (t / a.gx) * a.th;
+        int x1 = std::min(x0 + a.tw, lw[L]), y1 = std::min(y0 + a.th, lh[L]);
+        for (int l = L; l >= 2; l--) {
+            const int sw = lw[l - 1], sh = lh[l - 1];
+            const int nx0 = pyr_src(x0, a.sx[l], sw, true), sxl = pyr_src(x1 - 1, a.sx[l], sw, true);
+            const int nx1 = sxl >= sw - 1 ? sw : sxl + 2;
+            const int ny0 = std::min(std::max(pyr_src(y0, a.sy[l], sh, false), 0), sh - 1);
+            const int ny1 = std::min(std::max(pyr_src(y1 - 1, a.sy[l], sh, false) + 1, 0), sh - 1) + 1;
+            x0 = nx0, x1 = nx1, y0 = ny0, y1 = ny1;
+            if (l - 1 >= 1 && l - 1 < L) mw = std::max(mw, x1 - x0), mh = std::max(mh, y1 - y0);
+        }
+    }
+    a.lds_w = mw;
+    a.lds_h = mh;
+    if (2 * (size_t)mw * mh > 64 * 1024) return 0;
+    return (unsigned)(a.gx * gy);
+}
+
 namespace {
 // ORB of one image (host memory, or device memory when on_device); mcs_orb_detect_host /
 // mcs_orb_detect_device below.
@@ -525,10 +585,26 @@ int orb_detect(const uint8_t *image, bool on_device, int w, int h, int channels,
             e = A->hipMemcpyAsync(lvl0, in, in_bytes, hipMemcpyDeviceToDevice, s);
         }
     }
-    for (int l = 1; l < nlevels && e == hipSuccess && rc == MCS_OK; l++)
-        rc = mcs_resize_linear_device(buf + o_lvl + off[l - 1], lw[l - 1], lh[l - 1], lw[l - 1],
-                                      0, buf + o_lvl + off[l], lw[l], lh[l], lw[l], 0, 1, 1,
-                                      device, s);
+    // levels 1 .. nlevels-1: one launch (mcs_orb_pyramid) when every level is a < 2x
+    // downscale of the one before (its blocks' dependency regions then tile every level), else
+    // (or MCS_ORB_PYRAMID=0) one resize launch per level
+    mcs::KOrbBuildArgs ba;
+    static const bool fused_on = !getenv("MCS_ORB_PYRAMID") || strcmp(getenv("MCS_ORB_PYRAMID"), "0");
+    const unsigned pyr_blocks = fused_on && e == hipSuccess && rc == MCS_OK && nlevels > 1
+                                    ? pyramid_args(lw, lh, nlevels, off, buf + o_lvl, ba)
+                                    : 0u;
+    if (pyr_blocks > 0) {
+        size_t sz = sizeof(ba);
+        void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &ba, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz,
+                       HIP_LAUNCH_PARAM_END};
+        e = A->hipModuleLaunchKernel(k->orb_pyramid, pyr_blocks, 1, 1, 256, 1, 1,
+                                     (unsigned)(2 * ba.lds_w * ba.lds_h), s, nullptr, cfg);
+    } else {
+        for (int l = 1; l < nlevels && e == hipSuccess && rc == MCS_OK; l++)
+            rc = mcs_resize_linear_device(buf + o_lvl + off[l - 1], lw[l - 1], lh[l - 1],
+                                          lw[l - 1], 0, buf + o_lvl + off[l], lw[l], lh[l], lw[l],
+                                          0, 1, 1, device, s);
+    }
     if (e == hipSuccess && rc == MCS_OK) {
         // blur, FAST, NMS and Harris of every level: one launch (mcs_orb_level, 64 x 16 tiles)
         mcs::KOrbPyrArgs pa;

@@ -4,8 +4,11 @@
 // Brute-force Hamming kNN-2 (NS-4; BFMatcher(NORM_HAMMING).knnMatch(k=2), the reference's matcher
 // at StitcherClass.py:405-448 with binary descriptors).  VALU popcount-bound: per (query, train)
 // pair 8 v_xor_b32 + 8 v_bcnt_u32_b32 (accumulating) + 3 min/max for the running top-2, with
-// no HBM traffic to speak of (train descriptors are wave-uniform: scalar loads, one per 32 B,
-// shared by the 64 queries of a wave).
+// no HBM traffic to speak of.  The wave's train chunk is staged in LDS, 64 descriptors per pass
+// (one coalesced 32-byte load per lane), and every lane reads the same descriptor back
+// (ds_read_b128 broadcast, no bank conflict): no per-descriptor scalar-load round trip in the
+// compare loop (the round-2 form, wave-uniform s_load_dwordx8 per descriptor, was latency-bound:
+// VALU active 0.18).
 //
 // Top-2 order = OpenCV's: a train descriptor enters only with a strictly smaller distance, so
 // among equal distances the earlier train index wins.  Encoded as key = distance << 23 | index:
@@ -31,12 +34,13 @@ __device__ __forceinline__ void top2(uint32_t &k0, uint32_t &k1, uint32_t k)
     k0 = min(k0, k);
 }
 
-__device__ __forceinline__ uint32_t hamming(const uint32_t (&q)[8], const uint32_t *__restrict__ t)
+// Hamming distance of query q to a train descriptor staged in LDS (two 16-byte broadcast reads;
+// v_bcnt_u32_b32 accumulates).
+__device__ __forceinline__ uint32_t hamming_lds(const uint32_t (&q)[8], const uint4 *t)
 {
-    uint32_t c = 0;
-#pragma unroll
-    for (int i = 0; i < 8; i++) c += __popc(q[i] ^ t[i]);   // v_bcnt_u32_b32 accumulates
-    return c;
+    const uint4 a = t[0], b = t[1];
+    return __popc(q[0] ^ a.x) + __popc(q[1] ^ a.y) + __popc(q[2] ^ a.z) + __popc(q[3] ^ a.w) +
+           __popc(q[4] ^ b.x) + __popc(q[5] ^ b.y) + __popc(q[6] ^ b.z) + __popc(q[7] ^ b.w);
 }
 
 }  // namespace mcs
@@ -52,17 +56,31 @@ extern "C" __global__ __launch_bounds__(64) void mcs_hamming_knn2(const mcs::KHa
     d[0] = v0.x, d[1] = v0.y, d[2] = v0.z, d[3] = v0.w;
     d[4] = v1.x, d[5] = v1.y, d[6] = v1.z, d[7] = v1.w;
     const int j0 = blockIdx.y * a.per_chunk, j1 = min(a.nt, j0 + a.per_chunk);
-    const uint32_t *__restrict__ train = a.train;
+    const uint4 *__restrict__ train4 = reinterpret_cast<const uint4 *>(a.train);
+    __shared__ uint4 tl[2 * kKnnQueriesPerBlock];
     uint32_t k0 = kKeyNone, k1 = kKeyNone;
-    int j = j0;
-    for (; j + 4 <= j1; j += 4) {
-        uint32_t c[4];
+    for (int jt = j0; jt < j1; jt += kKnnQueriesPerBlock) {
+        const int n = min(kKnnQueriesPerBlock, j1 - jt);
+        if ((int)threadIdx.x < n) {
+            const uint4 *src = train4 + (int64_t)(jt + threadIdx.x) * 2;
+            const uint4 t0 = src[0], t1 = src[1];
+            tl[2 * threadIdx.x] = t0;
+            tl[2 * threadIdx.x + 1] = t1;
+        }
+        __syncthreads();
+        int u = 0;
+        for (; u + 4 <= n; u += 4) {
+            uint32_t c[4];
 #pragma unroll
-        for (int u = 0; u < 4; u++) c[u] = hamming(d, train + (int64_t)(j + u) * 8);
+            for (int v = 0; v < 4; v++) c[v] = hamming_lds(d, tl + 2 * (u + v));
 #pragma unroll
-        for (int u = 0; u < 4; u++) top2(k0, k1, (c[u] << kKnnKeyShift) | (uint32_t)(j + u));
+            for (int v = 0; v < 4; v++)
+                top2(k0, k1, (c[v] << kKnnKeyShift) | (uint32_t)(jt + u + v));
+        }
+        for (; u < n; u++)
+            top2(k0, k1, (hamming_lds(d, tl + 2 * u) << kKnnKeyShift) | (uint32_t)(jt + u));
+        __syncthreads();
     }
-    for (; j < j1; j++) top2(k0, k1, (hamming(d, train + (int64_t)j * 8) << kKnnKeyShift) | j);
     if (q >= a.nq) return;
     const uint32_t old = atomicMin(&a.keys[2 * q], k0);
     atomicMin(&a.keys[2 * q + 1], max(old, k0));
@@ -573,5 +591,80 @@ extern "C" __global__ __launch_bounds__(64) void mcs_orb_describe(const mcs::KOr
     if (lane == 0) {
         a.orient[2 * k] = cs;
         a.orient[2 * k + 1] = sn;
+    }
+}
+
+// ---- ORB pyramid in one launch ----------------------------------------------------------------
+namespace mcs {
+
+// OpenCV 3.4 resize(INTER_LINEAR) source index and 11-bit coefficients of destination index d
+// (the float arithmetic of mcs_kernels.hip resize_axis / oracle/orc_resize.c).
+__device__ __forceinline__ void pyr_axis(int d, double scale, int ssize, bool is_x, int &s,
+                                         int &c0, int &c1)
+{
+    float f = (float)((d + 0.5) * scale - 0.5);
+    int si = (int)floorf(f);
+    f -= (float)si;
+    if (is_x) {
+        if (si < 0) f = 0.f, si = 0;
+        if (si >= ssize - 1) f = 0.f, si = ssize - 1;
+    }
+    s = si;
+    c0 = __float2int_rn((1.f - f) * 2048.f);
+    c1 = __float2int_rn(f * 2048.f);
+}
+
+}  // namespace mcs
+
+extern "C" __global__ __launch_bounds__(256) void mcs_orb_pyramid(const mcs::KOrbBuildArgs a)
+{
+    using namespace mcs;
+    extern __shared__ uint8_t pyr_lds[];
+    const int L = a.nlevels - 1, tid = threadIdx.x;
+    const int t = blockIdx.x, tx = t % a.gx, ty = t / a.gx;
+    // regions [x0, x1) x [y0, y1) of every level, top down (block-uniform)
+    int x0[12], x1[12], y0[12], y1[12];
+    x0[L] = tx * a.tw;
+    y0[L] = ty * a.th;
+    x1[L] = min(x0[L] + a.tw, a.w[L]);
+    y1[L] = min(y0[L] + a.th, a.h[L]);
+    for (int l = L; l >= 2; l--) {
+        int s, c0, c1;
+        const int sw = a.w[l - 1], sh = a.h[l - 1];
+        pyr_axis(x0[l], a.sx[l], sw, true, s, c0, c1);
+        x0[l - 1] = s;
+        pyr_axis(x1[l] - 1, a.sx[l], sw, true, s, c0, c1);
+        x1[l - 1] = s >= sw - 1 ? sw : s + 2;
+        pyr_axis(y0[l], a.sy[l], sh, false, s, c0, c1);
+        y0[l - 1] = min(max(s, 0), sh - 1);
+        pyr_axis(y1[l] - 1, a.sy[l], sh, false, s, c0, c1);
+        y1[l - 1] = min(max(s + 1, 0), sh - 1) + 1;
+    }
+    uint8_t *buf[2] = {pyr_lds, pyr_lds + a.lds_w * a.lds_h};
+    for (int l = 1; l <= L; l++) {
+        const int rw = x1[l] - x0[l], rh = y1[l] - y0[l];
+        const int sw = a.w[l - 1], sh = a.h[l - 1];
+        // source: level 0 in global memory, else the previous region in LDS
+        const uint8_t *src = l == 1 ? a.lvl + a.off[0] : buf[(l - 1) & 1];
+        const int spitch = l == 1 ? sw : x1[l - 1] - x0[l - 1];
+        const int sx0 = l == 1 ? 0 : x0[l - 1], sy0 = l == 1 ? 0 : y0[l - 1];
+        uint8_t *dst = buf[l & 1];
+        uint8_t *out = a.lvl + a.off[l];
+        for (int i = tid; i < rw * rh; i += 256) {
+            const int x = x0[l] + i % rw, y = y0[l] + i / rw;
+            int s, a0, a1, sy, b0, b1;
+            pyr_axis(x, a.sx[l], sw, true, s, a0, a1);
+            pyr_axis(y, a.sy[l], sh, false, sy, b0, b1);
+            const int r0 = min(max(sy, 0), sh - 1), r1 = min(max(sy + 1, 0), sh - 1);
+            const uint8_t *p0 = src + (int64_t)(r0 - sy0) * spitch + (s - sx0);
+            const uint8_t *p1 = src + (int64_t)(r1 - sy0) * spitch + (s - sx0);
+            const bool one = s >= sw - 1;
+            const int d0 = one ? p0[0] * 2048 : p0[0] * a0 + p0[1] * a1;
+            const int d1 = one ? p1[0] * 2048 : p1[0] * a0 + p1[1] * a1;
+            const uint8_t v = (uint8_t)((((b0 * (d0 >> 4)) >> 16) + ((b1 * (d1 >> 4)) >> 16) + 2) >> 2);
+            if (l < L) dst[i] = v;
+            out[(int64_t)y * a.w[l] + x] = v;
+        }
+        __syncthreads();
     }
 }

@@ -80,6 +80,20 @@ struct KOrbPyrArgs {
     int coff[12], w[12], h[12], cap[12], bstart[13];
     int nlevels, threshold;
 };
+// The ORB pyramid in one launch (mcs_orb_pyramid): levels 1 .. nlevels-1, each OpenCV's
+// resize(INTER_LINEAR) of the level before it.  One block per tw x th tile of the LAST level;
+// the block derives, top down, the region of every level that tile depends on (a level-l
+// region = the source span of the level-(l+1) region), then computes them bottom up in LDS
+// (ping-pong buffers of lds_w x lds_h bytes), writing every computed pixel to its level image.
+// Neighbouring blocks' regions overlap by a pixel or two: those pixels are written twice with
+// the same value.  Level l lives at lvl + off[l]; sx / sy = OpenCV's 1 / (dst / src) per level.
+struct KOrbBuildArgs {
+    uint8_t *lvl;
+    int64_t off[12];
+    double sx[12], sy[12];
+    int w[12], h[12];
+    int nlevels, tw, th, gx, lds_w, lds_h;
+};
 struct KOrbDescArgs {
     const uint8_t *img[12], *blur[12];
     int w[12];

@@ -252,7 +252,17 @@ constexpr int kMbBandRows = (kMbUsedY + 11) / 12 * 12;
 constexpr int kMbBandAhead = MCS_MB_BAND_AHEAD;
 constexpr int kMbBandBufs = kMbBandAhead + 1;
 static_assert(12 % kMbBandBufs == 0, "band pass: buffers must divide the 12-row body");
-constexpr int kMbBandDescRows = kMbBandRows + kMbBandBufs;
+// descriptor ring of the band pass: the descriptor of row r + kMbBandDescRing - 1 is loaded at row
+// r and first used at row r + kMbBandDescRing - 1 - kMbBandAhead (to issue that row's window
+// loads), so a ring deeper than the window buffers gives the dependent descriptor -> window
+// loads more than one row of slack
+#ifndef MCS_MB_DESC_RING
+#define MCS_MB_DESC_RING 3
+#endif
+constexpr int kMbBandDescRing = MCS_MB_DESC_RING;
+static_assert(12 % kMbBandDescRing == 0 && kMbBandDescRing >= kMbBandBufs,
+              "band pass: descriptor ring must divide the 12-row body and hold the window rows");
+constexpr int kMbBandDescRows = kMbBandRows + kMbBandDescRing;
 constexpr int kMbBandStride = 52;  // window step: consecutive windows' level-2 outputs abut
 #ifndef MCS_MB_BAND_FRAMES
 #define MCS_MB_BAND_FRAMES 2
