@@ -574,15 +574,13 @@ def cpu_baseline(runner, cams, args, out_w, out_h, host):
         lines.append(head)
         lines.append(_time_line(run, cams, 1, sec / 2, mpix, what))
         if runner["cascade"] is not None and runner["cascade"] is not runner["workload"]:
-            lines.append(_time_line(*runner["cascade"][:1], cams, n_all, sec / 2, mpix,
+            # (blend workloads: the reference-structured paste cascade beside them)
+            lines.append(_time_line(runner["cascade"][0], cams, n_all, sec / 2, mpix,
                                     runner["cascade"][1]))
-            lines.append(_time_line(*runner["cascade"][:1], cams, 1, sec / 2, mpix,
-                                    runner["cascade"][1]))
-        elif runner["cascade"] is not None:
-            lines.append(_time_line(*runner["cascade"][:1], cams, 1, sec / 2, mpix,
+            lines.append(_time_line(runner["cascade"][0], cams, 1, sec / 2, mpix,
                                     runner["cascade"][1]))
         if runner["flat"] is not None:
-            lines.append(_time_line(*runner["flat"][:1], cams, n_all, sec / 2, mpix,
+            lines.append(_time_line(runner["flat"][0], cams, n_all, sec / 2, mpix,
                                     runner["flat"][1]))
     return {
         "value": head["value"],

@@ -1,6 +1,7 @@
 """Per-dispatch statistics of the bench's TIMED launches from a rocprofv3 kernel trace.
 
-    python tools/trace_stats.py <rocprofv3 output dir> [--bench-line line.json] [--out x.json]
+    python tools/trace_stats.py <rocprofv3 output dir | kernel_trace.csv> [--bench-line line.json]
+                                [--out x.json]
 
 The bench run must set MCS_BENCH_MARKERS=1: bench.py then launches a tiny spin kernel on its
 stream right before the first and right after the last timed launch of the main plan, and the
@@ -24,8 +25,11 @@ HBM_PEAK = 8000.0
 
 
 def load(d):
+    """Dispatches (start, end, name) of a rocprofv3 output directory or one kernel_trace.csv."""
     rows = []
-    for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
+    files = [d] if os.path.isfile(d) else glob.glob(os.path.join(d, "**", "*kernel_trace.csv"),
+                                                     recursive=True)
+    for f in files:
         for r in csv.DictReader(open(f)):
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
