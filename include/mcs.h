@@ -327,6 +327,34 @@ int mcs_ransac_homography_host(const float *src_xy, const float *dst_xy, int n, 
 int mcs_homography_refine_host(const float *src_xy, const float *dst_xy, int n,
                                const uint8_t *mask, double *H);
 
+/* ---- A whole rig capture ---------------------------------------------------
+ * Per capture, detectAndDescribe + matchKeypoints (StitcherClass.py:356-448) of every adjacent
+ * camera pair, made per-frame by config 3: ORB of the n_cams device frames (dense w x h x
+ * channels, sorted-label order), then per pair k (camera k+1 -> camera k: query k+1, train k)
+ * BF Hamming kNN-2, Lowe's ratio (m0 < ratio * m1, strict), more than 4 matches, RANSAC + LM
+ * (mcs_ransac_homography_host with thresh / iters / seed).  A job runs on libmcs's worker
+ * threads: the whole capture as one launch chain on the job's stream (ORB batched over the
+ * cameras, the pairs' matching, ratio test, RANSAC and best model batched over the pairs, one
+ * copy back; the host runs only the LM refinement), or per-call steps for a capture whose ORB
+ * ranking overflowed on the device.  submit returns at once, wait blocks for the result, so a
+ * caller with several jobs overlaps one capture's estimation with another's.  wait_event (a
+ * hipEvent_t or NULL): the frames' producer; the job's streams wait for it on the GPU.  Replaces the per-capture
+ * Python loop over StitcherBase.detectAndDescribe / matchKeypoints (StitcherClass.py:356-448)
+ * for config 3.  Results: H (n_cams - 1) x 9 row-major (0 where ok[k] = 0: the reference's
+ * H = None), per camera keypoints, per pair ratio-test matches and RANSAC inliers (each may be
+ * NULL).  A job holds one capture at a time; destroy waits for a running one. */
+typedef struct mcs_rig_job mcs_rig_job;
+int mcs_rig_job_create(int n_cams, int w, int h, int channels, int nfeatures, int nlevels,
+                       float scale_factor, int fast_threshold, float ratio, double reproj_thresh,
+                       int iters, uint32_t seed, int device, mcs_rig_job **out);
+int mcs_rig_job_submit(mcs_rig_job *job, const uint8_t *const *d_frames, void *wait_event);
+int mcs_rig_job_wait(mcs_rig_job *job, double *H, int *ok, int *n_keypoints, int *n_matches,
+                     int *n_inliers);
+/* Captures the job finished on the device path (one launch chain) and on the per-call path (a
+ * device ranking overflow, or MCS_RIG_PATH=calls). */
+int mcs_rig_job_counts(const mcs_rig_job *job, int *device_captures, int *call_captures);
+int mcs_rig_job_destroy(mcs_rig_job *job);
+
 /* ---- Multi-GPU group ---------------------------------------------------
  * One process per GPU of a node.  Rig captures are independent (capture f -> rank f mod N, each
  * rank stitching with its own plan, no collective in the stitch itself); the one collective is

@@ -46,7 +46,8 @@ EXPORTS = (
     "mcs_undistort_map_host", "mcs_match_l2_knn2", "mcs_match_l2_knn2_host",
     "mcs_stream_submit_strided", "mcs_build_id", "mcs_homography_refine_host", "mcs_stream_output",
     "mcs_stitch_direct", "mcs_orb_detect_device", "mcs_group_unique_id", "mcs_group_create",
-    "mcs_group_gather", "mcs_group_destroy", "mcs_rccl_library",
+    "mcs_group_gather", "mcs_group_destroy", "mcs_rccl_library", "mcs_rig_job_create",
+    "mcs_rig_job_submit", "mcs_rig_job_wait", "mcs_rig_job_counts", "mcs_rig_job_destroy",
 )
 MCS_GROUP_ID_BYTES = 128
 
@@ -205,6 +206,18 @@ def load() -> ctypes.CDLL:
         L.mcs_orb_detect_host.restype = I
         L.mcs_orb_detect_device.argtypes = L.mcs_orb_detect_host.argtypes
         L.mcs_orb_detect_device.restype = I
+        L.mcs_rig_job_create.argtypes = [I, I, I, I, I, I, ctypes.c_float, I, ctypes.c_float,
+                                         ctypes.c_double, I, ctypes.c_uint32, I,
+                                         ctypes.POINTER(P)]
+        L.mcs_rig_job_create.restype = I
+        L.mcs_rig_job_submit.argtypes = [P, P, P]
+        L.mcs_rig_job_submit.restype = I
+        L.mcs_rig_job_wait.argtypes = [P, P, P, P, P, P]
+        L.mcs_rig_job_wait.restype = I
+        L.mcs_rig_job_counts.argtypes = [P, P, P]
+        L.mcs_rig_job_counts.restype = I
+        L.mcs_rig_job_destroy.argtypes = [P]
+        L.mcs_rig_job_destroy.restype = I
         L.mcs_plan_set_blend.argtypes = [P, I]
         L.mcs_plan_create_cylindrical.argtypes = [ctypes.POINTER(CylCamera), I, I, I,
                                                   ctypes.c_double, ctypes.c_double,
@@ -764,6 +777,60 @@ def orb_detect_device(ptr: int, w: int, h: int, channels: int, nfeatures: int = 
                                   desc.ctypes.data, ctypes.byref(n), device))
     k = n.value
     return dict(xy=xy[:k], response=resp[:k], angle=ang[:k], level=lvl[:k], desc=desc[:k])
+
+
+class RigJob:
+    """mcs_rig_job: the per-capture estimation of config 3 (ORB of every camera, then BF Hamming
+    kNN-2 + ratio + RANSAC/LM per adjacent pair) on libmcs's worker threads.  submit() returns at
+    once; wait() gives (H list with None for failed pairs, stats dict)."""
+
+    def __init__(self, n_cams: int, w: int, h: int, channels: int = 3, nfeatures: int = 2000,
+                 nlevels: int = 8, scale_factor: float = 1.2, fast_threshold: int = 20,
+                 ratio: float = 0.75, reproj_thresh: float = 3.0, iters: int = 2000,
+                 seed: int = 0, device: int = 0):
+        self._lib = load()
+        self.n = n_cams
+        h_ = ctypes.c_void_p()
+        check(self._lib.mcs_rig_job_create(n_cams, w, h, channels, nfeatures, nlevels,
+                                           float(scale_factor), fast_threshold, float(ratio),
+                                           float(reproj_thresh), iters, int(seed) & 0xffffffff,
+                                           device, ctypes.byref(h_)))
+        self._h = h_
+        self._H = np.zeros((n_cams - 1, 9), np.float64)
+        self._ok = np.zeros(n_cams - 1, np.int32)
+        self._kp = np.zeros(n_cams, np.int32)
+        self._m = np.zeros(n_cams - 1, np.int32)
+        self._inl = np.zeros(n_cams - 1, np.int32)
+
+    def submit(self, frame_ptrs, wait_event: int = 0):
+        arr = (ctypes.c_void_p * self.n)(*[int(p) for p in frame_ptrs])
+        check(self._lib.mcs_rig_job_submit(self._h, arr, ctypes.c_void_p(int(wait_event)) if
+                                           wait_event else None))
+
+    def wait(self):
+        check(self._lib.mcs_rig_job_wait(self._h, self._H.ctypes.data, self._ok.ctypes.data,
+                                         self._kp.ctypes.data, self._m.ctypes.data,
+                                         self._inl.ctypes.data))
+        H = [self._H[k].reshape(3, 3).copy() if self._ok[k] else None for k in range(self.n - 1)]
+        return H, {"keypoints": self._kp.tolist(), "matches": self._m.tolist(),
+                   "inliers": self._inl.tolist()}
+
+    def counts(self):
+        """(captures finished on the device path, on the per-call path)."""
+        a, b = ctypes.c_int(), ctypes.c_int()
+        check(self._lib.mcs_rig_job_counts(self._h, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
+
+    def close(self):
+        if self._h:
+            self._lib.mcs_rig_job_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def seam_graphcut_host(labels, cover, samples):

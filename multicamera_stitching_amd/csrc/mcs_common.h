@@ -41,6 +41,9 @@ int module_function(const rt::Api *A, int device, Module m, const char *name, hi
 // + 10 Levenberg-Marquardt iterations; H (9 doubles) holds the RANSAC model on entry.
 void homography_refine(const float *src_xy, const float *dst_xy, int n, const uint8_t *mask,
                        double *H);
+// Orders the calling thread's feature-workspace stream on `device` (the stream its ORB / match /
+// RANSAC calls run on, mcs_features.cpp) after `event`: a GPU-side wait, no host round trip.
+int features_stream_wait(int device, void *event);
 // The HIP device a plan was created for (its tables, buffers and side streams live there).
 int plan_device(const mcs_plan *plan);
 

@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "mcs_common.h"
+#include "mcs_feat_int.h"
 #include "mcs_fparams.h"
 #include "mcs_orb_core.h"
 #include "mcs_ransac_core.h"
@@ -17,16 +18,10 @@ namespace {
 
 using mcs::DeviceGuard;
 using mcs::rt::Api;
+using mcs::feat::FeatureKernels;
+using mcs::feat::feature_kernels;
+using mcs::feat::launch;
 
-struct FeatureKernels {
-    bool loaded = false;
-    hipFunction_t knn2 = nullptr, knn2_finalize = nullptr;
-    hipFunction_t ransac_score = nullptr, ransac_mask = nullptr;
-    hipFunction_t orb_gray = nullptr, orb_level = nullptr, orb_describe = nullptr;
-    hipFunction_t orb_pyramid = nullptr;
-    hipFunction_t orb_select = nullptr;
-    hipFunction_t l2_prep = nullptr, l2_i8 = nullptr, l2_f32 = nullptr, l2_finalize = nullptr;
-};
 FeatureKernels g_fk[mcs::kMaxDevices];
 std::mutex g_fk_mu;
 
@@ -39,8 +34,30 @@ struct Workspace {
     uint8_t *buf = nullptr;
     size_t cap = 0;
     hipStream_t s = nullptr;
+    hipEvent_t ev = nullptr;   // blocking-sync event: ws_sync's wait point
 };
 thread_local Workspace tl_ws[mcs::kMaxDevices];
+
+// Waits for the work queued on workspace stream `s`: hipStreamSynchronize, or with
+// MCS_FEATURE_SYNC=block through an event created with hipEventBlockingSync (the thread sleeps
+// instead of spinning; measured slower for the C3 loop on the 16-CPU box, so not the default).
+hipError_t ws_sync(const Api *A, hipStream_t s)
+{
+    static const bool spin =
+        !getenv("MCS_FEATURE_SYNC") || strcmp(getenv("MCS_FEATURE_SYNC"), "block");
+    if (!spin)
+        for (Workspace &w : tl_ws)
+            if (w.s == s) {
+                if (!w.ev) {
+                    // hipEventBlockingSync | hipEventDisableTiming
+                    hipError_t e = A->hipEventCreateWithFlags(&w.ev, 0x1u | 0x2u);
+                    if (e != hipSuccess) return e;
+                }
+                hipError_t e = A->hipEventRecord(w.ev, s);
+                return e == hipSuccess ? A->hipEventSynchronize(w.ev) : e;
+            }
+    return A->hipStreamSynchronize(s);
+}
 
 int workspace(const Api *A, int device, size_t bytes, uint8_t **buf, hipStream_t *s)
 {
@@ -61,7 +78,24 @@ int workspace(const Api *A, int device, size_t bytes, uint8_t **buf, hipStream_t
     return MCS_OK;
 }
 
-int feature_kernels(const Api *A, int device, const FeatureKernels **out)
+}  // namespace
+
+int mcs::features_stream_wait(int device, void *event)
+{
+    const Api *A = mcs::rt::api();
+    if (!A) return MCS_E_HIP;
+    DeviceGuard g(A, device);
+    if (g.err != hipSuccess)
+        return mcs::fail(MCS_E_HIP, "hipSetDevice(%d): %s", device, A->hipGetErrorString(g.err));
+    uint8_t *buf = nullptr;
+    hipStream_t s = nullptr;
+    int rc = workspace(A, device, 0, &buf, &s);
+    if (rc) return rc;
+    HIP_TRY(A->hipStreamWaitEvent(s, (hipEvent_t)event, 0));
+    return MCS_OK;
+}
+
+int mcs::feat::feature_kernels(const Api *A, int device, const FeatureKernels **out)
 {
     if (device < 0 || device >= mcs::kMaxDevices)
         return mcs::fail(MCS_E_INVALID, "device %d", device);
@@ -86,7 +120,9 @@ int feature_kernels(const Api *A, int device, const FeatureKernels **out)
                    {"mcs_orb_describe", &k.orb_describe},
                    {"mcs_orb_select", &k.orb_select},
                    {"mcs_l2_prep", &k.l2_prep},       {"mcs_l2_knn2_i8", &k.l2_i8},
-                   {"mcs_l2_knn2_f32", &k.l2_f32},    {"mcs_l2_knn2_finalize", &k.l2_finalize}};
+                   {"mcs_l2_knn2_f32", &k.l2_f32},    {"mcs_l2_knn2_finalize", &k.l2_finalize},
+                   {"mcs_rig_knn2", &k.rig_knn2},     {"mcs_rig_match", &k.rig_match},
+                   {"mcs_rig_ransac", &k.rig_ransac}, {"mcs_rig_best", &k.rig_best}};
         for (const auto &o : orb)
             if (rc == MCS_OK) rc = mcs::module_function(A, device, mcs::kModFeatures, o.name, o.f);
         if (rc) return rc;
@@ -96,14 +132,16 @@ int feature_kernels(const Api *A, int device, const FeatureKernels **out)
     return MCS_OK;
 }
 
-int launch(const Api *A, hipFunction_t f, unsigned gx, unsigned gy, unsigned bx, void *args,
-           size_t sz, hipStream_t s)
+int mcs::feat::launch(const Api *A, hipFunction_t f, unsigned gx, unsigned gy, unsigned bx,
+                      void *args, size_t sz, hipStream_t s, unsigned gz, unsigned lds)
 {
     void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz,
                    HIP_LAUNCH_PARAM_END};
-    HIP_TRY(A->hipModuleLaunchKernel(f, gx, gy, 1, bx, 1, 1, 0, s, nullptr, cfg));
+    HIP_TRY(A->hipModuleLaunchKernel(f, gx, gy, gz, bx, 1, 1, lds, s, nullptr, cfg));
     return MCS_OK;
 }
+
+namespace {
 
 int knn2(const Api *A, const FeatureKernels *k, const uint8_t *q, int nq, const uint8_t *t, int nt,
          int32_t *idx2, int32_t *dist2, hipStream_t s)
@@ -193,7 +231,7 @@ int l2_knn2(const Api *A, const FeatureKernels *k, const float *dq, int nq, cons
     uint32_t hflag = 0;
     if (e == hipSuccess && rc == MCS_OK)
         e = A->hipMemcpyAsync(&hflag, flag, 4, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = A->hipStreamSynchronize(s);
+    if (e == hipSuccess) e = ws_sync(A, s);
     (void)A->hipFree(buf);
     if (rc) return rc;
     if (e != hipSuccess) return mcs::fail(MCS_E_HIP, "l2 knn2: %s", A->hipGetErrorString(e));
@@ -275,7 +313,7 @@ int mcs_match_hamming_knn2_host(const uint8_t *query, int n_query, const uint8_t
         e = A->hipMemcpyAsync(idx2, di, ob, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess && rc == MCS_OK)
         e = A->hipMemcpyAsync(dist2, dd, ob, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = A->hipStreamSynchronize(s);
+    if (e == hipSuccess) e = ws_sync(A, s);
     if (e != hipSuccess) return mcs::fail(MCS_E_HIP, "knn2 host path: %s", A->hipGetErrorString(e));
     return rc;
 }
@@ -336,7 +374,7 @@ int mcs_match_l2_knn2_host(const float *query, int n_query, const float *train, 
         e = A->hipMemcpyAsync(idx2, di, ob, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess && rc == MCS_OK)
         e = A->hipMemcpyAsync(dist2, dd, ob, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess && s) e = A->hipStreamSynchronize(s);
+    if (e == hipSuccess && s) e = ws_sync(A, s);
     if (s) (void)A->hipStreamDestroy(s);
     (void)A->hipFree(buf);
     if (e != hipSuccess) return mcs::fail(MCS_E_HIP, "l2 host path: %s", A->hipGetErrorString(e));
@@ -393,7 +431,7 @@ int mcs_ransac_homography_host(const float *src_xy, const float *dst_xy, int n, 
         rc = launch(A, k->ransac_score, iters, 1, mcs::kRansacBlock, &a, sizeof(a), s);
     if (e == hipSuccess && rc == MCS_OK)
         e = A->hipMemcpyAsync(scores.data(), a.scores, sb, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess && rc == MCS_OK) e = A->hipStreamSynchronize(s);
+    if (e == hipSuccess && rc == MCS_OK) e = ws_sync(A, s);
     int best = -1, best_score = -1;
     if (e == hipSuccess && rc == MCS_OK) {
         for (int i = 0; i < iters; i++)
@@ -406,7 +444,7 @@ int mcs_ransac_homography_host(const float *src_xy, const float *dst_xy, int n, 
             if (e == hipSuccess && rc == MCS_OK)
                 e = A->hipMemcpyAsync(hb8, a.hyps + (size_t)best * 8, sizeof(hb8),
                                       hipMemcpyDeviceToHost, s);
-            if (e == hipSuccess && rc == MCS_OK) e = A->hipStreamSynchronize(s);
+            if (e == hipSuccess && rc == MCS_OK) e = ws_sync(A, s);
         }
     }
     if (e != hipSuccess) return mcs::fail(MCS_E_HIP, "ransac: %s", A->hipGetErrorString(e));
@@ -422,6 +460,8 @@ int mcs_ransac_homography_host(const float *src_xy, const float *dst_xy, int n, 
         for (int i = 0; i < n; i++) mask[i] = m8[i];
     return MCS_OK;
 }
+
+}  // extern "C"
 
 // Source index of destination index d in OpenCV's resize(INTER_LINEAR) (mcs_orb_pyramid's
 // pyr_axis, the same float arithmetic).
@@ -440,9 +480,10 @@ static int pyr_src(int d, double scale, int ssize, bool is_x)
 // buffer size from every block's dependency regions (the kernel's top-down walk, on the host).
 // Returns the block count, 0 when the fused launch does not apply (a >= 2x level step, or
 // regions too large for LDS).
-static unsigned pyramid_args(const int *lw, const int *lh, int nlevels, const size_t *off,
-                             uint8_t *lvl, mcs::KOrbBuildArgs &a)
+unsigned mcs::feat::pyramid_args(const OrbGeom &g, uint8_t *lvl, KOrbBuildArgs &a)
 {
+    const int *lw = g.lw, *lh = g.lh, nlevels = g.nlevels;
+    const size_t *off = g.off;
     std::memset(&a, 0, sizeof(a));
     const int L = nlevels - 1;
     for (int l = 1; l <= L; l++) {
@@ -481,6 +522,37 @@ static unsigned pyramid_args(const int *lw, const int *lh, int nlevels, const si
     return (unsigned)(a.gx * gy);
 }
 
+int mcs::feat::orb_geom(int w, int h, int nfeatures, int nlevels, float scale_factor,
+                        OrbGeom *g)
+{
+    g->nlevels = nlevels;
+    for (int l = 0; l < nlevels; l++) {
+        g->lscale[l] = (float)std::pow((double)scale_factor, (double)l);
+        g->lw[l] = (int)std::lrint((float)w / g->lscale[l]);
+        g->lh[l] = (int)std::lrint((float)h / g->lscale[l]);
+        if (g->lw[l] < 1 || g->lh[l] < 1) return mcs::fail(MCS_E_INVALID, "level %d is empty", l);
+        g->off[l + 1] = g->off[l] + (((size_t)g->lw[l] * g->lh[l] + 255) & ~(size_t)255);
+    }
+    const float factor = (float)(1.0 / scale_factor);
+    float per = nfeatures * (1 - factor) / (1 - (float)std::pow((double)factor, (double)nlevels));
+    int sum = 0;
+    for (int l = 0; l < nlevels - 1; l++) {
+        g->quota[l] = (int)std::lrint(per);
+        sum += g->quota[l];
+        per *= factor;
+    }
+    g->quota[nlevels - 1] = std::max(nfeatures - sum, 0);
+    g->n_bound = 0;
+    g->cap_total = 0;
+    for (int l = 0; l < nlevels; l++) {
+        g->n_bound += g->quota[l];
+        g->cap[l] = std::max((size_t)4096, (size_t)g->lw[l] * g->lh[l] / 8);
+        g->coff[l + 1] = g->coff[l] + g->cap[l];
+        g->cap_total += g->cap[l];
+    }
+    return MCS_OK;
+}
+
 namespace {
 // ORB of one image (host memory, or device memory when on_device); mcs_orb_detect_host /
 // mcs_orb_detect_device below.
@@ -509,35 +581,13 @@ int orb_detect(const uint8_t *image, bool on_device, int w, int h, int channels,
     int rc = feature_kernels(A, device, &k);
     if (rc) return rc;
     // level sizes and quotas, as OpenCV's ORB computes them (float arithmetic)
-    int lw[mcs::kOrbMaxLevels], lh[mcs::kOrbMaxLevels], quota[mcs::kOrbMaxLevels];
-    float lscale[mcs::kOrbMaxLevels];
-    size_t off[mcs::kOrbMaxLevels + 1] = {0};
-    for (int l = 0; l < nlevels; l++) {
-        lscale[l] = (float)std::pow((double)scale_factor, (double)l);
-        lw[l] = (int)std::lrint((float)w / lscale[l]);
-        lh[l] = (int)std::lrint((float)h / lscale[l]);
-        if (lw[l] < 1 || lh[l] < 1) return mcs::fail(MCS_E_INVALID, "level %d is empty", l);
-        off[l + 1] = off[l] + (((size_t)lw[l] * lh[l] + 255) & ~(size_t)255);
-    }
-    {
-        const float factor = (float)(1.0 / scale_factor);
-        float per = nfeatures * (1 - factor) / (1 - (float)std::pow((double)factor,
-                                                                    (double)nlevels));
-        int sum = 0;
-        for (int l = 0; l < nlevels - 1; l++) {
-            quota[l] = (int)std::lrint(per);
-            sum += quota[l];
-            per *= factor;
-        }
-        quota[nlevels - 1] = std::max(nfeatures - sum, 0);
-    }
-    const size_t pix = off[nlevels];
-    size_t cap_total = 0, cap[mcs::kOrbMaxLevels], coff[mcs::kOrbMaxLevels + 1] = {0};
-    for (int l = 0; l < nlevels; l++) {
-        cap[l] = std::max((size_t)4096, (size_t)lw[l] * lh[l] / 8);
-        coff[l + 1] = coff[l] + cap[l];
-        cap_total += cap[l];
-    }
+    mcs::feat::OrbGeom geo;
+    rc = mcs::feat::orb_geom(w, h, nfeatures, nlevels, scale_factor, &geo);
+    if (rc) return rc;
+    const int *lw = geo.lw, *lh = geo.lh, *quota = geo.quota;
+    const float *lscale = geo.lscale;
+    const size_t *off = geo.off, *cap = geo.cap, *coff = geo.coff;
+    const size_t pix = off[nlevels], cap_total = geo.cap_total;
     // one allocation: input, levels, blur (u16 pass + u8), scores, candidates, counts, keypoints,
     // descriptors, orientations
     const size_t in_bytes = (size_t)w * h * channels;
@@ -576,11 +626,11 @@ int orb_detect(const uint8_t *image, bool on_device, int w, int h, int channels,
     if (e == hipSuccess) {
         if (channels == 3) {
             mcs::KGrayArgs ga;
-            ga.bgr = in;
+            std::memset(&ga, 0, sizeof(ga));
+            ga.bgr[0] = in;
             ga.gray = lvl0;
             ga.n = w * h;
-            ga.pad_ = 0;
-            rc = launch(A, k->orb_gray, (w * h + 255) / 256, 1, 256, &ga, sizeof(ga), s);
+            rc = launch(A, k->orb_gray, (w * h + 1023) / 1024, 1, 256, &ga, sizeof(ga), s);
         } else {
             e = A->hipMemcpyAsync(lvl0, in, in_bytes, hipMemcpyDeviceToDevice, s);
         }
@@ -591,7 +641,7 @@ int orb_detect(const uint8_t *image, bool on_device, int w, int h, int channels,
     mcs::KOrbBuildArgs ba;
     static const bool fused_on = !getenv("MCS_ORB_PYRAMID") || strcmp(getenv("MCS_ORB_PYRAMID"), "0");
     const unsigned pyr_blocks = fused_on && e == hipSuccess && rc == MCS_OK && nlevels > 1
-                                    ? pyramid_args(lw, lh, nlevels, off, buf + o_lvl, ba)
+                                    ? mcs::feat::pyramid_args(geo, buf + o_lvl, ba)
                                     : 0u;
     if (pyr_blocks > 0) {
         size_t sz = sizeof(ba);
@@ -642,8 +692,7 @@ int orb_detect(const uint8_t *image, bool on_device, int w, int h, int channels,
     da.kp = reinterpret_cast<const int *>(buf + o_kp);
     da.desc = buf + o_desc;
     da.orient = reinterpret_cast<double *>(buf + o_or);
-    int n_bound = 0;
-    for (int l = 0; l < nlevels; l++) n_bound += quota[l];
+    const int n_bound = geo.n_bound;
     if (e == hipSuccess && rc == MCS_OK) {
         mcs::KOrbSelArgs sa;
         std::memset(&sa, 0, sizeof(sa));
@@ -666,7 +715,7 @@ int orb_detect(const uint8_t *image, bool on_device, int w, int h, int channels,
     }
     if (e == hipSuccess && rc == MCS_OK)
         e = A->hipMemcpyAsync(blob.data(), buf + o_cnt, o_end - o_cnt, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess && rc == MCS_OK) e = A->hipStreamSynchronize(s);
+    if (e == hipSuccess && rc == MCS_OK) e = ws_sync(A, s);
     int n = 0;
     const int *sel = reinterpret_cast<const int *>(at(o_sel));
     const int *kpd = reinterpret_cast<const int *>(at(o_kp));
@@ -688,7 +737,7 @@ int orb_detect(const uint8_t *image, bool on_device, int w, int h, int channels,
                                       buf + o_cand + coff[l] * sizeof(mcs::OrbCand),
                                       (size_t)c * sizeof(mcs::OrbCand), hipMemcpyDeviceToHost, s);
         }
-        if (e == hipSuccess) e = A->hipStreamSynchronize(s);
+        if (e == hipSuccess) e = ws_sync(A, s);
         if (e == hipSuccess) {
             // per level: rank by response (desc), then y, then x; keep the level's quota (a
             // strict total order -- positions are unique -- so selecting the quota first and
@@ -724,10 +773,10 @@ int orb_detect(const uint8_t *image, bool on_device, int w, int h, int channels,
             if (e == hipSuccess && rc == MCS_OK)
                 e = A->hipMemcpyAsync(orient.data(), buf + o_or, (size_t)n * 2 * sizeof(double),
                                       hipMemcpyDeviceToHost, s);
-            if (e == hipSuccess && rc == MCS_OK) e = A->hipStreamSynchronize(s);
+            if (e == hipSuccess && rc == MCS_OK) e = ws_sync(A, s);
         }
     }
-    if (e == hipSuccess && rc != MCS_OK) e = A->hipStreamSynchronize(s);   // drain on error
+    if (e == hipSuccess && rc != MCS_OK) e = ws_sync(A, s);   // drain on error
     if (e != hipSuccess) return mcs::fail(MCS_E_HIP, "orb: %s", A->hipGetErrorString(e));
     if (rc) return rc;
     for (int i = 0; i < n; i++) {
@@ -746,6 +795,8 @@ int orb_detect(const uint8_t *image, bool on_device, int w, int h, int channels,
     return MCS_OK;
 }
 }  // namespace
+
+extern "C" {
 
 int mcs_orb_detect_host(const uint8_t *image, int w, int h, int channels, int nfeatures,
                         int nlevels, float scale_factor, int fast_threshold, float *kp_xy,

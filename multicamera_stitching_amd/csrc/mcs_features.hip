@@ -45,18 +45,22 @@ __device__ __forceinline__ uint32_t hamming_lds(const uint32_t (&q)[8], const ui
 
 }  // namespace mcs
 
-// grid (ceil(nq / 64), chunks), block 64.  keys must hold 0xffffffff on entry (memset).
-extern "C" __global__ __launch_bounds__(64) void mcs_hamming_knn2(const mcs::KHammingArgs a)
+namespace mcs {
+
+// One block of the kNN-2: queries blockIdx.x * 64 + lane against train chunk `chunk`, merged into
+// keys (0xffffffff on entry) by atomicMin.  nq > 0.
+__device__ __forceinline__ void knn2_block(const uint32_t *query, const uint32_t *train,
+                                           uint32_t *keys, int nq, int nt, int per_chunk,
+                                           int qblock, int chunk)
 {
-    using namespace mcs;
-    const int q = blockIdx.x * kKnnQueriesPerBlock + threadIdx.x;
+    const int q = qblock * kKnnQueriesPerBlock + threadIdx.x;
     uint32_t d[8];
-    const uint4 *qs = reinterpret_cast<const uint4 *>(a.query + (int64_t)min(q, a.nq - 1) * 8);
+    const uint4 *qs = reinterpret_cast<const uint4 *>(query + (int64_t)min(q, nq - 1) * 8);
     const uint4 v0 = qs[0], v1 = qs[1];
     d[0] = v0.x, d[1] = v0.y, d[2] = v0.z, d[3] = v0.w;
     d[4] = v1.x, d[5] = v1.y, d[6] = v1.z, d[7] = v1.w;
-    const int j0 = blockIdx.y * a.per_chunk, j1 = min(a.nt, j0 + a.per_chunk);
-    const uint4 *__restrict__ train4 = reinterpret_cast<const uint4 *>(a.train);
+    const int j0 = chunk * per_chunk, j1 = min(nt, j0 + per_chunk);
+    const uint4 *__restrict__ train4 = reinterpret_cast<const uint4 *>(train);
     __shared__ uint4 tl[2 * kKnnQueriesPerBlock];
     uint32_t k0 = kKeyNone, k1 = kKeyNone;
     for (int jt = j0; jt < j1; jt += kKnnQueriesPerBlock) {
@@ -81,10 +85,18 @@ extern "C" __global__ __launch_bounds__(64) void mcs_hamming_knn2(const mcs::KHa
             top2(k0, k1, (hamming_lds(d, tl + 2 * u) << kKnnKeyShift) | (uint32_t)(jt + u));
         __syncthreads();
     }
-    if (q >= a.nq) return;
-    const uint32_t old = atomicMin(&a.keys[2 * q], k0);
-    atomicMin(&a.keys[2 * q + 1], max(old, k0));
-    atomicMin(&a.keys[2 * q + 1], k1);
+    if (q >= nq) return;
+    const uint32_t old = atomicMin(&keys[2 * q], k0);
+    atomicMin(&keys[2 * q + 1], max(old, k0));
+    atomicMin(&keys[2 * q + 1], k1);
+}
+
+}  // namespace mcs
+
+// grid (ceil(nq / 64), chunks), block 64.  keys must hold 0xffffffff on entry (memset).
+extern "C" __global__ __launch_bounds__(64) void mcs_hamming_knn2(const mcs::KHammingArgs a)
+{
+    mcs::knn2_block(a.query, a.train, a.keys, a.nq, a.nt, a.per_chunk, blockIdx.x, blockIdx.y);
 }
 
 // keys -> (train index, distance) pairs; -1 where fewer than two train descriptors exist.
@@ -294,41 +306,44 @@ extern "C" __global__ __launch_bounds__(256) void mcs_l2_knn2_finalize(const mcs
 }
 
 // ---- RANSAC homography (NS-5) ------------------------------------------------------------------
-// grid (iters), block kRansacBlock: thread 0 draws hypothesis k and solves its 4-point model,
-// then the block counts its inliers over all n correspondences (FP64, mcs_ransac_core.h).
-extern "C" __global__ __launch_bounds__(256) void mcs_ransac_score(const mcs::KRansacArgs a)
+namespace mcs {
+
+// Hypothesis k of a RANSAC over n correspondences (block kRansacBlock): thread 0 draws the
+// sample and solves its 4-point model, then the block counts its inliers (FP64,
+// mcs_ransac_core.h).  hyps[8 k ..] = the model (NaN: rejected), scores[k] = inliers (-1).
+__device__ __forceinline__ void ransac_block(const double *pts, double *hyps, int32_t *scores,
+                                             int n, uint32_t seed, double t2, int k)
 {
-    using namespace mcs;
     __shared__ double h[8];
     __shared__ int valid;
     __shared__ int wsum[kRansacBlock / 64];
-    const int k = blockIdx.x, tid = threadIdx.x;
+    const int tid = threadIdx.x;
     if (tid == 0) {
         int idx[4];
         double s[8], d[8], hh[8];
-        bool ok = rs_subset(a.seed, (uint32_t)k, (uint32_t)a.n, idx);
+        bool ok = rs_subset(seed, (uint32_t)k, (uint32_t)n, idx);
         if (ok) {
             for (int m = 0; m < 4; m++) {
-                s[2 * m] = a.pts[4 * idx[m]], s[2 * m + 1] = a.pts[4 * idx[m] + 1];
-                d[2 * m] = a.pts[4 * idx[m] + 2], d[2 * m + 1] = a.pts[4 * idx[m] + 3];
+                s[2 * m] = pts[4 * idx[m]], s[2 * m + 1] = pts[4 * idx[m] + 1];
+                d[2 * m] = pts[4 * idx[m] + 2], d[2 * m + 1] = pts[4 * idx[m] + 3];
             }
             ok = rs_model4(s, d, hh);
         }
         valid = ok;
         for (int j = 0; j < 8; j++) {
             h[j] = ok ? hh[j] : 0.0;
-            a.hyps[(int64_t)k * 8 + j] = ok ? hh[j] : __builtin_nan("");
+            hyps[(int64_t)k * 8 + j] = ok ? hh[j] : __builtin_nan("");
         }
     }
     __syncthreads();
     if (!valid) {
-        if (tid == 0) a.scores[k] = -1;
+        if (tid == 0) scores[k] = -1;
         return;
     }
     int c = 0;
-    for (int i = tid; i < a.n; i += kRansacBlock) {
-        const double *p = a.pts + 4 * (int64_t)i;
-        c += rs_inlier(h, p[0], p[1], p[2], p[3], a.t2) ? 1 : 0;
+    for (int i = tid; i < n; i += kRansacBlock) {
+        const double *p = pts + 4 * (int64_t)i;
+        c += rs_inlier(h, p[0], p[1], p[2], p[3], t2) ? 1 : 0;
     }
     for (int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off, 64);
     if ((tid & 63) == 0) wsum[tid >> 6] = c;
@@ -336,8 +351,16 @@ extern "C" __global__ __launch_bounds__(256) void mcs_ransac_score(const mcs::KR
     if (tid == 0) {
         int t = 0;
         for (int w = 0; w < kRansacBlock / 64; w++) t += wsum[w];
-        a.scores[k] = t;
+        scores[k] = t;
     }
+}
+
+}  // namespace mcs
+
+// grid (iters), block kRansacBlock: hypothesis blockIdx.x.
+extern "C" __global__ __launch_bounds__(256) void mcs_ransac_score(const mcs::KRansacArgs a)
+{
+    mcs::ransac_block(a.pts, a.hyps, a.scores, a.n, a.seed, a.t2, blockIdx.x);
 }
 
 // grid (ceil(n / 256)), block 256: inlier mask of hypothesis a.best.
@@ -353,12 +376,32 @@ extern "C" __global__ __launch_bounds__(256) void mcs_ransac_mask(const mcs::KRa
 
 // ---- ORB (NS-3) ----------------------------------------------------------------------------
 // BGR -> gray with OpenCV's fixed point: (1868 B + 9617 G + 4899 R + 8192) >> 14.
+// Four pixels per thread: three dword loads (12 bytes of BGR) and one dword store when the
+// frame is 4-byte aligned (the gray level always is), bytes otherwise.
 extern "C" __global__ __launch_bounds__(256) void mcs_orb_gray(const mcs::KGrayArgs a)
 {
-    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int q = blockIdx.x * 256 + threadIdx.x, i = 4 * q;
+    const uint8_t *bgr = a.bgr[blockIdx.y];
+    uint8_t *gray = a.gray + blockIdx.y * a.stride;
     if (i >= a.n) return;
-    const uint8_t *p = a.bgr + 3 * (int64_t)i;
-    a.gray[i] = (uint8_t)((1868 * p[0] + 9617 * p[1] + 4899 * p[2] + 8192) >> 14);
+    auto g = [](uint32_t b, uint32_t gg, uint32_t r) {
+        return (1868u * b + 9617u * gg + 4899u * r + 8192u) >> 14;
+    };
+    if (i + 4 <= a.n && ((uintptr_t)bgr & 3) == 0) {
+        const uint32_t *p = reinterpret_cast<const uint32_t *>(bgr) + 3 * (int64_t)q;
+        const uint32_t w0 = __builtin_nontemporal_load(p), w1 = __builtin_nontemporal_load(p + 1),
+                       w2 = __builtin_nontemporal_load(p + 2);
+        const uint32_t v0 = g(w0 & 255, (w0 >> 8) & 255, (w0 >> 16) & 255);
+        const uint32_t v1 = g(w0 >> 24, w1 & 255, (w1 >> 8) & 255);
+        const uint32_t v2 = g((w1 >> 16) & 255, w1 >> 24, w2 & 255);
+        const uint32_t v3 = g((w2 >> 8) & 255, (w2 >> 16) & 255, w2 >> 24);
+        reinterpret_cast<uint32_t *>(gray)[q] = v0 | v1 << 8 | v2 << 16 | v3 << 24;
+        return;
+    }
+    for (int j = i; j < min(i + 4, a.n); j++) {
+        const uint8_t *p = bgr + 3 * (int64_t)j;
+        gray[j] = (uint8_t)g(p[0], p[1], p[2]);
+    }
 }
 
 __device__ __forceinline__ int orb_refl(int i, int n)
@@ -372,7 +415,8 @@ __device__ __forceinline__ int orb_refl(int i, int n)
 //   - the 7-tap Gaussian blur (horizontal pass in u16 into LDS, vertical pass with one
 //     rounding, (s + 32768) >> 16: the descriptors' image),
 //   - the FAST-9 scores of the tile and a one-pixel ring (score > threshold, else 0; 0 outside
-//     the region where a keypoint's NMS can look),
+//     the region where a keypoint's NMS can look): the bit-mask segment test on every position,
+//     the score only on the (compacted) positions that pass it,
 //   - the 3x3 non-maximum suppression of the tile's pixels (strict, inside the kOrbEdge
 //     border), the survivors compacted in LDS so that the Harris sums (32-bit exact, 7x7 Sobel
 //     on the staged image) run on full waves, and appended to the level's candidates (their
@@ -388,15 +432,16 @@ extern "C" __global__ __launch_bounds__(256) void mcs_orb_level(const mcs::KOrbP
     __shared__ uint16_t hb[(kOrbTY + 6) * kOrbTX];
     __shared__ uint8_t sc[kOrbSY * kOrbSX];
     __shared__ int sx[kOrbTX * kOrbTY];
-    __shared__ int ns;
-    const int b = blockIdx.x, tid = threadIdx.x;
+    __shared__ uint16_t fl[kOrbSY * kOrbSX];
+    __shared__ int ns, nf;
+    const int b = blockIdx.x, tid = threadIdx.x, cam = blockIdx.y;
     int l = 0;
     for (int k = 1; k < p.nlevels; k++) l += b >= p.bstart[k] ? 1 : 0;
     const int w = p.w[l], h = p.h[l];
     const int bx = (w + kOrbTX - 1) / kOrbTX, loc = b - p.bstart[l];
     const int y0 = (loc / bx) * kOrbTY, x0 = (loc % bx) * kOrbTX;
-    const uint8_t *im = p.img + p.off[l];
-    if (tid == 0) ns = 0;
+    const uint8_t *im = p.img + cam * p.stride + p.off[l];
+    if (tid == 0) ns = 0, nf = 0;
     for (int i = tid; i < kOrbLY * kOrbLX; i += 256) {
         const int yy = orb_refl(min(max(y0 - kOrbHalo + i / kOrbLX, -(h - 1)), 2 * h - 2), h);
         const int xx = orb_refl(min(max(x0 - kOrbHalo + i % kOrbLX, -(w - 1)), 2 * w - 2), w);
@@ -411,20 +456,32 @@ extern "C" __global__ __launch_bounds__(256) void mcs_orb_level(const mcs::KOrbP
         for (int t = 0; t < 7; t++) s += mcs::kOrbBlur[t] * r[t];
         hb[i] = (uint16_t)s;
     }
-    // FAST on the tile and a one-pixel ring (positions x0 - 1 .., y0 - 1 ..)
+    // FAST on the tile and a one-pixel ring (positions x0 - 1 .., y0 - 1 ..): the segment test
+    // (= score > threshold) everywhere, the survivors compacted in LDS and scored on full waves
     const int lo = mcs::kOrbEdge - 1;
     for (int i = tid; i < kOrbSY * kOrbSX; i += 256) {
         const int yy = y0 - 1 + i / kOrbSX, xx = x0 - 1 + i % kOrbSX;
-        uint8_t v = 0;
-        if (xx >= lo && yy >= lo && xx < w - lo && yy < h - lo) {
-            const int s = mcs::orb_fast_score(
-                img + (i / kOrbSX + kOrbHalo - 1) * kOrbLX + i % kOrbSX + kOrbHalo - 1, kOrbLX);
-            v = s > p.threshold ? (uint8_t)s : 0;
+        bool corner = false;
+        if (xx >= lo && yy >= lo && xx < w - lo && yy < h - lo)
+            corner = mcs::orb_fast_test(
+                img + (i / kOrbSX + kOrbHalo - 1) * kOrbLX + i % kOrbSX + kOrbHalo - 1, kOrbLX,
+                p.threshold);
+        sc[i] = 0;
+        if (corner) {
+            const unsigned long long act = __ballot(1);
+            const int lane = __lane_id(), leader = __ffsll((long long)act) - 1;
+            int base = 0;
+            if (lane == leader) base = atomicAdd(&nf, __popcll(act));
+            fl[__shfl(base, leader) + __popcll(act & ((1ull << lane) - 1ull))] = (uint16_t)i;
         }
-        sc[i] = v;
     }
     __syncthreads();
-    uint8_t *blur = p.blur + p.off[l];
+    for (int j = tid; j < nf; j += 256) {
+        const int i = fl[j];
+        sc[i] = (uint8_t)mcs::orb_fast_score(
+            img + (i / kOrbSX + kOrbHalo - 1) * kOrbLX + i % kOrbSX + kOrbHalo - 1, kOrbLX);
+    }
+    uint8_t *blur = p.blur + cam * p.stride + p.off[l];
     for (int i = tid; i < kOrbTY * kOrbTX; i += 256) {
         const int yy = y0 + i / kOrbTX, xx = x0 + i % kOrbTX;
         if (yy >= h || xx >= w) continue;
@@ -434,6 +491,7 @@ extern "C" __global__ __launch_bounds__(256) void mcs_orb_level(const mcs::KOrbP
         for (int t = 0; t < 7; t++) s += mcs::kOrbBlur[t] * (int)c[t * kOrbTX];
         blur[(int64_t)yy * w + xx] = (uint8_t)((s + 32768) >> 16);
     }
+    __syncthreads();
     // 3x3 NMS of the tile's pixels; survivors (packed y << 16 | x) compacted in LDS
     const int e = mcs::kOrbEdge;
     for (int i = tid; i < kOrbTY * kOrbTX; i += 256) {
@@ -468,10 +526,10 @@ extern "C" __global__ __launch_bounds__(256) void mcs_orb_level(const mcs::KOrbP
         const unsigned long long act = __ballot(1);
         const int lane = __lane_id(), leader = __ffsll((long long)act) - 1;
         int base = 0;
-        if (lane == leader) base = atomicAdd(p.ncand + l, __popcll(act));
+        if (lane == leader) base = atomicAdd(p.ncand + cam * mcs::kOrbMaxLevels + l, __popcll(act));
         const int q = __shfl(base, leader) + __popcll(act & ((1ull << lane) - 1ull));
         if (q < p.cap[l]) {
-            mcs::OrbCand *cand = p.cand + p.coff[l];
+            mcs::OrbCand *cand = p.cand + cam * p.cstride + p.coff[l];
             cand[q].x = x0 + i % kOrbTX;
             cand[q].y = y0 + i / kOrbTX;
             cand[q].response = r;
@@ -488,24 +546,27 @@ extern "C" __global__ __launch_bounds__(1024) void mcs_orb_select(const mcs::KOr
     using namespace mcs;
     __shared__ double rs[kOrbSelMax];
     __shared__ uint32_t ks[kOrbSelMax];
-    const int l = blockIdx.x, tid = threadIdx.x;
-    auto kept = [&](int i) { return min(min(a.ncand[i], a.cap[i]), a.quota[i]); };
+    const int l = blockIdx.x, tid = threadIdx.x, cam = blockIdx.y;
+    const int *ncand = a.ncand + cam * kOrbMaxLevels;
+    int *kp = a.kp + 3 * cam * a.kstride, *sel = a.sel + 2 * cam;
+    double *resp = a.resp + cam * a.kstride;
+    auto kept = [&](int i) { return min(min(ncand[i], a.cap[i]), a.quota[i]); };
     int base = 0, total = 0;
     for (int i = 0; i < a.nlevels; i++) {
         if (i < l) base += kept(i);
         total += kept(i);
     }
     bool over = false;
-    for (int i = 0; i < a.nlevels; i++) over = over || min(a.ncand[i], a.cap[i]) > kOrbSelMax;
+    for (int i = 0; i < a.nlevels; i++) over = over || min(ncand[i], a.cap[i]) > kOrbSelMax;
     if (l == 0 && tid == 0) {
-        a.sel[0] = total;
-        a.sel[1] = over ? 1 : 0;
+        sel[0] = total;
+        sel[1] = over ? 1 : 0;
     }
     if (over) return;   // uniform
-    const int c = min(a.ncand[l], a.cap[l]), q = kept(l);
+    const int c = min(ncand[l], a.cap[l]), q = kept(l);
     int n = 64;
     while (n < c) n <<= 1;
-    const OrbCand *cd = a.cand + a.coff[l];
+    const OrbCand *cd = a.cand + cam * a.cstride + a.coff[l];
     for (int i = tid; i < n; i += kOrbSelThreads) {
         const bool v = i < c;
         rs[i] = v ? cd[i].response : -__builtin_inf();
@@ -535,10 +596,10 @@ extern "C" __global__ __launch_bounds__(1024) void mcs_orb_select(const mcs::KOr
         }
     for (int i = tid; i < q; i += kOrbSelThreads) {
         const int o = base + i;
-        a.kp[3 * o] = l;
-        a.kp[3 * o + 1] = (int)(ks[i] & 0xffffu);
-        a.kp[3 * o + 2] = (int)(ks[i] >> 16);
-        a.resp[o] = rs[i];
+        kp[3 * o] = l;
+        kp[3 * o + 1] = (int)(ks[i] & 0xffffu);
+        kp[3 * o + 2] = (int)(ks[i] >> 16);
+        resp[o] = rs[i];
     }
 }
 
@@ -547,11 +608,14 @@ extern "C" __global__ __launch_bounds__(1024) void mcs_orb_select(const mcs::KOr
 extern "C" __global__ __launch_bounds__(64) void mcs_orb_describe(const mcs::KOrbDescArgs a)
 {
     using namespace mcs;
-    const int k = blockIdx.x, lane = threadIdx.x;
-    if (a.sel && (k >= a.sel[0] || a.sel[1])) return;   // past the device ranking's count
-    const int lvl = a.kp[3 * k], x = a.kp[3 * k + 1], y = a.kp[3 * k + 2];
+    const int k = blockIdx.x, lane = threadIdx.x, cam = blockIdx.y;
+    const int *sel = a.sel ? a.sel + 2 * cam : nullptr;
+    if (sel && (k >= sel[0] || sel[1])) return;   // past the device ranking's count
+    const int *kp = a.kp + 3 * cam * a.kstride;
+    const int lvl = kp[3 * k], x = kp[3 * k + 1], y = kp[3 * k + 2];
     const int w = a.w[lvl];
-    const uint8_t *p = a.img[lvl] + (int64_t)y * w + x;
+    const int64_t co = cam * a.stride;
+    const uint8_t *p = a.img[lvl] + co + (int64_t)y * w + x;
     long long m10 = 0, m01 = 0;
     if (lane <= kOrbHalfPatch) {
         const int v = lane;
@@ -577,7 +641,7 @@ extern "C" __global__ __launch_bounds__(64) void mcs_orb_describe(const mcs::KOr
     const double fx = (double)m10, fy = (double)m01;
     const double r = sqrt(fx * fx + fy * fy);
     const double cs = r > 0.0 ? fx / r : 1.0, sn = r > 0.0 ? fy / r : 0.0;
-    const uint8_t *b = a.blur[lvl] + (int64_t)y * w + x;
+    const uint8_t *b = a.blur[lvl] + co + (int64_t)y * w + x;
     uint32_t bits = 0;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
@@ -587,10 +651,10 @@ extern "C" __global__ __launch_bounds__(64) void mcs_orb_describe(const mcs::KOr
         bits |= (uint32_t)(v1 < v2) << j;
     }
     const uint32_t hi = __shfl_down(bits, 1, 64);
-    if ((lane & 1) == 0) a.desc[32 * (int64_t)k + (lane >> 1)] = (uint8_t)(bits | (hi << 4));
+    if ((lane & 1) == 0) a.desc[32 * ((int64_t)cam * a.kstride + k) + (lane >> 1)] = (uint8_t)(bits | (hi << 4));
     if (lane == 0) {
-        a.orient[2 * k] = cs;
-        a.orient[2 * k + 1] = sn;
+        a.orient[2 * ((int64_t)cam * a.kstride + k)] = cs;
+        a.orient[2 * ((int64_t)cam * a.kstride + k) + 1] = sn;
     }
 }
 
@@ -622,6 +686,7 @@ extern "C" __global__ __launch_bounds__(256) void mcs_orb_pyramid(const mcs::KOr
     extern __shared__ uint8_t pyr_lds[];
     const int L = a.nlevels - 1, tid = threadIdx.x;
     const int t = blockIdx.x, tx = t % a.gx, ty = t / a.gx;
+    uint8_t *const lvl = a.lvl + blockIdx.y * a.stride;
     // regions [x0, x1) x [y0, y1) of every level, top down (block-uniform)
     int x0[12], x1[12], y0[12], y1[12];
     x0[L] = tx * a.tw;
@@ -645,11 +710,11 @@ extern "C" __global__ __launch_bounds__(256) void mcs_orb_pyramid(const mcs::KOr
         const int rw = x1[l] - x0[l], rh = y1[l] - y0[l];
         const int sw = a.w[l - 1], sh = a.h[l - 1];
         // source: level 0 in global memory, else the previous region in LDS
-        const uint8_t *src = l == 1 ? a.lvl + a.off[0] : buf[(l - 1) & 1];
+        const uint8_t *src = l == 1 ? lvl + a.off[0] : buf[(l - 1) & 1];
         const int spitch = l == 1 ? sw : x1[l - 1] - x0[l - 1];
         const int sx0 = l == 1 ? 0 : x0[l - 1], sy0 = l == 1 ? 0 : y0[l - 1];
         uint8_t *dst = buf[l & 1];
-        uint8_t *out = a.lvl + a.off[l];
+        uint8_t *out = lvl + a.off[l];
         for (int i = tid; i < rw * rh; i += 256) {
             const int x = x0[l] + i % rw, y = y0[l] + i / rw;
             int s, a0, a1, sy, b0, b1;
@@ -666,5 +731,130 @@ extern "C" __global__ __launch_bounds__(256) void mcs_orb_pyramid(const mcs::KOr
             out[(int64_t)y * a.w[l] + x] = v;
         }
         __syncthreads();
+    }
+}
+
+// ---- A rig capture on the device (mcs_rig.cpp; KRigArgs) ---------------------------------------
+// grid (ceil(kstride / 64), chunks, pairs), block 64: pair p's kNN-2, query camera p + 1 against
+// train camera p, the keypoint counts read from the device (a camera whose ranking overflowed
+// counts as empty: the host redoes that capture through the per-call path).
+extern "C" __global__ __launch_bounds__(64) void mcs_rig_knn2(const mcs::KRigArgs a)
+{
+    using namespace mcs;
+    const int p = blockIdx.z;
+    const int nq = a.sel[2 * (p + 1) + 1] ? 0 : a.sel[2 * (p + 1)];
+    const int nt = a.sel[2 * p + 1] ? 0 : a.sel[2 * p];
+    if ((int)blockIdx.x * kKnnQueriesPerBlock >= nq || (int)blockIdx.y * a.per_chunk >= nt)
+        return;   // block-uniform
+    knn2_block(reinterpret_cast<const uint32_t *>(a.desc + (int64_t)32 * (p + 1) * a.kstride),
+               reinterpret_cast<const uint32_t *>(a.desc + (int64_t)32 * p * a.kstride),
+               a.keys + (int64_t)2 * p * a.kstride, nq, nt, a.per_chunk, blockIdx.x, blockIdx.y);
+}
+
+// grid (pairs), block 1024: pair p's kNN-2 keys -> Lowe's ratio (a second neighbour exists and
+// (double)d0 < (double)d1 * ratio, strict) -> the passing queries' positions (query and its best
+// train keypoint, level-0 pixels as the float (float)x * lscale[level]) compacted in query order
+// into pts; info[4 p] = their count.
+extern "C" __global__ __launch_bounds__(1024) void mcs_rig_match(const mcs::KRigArgs a)
+{
+    using namespace mcs;
+    const int p = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nq = a.sel[2 * (p + 1) + 1] ? 0 : a.sel[2 * (p + 1)];
+    const int nt = a.sel[2 * p + 1] ? 0 : a.sel[2 * p];
+    const uint32_t *keys = a.keys + (int64_t)2 * p * a.kstride;
+    const int *kq = a.kp + (int64_t)3 * (p + 1) * a.kstride, *kt = a.kp + (int64_t)3 * p * a.kstride;
+    double *pts = a.pts + (int64_t)4 * p * a.kstride;
+    __shared__ int wcount[16];
+    int base = 0;
+    for (int q0 = 0; q0 < (nt > 0 ? nq : 0); q0 += 1024) {
+        const int q = q0 + tid;
+        bool pass = false;
+        uint32_t k0 = kKeyNone;
+        if (q < nq) {
+            k0 = keys[2 * q];
+            const uint32_t k1 = keys[2 * q + 1];
+            pass = k1 != kKeyNone &&
+                   (double)(k0 >> kKnnKeyShift) < (double)(k1 >> kKnnKeyShift) * a.ratio;
+        }
+        const unsigned long long bal = __ballot(pass);
+        if (lane == 0) wcount[wave] = __popcll(bal);
+        __syncthreads();
+        int before = 0, total = 0;
+        for (int w = 0; w < 16; w++) {
+            before += w < wave ? wcount[w] : 0;
+            total += wcount[w];
+        }
+        if (pass) {
+            const int o = base + before + __popcll(bal & ((1ull << lane) - 1ull));
+            const int t = (int)(k0 & (kKnnMaxTrain - 1));
+            pts[4 * o] = (double)((float)kq[3 * q + 1] * a.lscale[kq[3 * q]]);
+            pts[4 * o + 1] = (double)((float)kq[3 * q + 2] * a.lscale[kq[3 * q]]);
+            pts[4 * o + 2] = (double)((float)kt[3 * t + 1] * a.lscale[kt[3 * t]]);
+            pts[4 * o + 3] = (double)((float)kt[3 * t + 2] * a.lscale[kt[3 * t]]);
+        }
+        base += total;
+        __syncthreads();
+    }
+    if (tid == 0) {
+        a.info[4 * p] = base;
+        a.info[4 * p + 3] = 0;
+    }
+}
+
+// grid (iters, pairs), block kRansacBlock: pair p's hypotheses (none -- scores -1 -- with 4 or
+// fewer matches: the reference needs more than 4 to call findHomography).
+extern "C" __global__ __launch_bounds__(256) void mcs_rig_ransac(const mcs::KRigArgs a)
+{
+    using namespace mcs;
+    const int p = blockIdx.y, k = blockIdx.x, n = a.info[4 * p];
+    int32_t *scores = a.scores + (int64_t)p * a.iters;
+    if (n <= 4) {
+        if (threadIdx.x == 0) scores[k] = -1;
+        return;
+    }
+    ransac_block(a.pts + (int64_t)4 * p * a.kstride, a.hyps + (int64_t)8 * p * a.iters, scores, n,
+                 a.seed, a.t2, k);
+}
+
+// grid (pairs), block 1024: pair p's best hypothesis -- the first of the highest score, as the
+// host scan -- into info[4 p + 1 ..] (index, score; -1, -1 without matches to score), its model
+// into hbest and, when it has 4 or more inliers, its inlier mask.
+extern "C" __global__ __launch_bounds__(1024) void mcs_rig_best(const mcs::KRigArgs a)
+{
+    using namespace mcs;
+    const int p = blockIdx.x, tid = threadIdx.x, n = a.info[4 * p];
+    const int32_t *scores = a.scores + (int64_t)p * a.iters;
+    __shared__ int ws[16], wi[16];
+    __shared__ int best_s, best_i;
+    int bs = -1, bi = -1;
+    if (n > 4)
+        for (int i = tid; i < a.iters; i += 1024)
+            if (scores[i] > bs) bs = scores[i], bi = i;   // ascending i: the first of the max
+    for (int off = 32; off > 0; off >>= 1) {
+        const int s2 = __shfl_down(bs, off, 64), i2 = __shfl_down(bi, off, 64);
+        if (s2 > bs || (s2 == bs && i2 >= 0 && (bi < 0 || i2 < bi))) bs = s2, bi = i2;
+    }
+    if ((tid & 63) == 0) ws[tid >> 6] = bs, wi[tid >> 6] = bi;
+    __syncthreads();
+    if (tid == 0) {
+        for (int w = 1; w < 16; w++)
+            if (ws[w] > bs || (ws[w] == bs && wi[w] >= 0 && (bi < 0 || wi[w] < bi)))
+                bs = ws[w], bi = wi[w];
+        best_s = bs;
+        best_i = bi;
+        a.info[4 * p + 1] = bi;
+        a.info[4 * p + 2] = bs;
+    }
+    __syncthreads();
+    bs = best_s;
+    bi = best_i;
+    if (bs < 4) return;
+    const double *h = a.hyps + ((int64_t)p * a.iters + bi) * 8;
+    if (tid < 8) a.hbest[8 * p + tid] = h[tid];
+    const double *pts = a.pts + (int64_t)4 * p * a.kstride;
+    uint8_t *mask = a.mask + (int64_t)p * a.kstride;
+    for (int i = tid; i < n; i += 1024) {
+        const double *q = pts + 4 * (int64_t)i;
+        mask[i] = rs_inlier(h, q[0], q[1], q[2], q[3], a.t2) ? 1 : 0;
     }
 }

@@ -71,6 +71,11 @@ struct OrbCand {
 // All levels of one frame in one launch (mcs_orb_level): grid (bstart[nlevels]) blocks of 256
 // threads, level l owning blocks [bstart[l], bstart[l + 1]), one block per 64 x 16 tile (row-major
 // over the level).  Level buffers are the bases + off[l] (pixels) and cand + coff[l].
+// Every ORB kernel also runs over a batch of frames (the cameras of a rig capture, grid.y =
+// camera c): camera c's level images at + c * stride pixels, its candidates at + c * cstride,
+// its counts at ncand + c * kOrbMaxLevels, its keypoints (kp, resp, desc, orient) at
+// + c * kstride keypoints, its sel at + 2 c.  Single-frame launches: grid.y = 1.
+constexpr int kOrbMaxCams = 16;
 struct KOrbPyrArgs {
     const uint8_t *img;
     uint8_t *blur;
@@ -79,6 +84,8 @@ struct KOrbPyrArgs {
     int64_t off[12];
     int coff[12], w[12], h[12], cap[12], bstart[13];
     int nlevels, threshold;
+    int64_t stride;
+    int cstride, pad_;
 };
 // The ORB pyramid in one launch (mcs_orb_pyramid): levels 1 .. nlevels-1, each OpenCV's
 // resize(INTER_LINEAR) of the level before it.  One block per tw x th tile of the LAST level;
@@ -93,6 +100,7 @@ struct KOrbBuildArgs {
     double sx[12], sy[12];
     int w[12], h[12];
     int nlevels, tw, th, gx, lds_w, lds_h;
+    int64_t stride;
 };
 struct KOrbDescArgs {
     const uint8_t *img[12], *blur[12];
@@ -101,7 +109,8 @@ struct KOrbDescArgs {
     uint8_t *desc;         // n x 32
     double *orient;        // n x 2: cos, sin
     const int *sel;        // mcs_orb_select's [n, overflow] (grid = the n bound), or NULL: n
-    int n, pad_;
+    int n, kstride;
+    int64_t stride;
 };
 // Per-level ranking on the device (mcs_orb_select): one block per level sorts the level's
 // candidates (<= kOrbSelMax, else the host ranks every level) and writes its quota's
@@ -115,12 +124,35 @@ struct KOrbSelArgs {
     double *resp;          // n
     int *sel;              // [2]: n, overflow
     int coff[12], cap[12], quota[12];
-    int nlevels, pad_;
+    int nlevels, cstride, kstride, pad_;
 };
 struct KGrayArgs {
-    const uint8_t *bgr;
-    uint8_t *gray;
+    const uint8_t *bgr[kOrbMaxCams];   // camera c = grid.y
+    uint8_t *gray;                     // camera c at gray + c * stride
+    int64_t stride;
     int n, pad_;
+};
+
+// A whole rig capture's estimation on the device (mcs_rig.cpp): after the batched ORB, per
+// adjacent pair p (query camera p + 1, train camera p) the Hamming kNN-2 (mcs_rig_knn2), Lowe's
+// ratio with the matched positions compacted in query order (mcs_rig_match), the RANSAC
+// hypotheses (mcs_rig_ransac) and the best one with its inlier mask (mcs_rig_best) -- counts read
+// from the device, so the chain needs no host round trip.
+struct KRigArgs {
+    const int *kp;          // camera c: kp + 3 c kstride (level, x, y)
+    const uint8_t *desc;    // camera c: desc + 32 c kstride
+    const int *sel;         // camera c: sel[2 c] keypoints, sel[2 c + 1] overflow
+    uint32_t *keys;         // pair p: keys + 2 p kstride (kNN-2 keys, 0xffffffff on entry)
+    double *pts;            // pair p: pts + 4 p kstride: x, y (camera p + 1), u, v (camera p)
+    int *info;              // pair p: info[4 p ..]: matches, best hypothesis, its score, 0
+    double *hyps;           // pair p: hyps + 8 p iters
+    int32_t *scores;        // pair p: scores + p iters
+    uint8_t *mask;          // pair p: mask + p kstride
+    double *hbest;          // pair p: hbest + 8 p
+    float lscale[12];       // level -> level-0 scale ((float)scale_factor^level)
+    double ratio, t2;
+    int kstride, iters, per_chunk;
+    uint32_t seed;
 };
 
 }  // namespace mcs

@@ -22,6 +22,7 @@
 //   keypoint     (x, y) * (float)1.2^level in level-0 pixels.
 #pragma once
 
+#include <math.h>
 #include <stdint.h>
 
 #include "mcs_orb_pattern.h"
@@ -45,24 +46,60 @@ constexpr int kFastCircle[16][2] = {{0, 3},  {1, 3},   {2, 2},   {3, 1},   {3, 0
                                     {2, -2}, {1, -3},  {0, -3},  {-1, -3}, {-2, -2}, {-3, -1},
                                     {-3, 0}, {-3, 1},  {-2, 2},  {-1, 3}};
 
-// FAST score of the pixel at p (row stride `step`).
+// FAST score of the pixel at p (row stride `step`): the arcs' minima by doubling windows
+// (2, 4, 8, then the ninth pixel) over the circle unrolled to 24 entries -- the same values as
+// the 16 x 9 scan, in a quarter of the operations.
 MCS_ORB_HD int orb_fast_score(const uint8_t *p, int step)
 {
-    int d[16];
+    int d[24], lo[23], hi[23];
     const int c = p[0];
     for (int i = 0; i < 16; i++) d[i] = (int)p[kFastCircle[i][1] * step + kFastCircle[i][0]] - c;
+    for (int i = 16; i < 24; i++) d[i] = d[i - 16];
+    // lo: min of d (I_p - I_c) over the window, hi: max of d (so min(I_c - I_p) = -hi)
+    for (int i = 0; i < 23; i++) {
+        lo[i] = d[i] < d[i + 1] ? d[i] : d[i + 1];
+        hi[i] = d[i] > d[i + 1] ? d[i] : d[i + 1];
+    }
+    for (int i = 0; i < 21; i++) {                       // windows of 4
+        lo[i] = lo[i] < lo[i + 2] ? lo[i] : lo[i + 2];
+        hi[i] = hi[i] > hi[i + 2] ? hi[i] : hi[i + 2];
+    }
     int best = -255;
-    for (int s = 0; s < 16; s++) {
-        int lo = 255, hi = 255;   // min(I_c - I_p), min(I_p - I_c) over the arc
-        for (int k = 0; k < 9; k++) {
-            const int v = d[(s + k) & 15];
-            lo = v < lo ? v : lo;
-            hi = -v < hi ? -v : hi;
-        }
-        const int m = lo > hi ? lo : hi;
+    for (int s = 0; s < 16; s++) {                       // windows of 8, then 9
+        int l = lo[s] < lo[s + 4] ? lo[s] : lo[s + 4];
+        int h = hi[s] > hi[s + 4] ? hi[s] : hi[s + 4];
+        l = l < d[s + 8] ? l : d[s + 8];
+        h = h > d[s + 8] ? h : d[s + 8];
+        const int m = l > -h ? l : -h;
         best = m > best ? m : best;
     }
     return best;
+}
+
+// FAST segment test: some arc of 9 contiguous circle pixels is entirely brighter than
+// I_c + t or entirely darker than I_c - t.  Exactly orb_fast_score(p) > t (an arc's
+// max(min(I_c - I_p), min(I_p - I_c)) exceeds t iff every pixel of it is beyond t on one side),
+// in bit operations: bit i of the masks per circle pixel, runs of 9 found on the mask doubled
+// to 32 bits (a & a >> 1: runs of 2, then 4, 8, and the ninth).
+MCS_ORB_HD bool orb_fast_test(const uint8_t *p, int step, int t)
+{
+    const int c = p[0];
+    uint32_t br = 0, dk = 0;
+    for (int i = 0; i < 16; i++) {
+        const int v = p[kFastCircle[i][1] * step + kFastCircle[i][0]];
+        br |= (uint32_t)(v > c + t) << i;
+        dk |= (uint32_t)(v < c - t) << i;
+    }
+    br |= br << 16;
+    dk |= dk << 16;
+    uint32_t a = br & (br >> 1), b = dk & (dk >> 1);
+    a &= a >> 2;
+    b &= b >> 2;
+    a &= a >> 4;
+    b &= b >> 4;
+    a &= br >> 8;
+    b &= dk >> 8;
+    return ((a | b) & 0xffffu) != 0;
 }
 
 // 3x3 Sobel gradients at p.

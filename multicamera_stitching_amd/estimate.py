@@ -7,10 +7,16 @@ re-estimates them for every capture; this module closes that loop on the GPU:
 
   1. ORB (nfeatures, 8 levels x 1.2, FAST 20) of every camera frame, read where it lies in device
      memory (mcs_orb_detect_device: the same frames are stitched afterwards, so nothing is
-     uploaded twice); one host thread per camera, each with its own HIP stream in libmcs;
+     uploaded twice);
   2. per adjacent pair (camera k+1 -> camera k): BF Hamming kNN-2 (mcs_match_hamming_knn2),
      Lowe's ratio 0.75 (strict, as :432), and findHomography's RANSAC + LM refinement
      (mcs_ransac_homography_host, 3.0 px);
+     steps 1-2 run as one mcs_rig_job in libmcs (csrc/mcs_rig.cpp): the cameras' ORBs side by
+     side on libmcs's worker threads (each with its own HIP stream), then the pairs, with no
+     interpreter between the steps.  submit() returns at once, so a caller holding two captures
+     in flight (slots 0 and 1) overlaps one capture's ORB with the previous one's pairs and
+     stitch.  features() / pair_homography() are the same steps issued from Python (kept as the
+     cross-check of the job: both give identical homographies);
   3. the chain geometry on the host: stage k maps camera k+1 into the mosaic of cameras 0..k,
      H_k = T(o_k) . H_0 . H_1 ... H_k (pair homographies composed into camera 0's frame, o_k =
      camera 0's origin in that mosaic), and each stage's plan fields come from geometry.py --
@@ -105,11 +111,45 @@ class CaptureEstimator:
         self.ahead = ThreadPoolExecutor(max_workers=1)
         self.last_H = [None] * (n_cams - 1)
         self.stats = {}
+        self._jobs = []
 
     def close(self):
+        for j in self._jobs:
+            if j is not None:
+                j.close()
+        self._jobs = []
         self.ahead.shutdown()
         self.fpool.shutdown()
         self.pool.shutdown()
+
+    def _job(self, slot):
+        if slot >= len(self._jobs):
+            self._jobs += [None] * (slot + 1 - len(self._jobs))
+        if self._jobs[slot] is None:
+            nf, nl, sf, ft = self.orb
+            self._jobs[slot] = _capi.RigJob(self.n_cams, self.w, self.h, self.c, nf, nl, sf, ft,
+                                            self.ratio, self.thresh, self.iters, self.seed,
+                                            self.device)
+        return self._jobs[slot]
+
+    def submit(self, frame_ptrs, wait_event: int = 0, slot: int = 0):
+        """Starts the estimation of one capture (device frame pointers) in rig-job `slot` (any
+        small index: one job per capture in flight) and returns at once.  wait_event: a hipEvent_t (e.g. torch.cuda.Event.cuda_event)
+        after which the frames are complete, or 0 when they already are.  The frames must stay
+        untouched until collect(slot)."""
+        self._job(slot).submit(frame_ptrs, wait_event)
+
+    def collect(self, slot: int = 0):
+        """Pair homographies of the capture submitted in `slot` (blocks until done); a failed
+        pair keeps the previous capture's estimate."""
+        res, st = self._jobs[slot].wait()
+        pair_H = []
+        for k, H in enumerate(res):
+            if H is not None:
+                self.last_H[k] = H
+            pair_H.append(self.last_H[k])
+        self.stats = st
+        return pair_H
 
     def features(self, frame_ptrs, pool=None):
         """ORB of every camera frame (device pointers, dense h x w x C, producers finished)."""
@@ -144,12 +184,14 @@ class CaptureEstimator:
         return (H if n_in > 0 else None), len(q), n_in
 
     def estimate(self, frame_ptrs):
-        """Pair homographies of one capture (camera k+1 -> camera k); a failed pair keeps the
-        previous capture's estimate."""
-        return self.estimate_from(self.features(frame_ptrs))
+        """Pair homographies of one capture (camera k+1 -> camera k), through the rig job; a
+        failed pair keeps the previous capture's estimate."""
+        self.submit(frame_ptrs)
+        return self.collect()
 
     def estimate_from(self, feats):
-        """estimate() from the capture's features (features / features_async)."""
+        """The pair step issued from Python, from the capture's features (features /
+        features_async); same result as the rig job."""
         res = list(self.pool.map(lambda k: self.pair_homography(feats[k + 1], feats[k]),
                                  range(self.n_cams - 1)))
         pair_H = []

@@ -111,3 +111,22 @@ def test_passthrough_stages_flatten_away():
     assert fl["n_stages"] == 1 and fl["cam"] == [2]
     p2 = _capi.Plan([un], 64, 48, 1)
     assert p2.out_shape() == (48, 64)
+
+
+def test_rig_job_host_validation():
+    """mcs_rig_job: creation touches no GPU; bad shapes and a wait with nothing submitted are
+    status codes, not crashes."""
+    L = _capi.load()
+    j = _capi.RigJob(4, 640, 480, 3)
+    with pytest.raises(_capi.McsError) as e:
+        j.wait()
+    assert e.value.code == _capi.MCS_E_INVALID
+    j.close()
+    for bad in ({"n_cams": 1}, {"channels": 2}, {"nfeatures": 0}, {"iters": 0}):
+        kw = dict(n_cams=4, w=640, h=480, channels=3)
+        kw.update(bad)
+        with pytest.raises(_capi.McsError) as e:
+            _capi.RigJob(**kw)
+        assert e.value.code == _capi.MCS_E_INVALID
+    assert L.mcs_rig_job_submit(None, None, None) == _capi.MCS_E_INVALID
+    assert L.mcs_rig_job_destroy(None) == _capi.MCS_OK

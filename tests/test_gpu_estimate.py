@@ -59,6 +59,49 @@ def test_estimate_then_stitch_full_size(super_mode):
         est.close()
 
 
+def test_rig_job_equals_python_issued_steps():
+    """mcs_rig_job's device path (the capture as one launch chain: ORB batched over the cameras,
+    matching / ratio / RANSAC / best model batched over the pairs, csrc/mcs_rig.cpp) gives the very
+    homographies, keypoint, match and inlier counts of the per-call steps issued one by one from
+    Python; two jobs in flight at once
+    (slots 0 and 1, one waiting on an upload event) give the same result as one."""
+    import torch
+    from multicamera_stitching_amd import estimate
+    W, H, N = 960, 540, 4
+    _, frames, _ = rig.estimation_rig(N, W, H, 3, seed=2)
+    dev = torch.device("cuda", 0)
+    d = [torch.from_numpy(f).to(dev) for f in frames]
+    torch.cuda.synchronize()
+    ptrs = [t.data_ptr() for t in d]
+    est = estimate.CaptureEstimator(N, W, H, 3, nfeatures=1000)
+    try:
+        py = est.estimate_from(est.features(ptrs))
+        py_stats = dict(est.stats)
+        est.last_H = [None] * (N - 1)
+        job = est.estimate(ptrs)
+        assert est.stats == py_stats
+        for a, b in zip(py, job):
+            assert (a is None) == (b is None)
+            if a is not None:
+                assert np.array_equal(a, b)
+        s = torch.cuda.Stream()
+        d2 = [torch.empty_like(t) for t in d]
+        ev = torch.cuda.Event()
+        with torch.cuda.stream(s):
+            for a, b in zip(d2, d):
+                a.copy_(b, non_blocking=True)
+            ev.record(s)
+        est.submit([t.data_ptr() for t in d2], ev.cuda_event, 1)
+        est.submit(ptrs, 0, 0)
+        r0, r1 = est.collect(0), est.collect(1)
+        for a, b, c in zip(job, r0, r1):
+            assert np.array_equal(a, b) and np.array_equal(a, c)
+        # every capture ran as the one launch chain (no ranking overflow at this size)
+        assert est._jobs[0].counts() == (2, 0) and est._jobs[1].counts() == (1, 0)
+    finally:
+        est.close()
+
+
 def test_orb_device_input_equals_host_input():
     import torch
     from multicamera_stitching_amd import _capi

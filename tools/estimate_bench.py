@@ -104,10 +104,14 @@ def main():
     ap.add_argument("--stitch", action="store_true",
                     help="estimate -> stitch per capture (estimate.py, mcs_stitch_direct)")
     ap.add_argument("--overlap", action="store_true",
-                    help="with --pipelined: ORB of capture f+1 beside the pairs + stitch of f")
+                    help="with --pipelined: each capture's estimation in its own rig job "
+                         "(mcs_rig_job), started once its upload is queued, so the ORBs of the "
+                         "next captures run beside the pairs + stitch of this one")
     ap.add_argument("--pipelined", action="store_true",
                     help="with --stitch: upload capture f+1 (pinned host frames, own stream, two "
                          "device frame sets) while capture f is estimated and stitched")
+    ap.add_argument("--depth", type=int, default=2,
+                    help="with --pipelined: captures in flight (frame sets, rig jobs, outputs)")
     ap.add_argument("--pinned", action="store_true",
                     help="camera frames in pinned host buffers (default: pageable numpy arrays, "
                          "as the reference's capture loop holds them)")
@@ -241,29 +245,33 @@ def stitch_main(args, frames, truth, W, Hh, N):
 
 
 def pipelined_main(args, frames, truth, W, Hh, N):
-    """Config 3 end to end, pipelined: the cameras' frames of capture f+1 go up (pinned host
-    buffers, a dedicated stream, two device frame sets) while capture f is estimated and stitched
-    (its stitch on its own stream; a plan is released once its stitch has finished)."""
+    """Config 3 end to end, pipelined --depth captures deep: the cameras' frames of capture f+D-1
+    go up (pinned host buffers, a dedicated stream, D device frame sets) while the captures before
+    it are estimated (with --overlap: each in its own rig job, submitted as soon as its upload is
+    queued, its ORB streams waiting on the upload event on the GPU) and stitched (its stitch on
+    its own stream; a plan is released once its stitch has finished)."""
     import torch
     from multicamera_stitching_amd import estimate
     from oracle import oracle
+    D = max(2, args.depth)
     dev = torch.device("cuda", 0)
     host = []
     for f in frames:
         t = torch.empty(f.shape, dtype=torch.uint8, pin_memory=True)
         t.numpy()[...] = f
         host.append(t)
-    d = [[torch.empty(f.shape, dtype=torch.uint8, device=dev) for f in frames] for _ in range(2)]
+    d = [[torch.empty(f.shape, dtype=torch.uint8, device=dev) for f in frames] for _ in range(D)]
     ptrs = [[t.data_ptr() for t in ds] for ds in d]
     pitch = 8192 * 3
-    out = [torch.empty((2048, pitch), dtype=torch.uint8, device=dev) for _ in range(2)]
+    out = [torch.empty((2048, pitch), dtype=torch.uint8, device=dev) for _ in range(D)]
     up, st = torch.cuda.Stream(), torch.cuda.Stream()
-    ev_up = [torch.cuda.Event() for _ in range(2)]
-    ev_done = [torch.cuda.Event() for _ in range(2)]
+    ev_up = [torch.cuda.Event() for _ in range(D)]
+    ev_done = [torch.cuda.Event() for _ in range(D)]
     for e in ev_done:
         e.record(st)
     est = estimate.CaptureEstimator(N, W, Hh, 3, nfeatures=args.nfeatures, threads=args.threads)
-    pending = [None, None]        # plan of the capture last stitched from frame set / output i
+    pending = [None] * D          # plan of the capture last stitched from frame set / output i
+    lat = []
 
     def upload(slot):
         with torch.cuda.stream(up):
@@ -272,26 +280,29 @@ def pipelined_main(args, frames, truth, W, Hh, N):
                 t.copy_(h, non_blocking=True)
             ev_up[slot].record(up)
 
+    def start(i, t_start):
+        slot = i % D
+        upload(slot)
+        t_start[slot] = time.perf_counter()
+        if args.overlap:
+            est.submit(ptrs[slot], ev_up[slot].cuda_event, slot)
+
     def run(n):
         mpix = 0.0
-        upload(0)
-        fut = est.features_async(ptrs[0], ev_up[0].synchronize) if args.overlap else None
+        t_start = [0.0] * D
+        lat.clear()
+        for i in range(min(D - 1, n)):
+            start(i, t_start)
         for i in range(n):
-            slot = i & 1
+            slot = i % D
+            if i + D - 1 < n:
+                start(i + D - 1, t_start)
             if args.overlap:
-                # two-stage pipeline: the ORB of capture i+1 (its frames uploaded into the other
-                # set once that set's previous stitch is done) runs while capture i's pairs are
-                # matched, estimated and stitched
-                feats = fut.result()
-                if i + 1 < n:
-                    upload(slot ^ 1)
-                    fut = est.features_async(ptrs[slot ^ 1], ev_up[slot ^ 1].synchronize)
-                pair_H = est.estimate_from(feats)
+                pair_H = est.collect(slot)
             else:
-                if i + 1 < n:
-                    upload(slot ^ 1)
                 ev_up[slot].synchronize()             # this capture's frames are on the device
                 pair_H = est.estimate(ptrs[slot])
+            lat.append(time.perf_counter() - t_start[slot])
             if pending[slot] is not None:         # the set's previous plan: its stitch is done
                 ev_done[slot].synchronize()
                 pending[slot].close()
@@ -328,9 +339,12 @@ def pipelined_main(args, frames, truth, W, Hh, N):
                                "2000 hypotheses + LM; chain geometry + plan on the host; "
                                "mcs_stitch_direct (paste)" % args.nfeatures,
                    "host_frames": "pinned, uploaded every capture on their own stream while the "
-                                  "previous capture is estimated and stitched",
+                                  "previous captures are estimated and stitched",
+                   "pipeline_depth": D, "rig_jobs": bool(args.overlap),
                    "host_threads": args.threads},
-        "max_reproj_err_px_vs_truth": errs,
+        "latency_ms_upload_to_homographies": round(float(np.mean(lat)) * 1e3, 3),
+        "keypoints": est.stats.get("keypoints"), "matches": est.stats.get("matches"),
+        "inliers": est.stats.get("inliers"), "max_reproj_err_px_vs_truth": errs,
         "max_abs_diff_vs_cpu_render": int(np.abs(got.astype(np.int16) - want).max()),
     }))
 
