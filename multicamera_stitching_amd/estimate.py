@@ -26,7 +26,11 @@ re-estimates them for every capture; this module closes that loop on the GPU:
 
 A pair whose estimate fails (too few matches or inliers, the reference's H = None) keeps the
 previous capture's homography for that pair; with none yet, its stage stays uncalibrated and
-passes B through, as the reference's reset() stage does (:253-256).
+passes B through, as the reference's reset() stage does (:253-256) -- and so do all the stages
+after it: their pair homographies are relative to a camera that has no place in the mosaic.
+(The reference would still try to match each later camera against the mosaic B of the cameras
+before the gap, which for a linear rig's non-adjacent cameras has no overlap to match; a rig that
+needs that case should calibrate once, StitcherClass's own path, rather than per capture.)
 
 (The reference matches camera k+1 against the mosaic B_k; matching it against camera k and
 composing gives the same homography up to estimation noise without re-stitching the mosaic
@@ -56,7 +60,9 @@ def ratio_filter(idx, dist, ratio: float = 0.75):
 def chain_stages(pair_H, cam_shapes, super_mode: bool = False):
     """Stage records (the StitcherBase fields the plan needs) of a left-to-right chain whose
     adjacent-pair homographies pair_H[k] map camera k+1 into camera k (None: uncalibrated).
-    cam_shapes: (h, w[, C]) of every camera in sorted-label order."""
+    cam_shapes: (h, w[, C]) of every camera in sorted-label order.  The first None leaves its
+    stage and every later one uncalibrated (pass-through): the later homographies are relative
+    to cameras with no place in the mosaic (see the module docstring)."""
     stages = []
     b_shape = tuple(cam_shapes[0])
     ox, oy = 0, 0               # camera 0's origin in the mosaic B_k
