@@ -155,16 +155,17 @@ int knn2(const Api *A, const FeatureKernels *k, const uint8_t *q, int nq, const 
     a.nq = nq;
     a.nt = nt;
     a.pad_ = 0;
-    // enough (query wave x train chunk) blocks to fill the chip -- a 2000 x 2000 frame pair is
-    // ~1000 waves -- with chunks of >= 64 descriptors (3 atomics per query and chunk)
+    // enough (query wave x train chunk) blocks to fill the chip twice over (16384 waves: 16 per
+    // SIMD, the compare loop's LDS-read latency needs them; 4096 left waves waiting on it half
+    // their cycles) with chunks of >= 64 descriptors (3 atomics per query and chunk)
     const int qblocks = (nq + mcs::kKnnQueriesPerBlock - 1) / mcs::kKnnQueriesPerBlock;
-    int chunks = (4096 + qblocks - 1) / qblocks;
+    int chunks = (mcs::kKnnTargetBlocks + qblocks - 1) / qblocks;
     chunks = std::max(1, std::min(chunks, (nt + 63) / 64));
     a.per_chunk = (nt + chunks - 1) / chunks;
     chunks = nt > 0 ? (nt + a.per_chunk - 1) / a.per_chunk : 0;
     int rc = MCS_OK;
     if (chunks > 0)
-        rc = launch(A, k->knn2, qblocks, chunks, mcs::kKnnQueriesPerBlock, &a, sizeof(a), s);
+        rc = launch(A, k->knn2, qblocks, chunks, mcs::kKnnLanes, &a, sizeof(a), s);
     if (rc == MCS_OK)
         rc = launch(A, k->knn2_finalize, (2 * nq + 255) / 256, 1, 256, &a, sizeof(a), s);
     return rc;

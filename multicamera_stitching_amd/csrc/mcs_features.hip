@@ -47,24 +47,33 @@ __device__ __forceinline__ uint32_t hamming_lds(const uint32_t (&q)[8], const ui
 
 namespace mcs {
 
-// One block of the kNN-2: queries blockIdx.x * 64 + lane against train chunk `chunk`, merged into
-// keys (0xffffffff on entry) by atomicMin.  nq > 0.
+// One block of the kNN-2: queries qblock * kKnnQueriesPerBlock + lane + 64 i (i < kKnnQueriesPerLane)
+// against train chunk `chunk`, merged into keys (0xffffffff on entry) by atomicMin.  Each train
+// descriptor staged in LDS is read back once per lane (two 16-byte broadcast reads) and compared
+// with all of the lane's queries: the LDS return path (1 KiB per wave per read) is shared by more
+// pairs.  nq > 0.
 __device__ __forceinline__ void knn2_block(const uint32_t *query, const uint32_t *train,
                                            uint32_t *keys, int nq, int nt, int per_chunk,
                                            int qblock, int chunk)
 {
-    const int q = qblock * kKnnQueriesPerBlock + threadIdx.x;
-    uint32_t d[8];
-    const uint4 *qs = reinterpret_cast<const uint4 *>(query + (int64_t)min(q, nq - 1) * 8);
-    const uint4 v0 = qs[0], v1 = qs[1];
-    d[0] = v0.x, d[1] = v0.y, d[2] = v0.z, d[3] = v0.w;
-    d[4] = v1.x, d[5] = v1.y, d[6] = v1.z, d[7] = v1.w;
+    constexpr int QL = kKnnQueriesPerLane;
+    uint32_t d[QL][8];
+#pragma unroll
+    for (int i = 0; i < QL; i++) {
+        const int q = qblock * kKnnQueriesPerBlock + i * kKnnLanes + threadIdx.x;
+        const uint4 *qs = reinterpret_cast<const uint4 *>(query + (int64_t)min(q, nq - 1) * 8);
+        const uint4 v0 = qs[0], v1 = qs[1];
+        d[i][0] = v0.x, d[i][1] = v0.y, d[i][2] = v0.z, d[i][3] = v0.w;
+        d[i][4] = v1.x, d[i][5] = v1.y, d[i][6] = v1.z, d[i][7] = v1.w;
+    }
     const int j0 = chunk * per_chunk, j1 = min(nt, j0 + per_chunk);
     const uint4 *__restrict__ train4 = reinterpret_cast<const uint4 *>(train);
-    __shared__ uint4 tl[2 * kKnnQueriesPerBlock];
-    uint32_t k0 = kKeyNone, k1 = kKeyNone;
-    for (int jt = j0; jt < j1; jt += kKnnQueriesPerBlock) {
-        const int n = min(kKnnQueriesPerBlock, j1 - jt);
+    __shared__ uint4 tl[2 * kKnnLanes];
+    uint32_t k0[QL], k1[QL];
+#pragma unroll
+    for (int i = 0; i < QL; i++) k0[i] = k1[i] = kKeyNone;
+    for (int jt = j0; jt < j1; jt += kKnnLanes) {
+        const int n = min(kKnnLanes, j1 - jt);
         if ((int)threadIdx.x < n) {
             const uint4 *src = train4 + (int64_t)(jt + threadIdx.x) * 2;
             const uint4 t0 = src[0], t1 = src[1];
@@ -74,26 +83,44 @@ __device__ __forceinline__ void knn2_block(const uint32_t *query, const uint32_t
         __syncthreads();
         int u = 0;
         for (; u + 4 <= n; u += 4) {
-            uint32_t c[4];
+            uint32_t c[QL][4];
 #pragma unroll
-            for (int v = 0; v < 4; v++) c[v] = hamming_lds(d, tl + 2 * (u + v));
+            for (int v = 0; v < 4; v++) {
+                const uint4 a = tl[2 * (u + v)], b = tl[2 * (u + v) + 1];
+#pragma unroll
+                for (int i = 0; i < QL; i++)
+                    c[i][v] = __popc(d[i][0] ^ a.x) + __popc(d[i][1] ^ a.y) +
+                              __popc(d[i][2] ^ a.z) + __popc(d[i][3] ^ a.w) +
+                              __popc(d[i][4] ^ b.x) + __popc(d[i][5] ^ b.y) +
+                              __popc(d[i][6] ^ b.z) + __popc(d[i][7] ^ b.w);
+            }
 #pragma unroll
             for (int v = 0; v < 4; v++)
-                top2(k0, k1, (c[v] << kKnnKeyShift) | (uint32_t)(jt + u + v));
+#pragma unroll
+                for (int i = 0; i < QL; i++)
+                    top2(k0[i], k1[i], (c[i][v] << kKnnKeyShift) | (uint32_t)(jt + u + v));
         }
         for (; u < n; u++)
-            top2(k0, k1, (hamming_lds(d, tl + 2 * u) << kKnnKeyShift) | (uint32_t)(jt + u));
+#pragma unroll
+            for (int i = 0; i < QL; i++)
+                top2(k0[i], k1[i],
+                     (hamming_lds(d[i], tl + 2 * u) << kKnnKeyShift) | (uint32_t)(jt + u));
         __syncthreads();
     }
-    if (q >= nq) return;
-    const uint32_t old = atomicMin(&keys[2 * q], k0);
-    atomicMin(&keys[2 * q + 1], max(old, k0));
-    atomicMin(&keys[2 * q + 1], k1);
+#pragma unroll
+    for (int i = 0; i < QL; i++) {
+        const int q = qblock * kKnnQueriesPerBlock + i * kKnnLanes + threadIdx.x;
+        if (q >= nq) break;
+        const uint32_t old = atomicMin(&keys[2 * q], k0[i]);
+        atomicMin(&keys[2 * q + 1], max(old, k0[i]));
+        atomicMin(&keys[2 * q + 1], k1[i]);
+    }
 }
 
 }  // namespace mcs
 
-// grid (ceil(nq / 64), chunks), block 64.  keys must hold 0xffffffff on entry (memset).
+// grid (ceil(nq / kKnnQueriesPerBlock), chunks), block 64.  keys must hold 0xffffffff on entry
+// (memset).
 extern "C" __global__ __launch_bounds__(64) void mcs_hamming_knn2(const mcs::KHammingArgs a)
 {
     mcs::knn2_block(a.query, a.train, a.keys, a.nq, a.nt, a.per_chunk, blockIdx.x, blockIdx.y);
@@ -735,7 +762,7 @@ extern "C" __global__ __launch_bounds__(256) void mcs_orb_pyramid(const mcs::KOr
 }
 
 // ---- A rig capture on the device (mcs_rig.cpp; KRigArgs) ---------------------------------------
-// grid (ceil(kstride / 64), chunks, pairs), block 64: pair p's kNN-2, query camera p + 1 against
+// grid (ceil(kstride / kKnnQueriesPerBlock), chunks, pairs), block 64: pair p's kNN-2, query camera p + 1 against
 // train camera p, the keypoint counts read from the device (a camera whose ranking overflowed
 // counts as empty: the host redoes that capture through the per-call path).
 extern "C" __global__ __launch_bounds__(64) void mcs_rig_knn2(const mcs::KRigArgs a)

@@ -9,9 +9,18 @@ namespace mcs {
 // Brute-force Hamming kNN-2 over 256-bit descriptors (BFMatcher(NORM_HAMMING).knnMatch(k=2),
 // the per-frame matcher of SURVEY.md 8 NS-4; reference counterpart StitcherClass.py:405-448).
 constexpr int kDescBytes = 32;
-constexpr int kKnnQueriesPerBlock = 64;   // one query per lane
+#ifndef MCS_KNN_QPL
+#define MCS_KNN_QPL 1
+#endif
+constexpr int kKnnLanes = 64;                               // one wave per block
+constexpr int kKnnQueriesPerLane = MCS_KNN_QPL;             // each staged train descriptor
+constexpr int kKnnQueriesPerBlock = kKnnLanes * kKnnQueriesPerLane;   // serves this many
 constexpr int kKnnKeyShift = 23;          // key = distance << 23 | train index
 constexpr int kKnnMaxTrain = 1 << kKnnKeyShift;
+#ifndef MCS_KNN_TARGET_BLOCKS
+#define MCS_KNN_TARGET_BLOCKS 65536
+#endif
+constexpr int kKnnTargetBlocks = MCS_KNN_TARGET_BLOCKS;   // (query wave, train chunk) blocks
 struct KHammingArgs {
     const uint32_t *query;   // nq x 8 words
     const uint32_t *train;   // nt x 8 words

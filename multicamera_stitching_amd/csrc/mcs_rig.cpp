@@ -358,7 +358,7 @@ int device_setup(mcs_rig_job *j)
     // kNN-2 blocks: query waves x train chunks x pairs, enough to fill the chip (as the per-call
     // matcher sizes them; the result does not depend on the chunking)
     d.knn_qblocks = (unsigned)((K + mcs::kKnnQueriesPerBlock - 1) / mcs::kKnnQueriesPerBlock);
-    int chunks = (int)((4096 + d.knn_qblocks * P - 1) / (d.knn_qblocks * P));
+    int chunks = (int)((mcs::kKnnTargetBlocks + d.knn_qblocks * P - 1) / (d.knn_qblocks * P));
     chunks = std::max(1, std::min(chunks, (K + 63) / 64));
     d.ra.per_chunk = (K + chunks - 1) / chunks;
     d.knn_chunks = (unsigned)((K + d.ra.per_chunk - 1) / d.ra.per_chunk);
@@ -431,7 +431,7 @@ int device_capture(mcs_rig_job *j, bool *overflow)
     if (rc == MCS_OK && g.n_bound > 0)
         rc = launch(A, k->orb_describe, (unsigned)g.n_bound, C, 64, &d.da, sizeof(d.da), s);
     if (rc == MCS_OK)
-        rc = launch(A, k->rig_knn2, d.knn_qblocks, d.knn_chunks, mcs::kKnnQueriesPerBlock, &d.ra,
+        rc = launch(A, k->rig_knn2, d.knn_qblocks, d.knn_chunks, mcs::kKnnLanes, &d.ra,
                     sizeof(d.ra), s, (unsigned)P);
     if (rc == MCS_OK) rc = launch(A, k->rig_match, (unsigned)P, 1, 1024, &d.ra, sizeof(d.ra), s);
     if (rc == MCS_OK)

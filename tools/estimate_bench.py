@@ -112,6 +112,9 @@ def main():
                          "device frame sets) while capture f is estimated and stitched")
     ap.add_argument("--depth", type=int, default=2,
                     help="with --pipelined: captures in flight (frame sets, rig jobs, outputs)")
+    ap.add_argument("--resident", action="store_true",
+                    help="with --pipelined: the frames stay in HBM (no per-capture upload): the "
+                         "GPU-bound rate of estimate + stitch")
     ap.add_argument("--pinned", action="store_true",
                     help="camera frames in pinned host buffers (default: pageable numpy arrays, "
                          "as the reference's capture loop holds them)")
@@ -276,9 +279,16 @@ def pipelined_main(args, frames, truth, W, Hh, N):
     def upload(slot):
         with torch.cuda.stream(up):
             up.wait_event(ev_done[slot])          # that set's previous stitch has read it
-            for t, h in zip(d[slot], host):
-                t.copy_(h, non_blocking=True)
+            if not args.resident:
+                for t, h in zip(d[slot], host):
+                    t.copy_(h, non_blocking=True)
             ev_up[slot].record(up)
+
+    if args.resident:                             # the frames stay in HBM: uploaded once
+        for ds in d:
+            for t, h in zip(ds, host):
+                t.copy_(h)
+        torch.cuda.synchronize()
 
     def start(i, t_start):
         slot = i % D
@@ -342,6 +352,7 @@ def pipelined_main(args, frames, truth, W, Hh, N):
                                   "previous captures are estimated and stitched",
                    "pipeline_depth": D, "rig_jobs": bool(args.overlap),
                    "host_threads": args.threads},
+        "frames_resident_in_hbm": bool(args.resident),
         "latency_ms_upload_to_homographies": round(float(np.mean(lat)) * 1e3, 3),
         "keypoints": est.stats.get("keypoints"), "matches": est.stats.get("matches"),
         "inliers": est.stats.get("inliers"), "max_reproj_err_px_vs_truth": errs,
