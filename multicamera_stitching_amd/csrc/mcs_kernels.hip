@@ -544,15 +544,16 @@ __device__ __forceinline__ void prepare_tile(const KParams &P, TileHdr *tiles, u
                 break;
             }
             const int cal = fl.cmin[c] & ~15;
-            const int stride = (fl.cmax[c] + 8 - cal + 15) & ~15;
+            const int stride = (fl.cmax[c] + 8 - cal + 15) & ~15;   // DMA bytes per row
+            const int lpitch = lds_row_pitch(stride);                 // LDS row spacing
             const int rows = fl.rmax[c] - fl.rmin[c] + 1;
             th.cam[n] = c;
             th.rmin[n] = fl.rmin[c];
             th.cal[n] = cal;
-            th.stride[n] = stride;
+            th.stride[n] = lpitch | ((stride >> 4) << 16);
             th.base[n] = total;
             th.jobstart[n] = jobs;
-            total += rows * stride;
+            total += rows * lpitch;
             jobs += rows;
             if (stride > 16 * kWave) fits = 0;
             // DMA chunks must end inside the camera frame: the frame's last row is fetched from
@@ -589,7 +590,7 @@ __device__ __forceinline__ void prepare_tile(const KParams &P, TileHdr *tiles, u
     for (int p = 0; p < kPx; p++) {
         int k = 0;
         while (k < th.ncam - 1 && th.cam[k] != g[p].cam) k++;
-        const int st = th.stride[k], rm = th.rmin[k], ca = th.cal[k], bs = th.base[k];
+        const int st = th.stride[k] & 0xffff, rm = th.rmin[k], ca = th.cal[k], bs = th.base[k];
         const int last = P.cam_h[g[p].cam] - 1, e = (th.last_shift >> (8 * k)) & 255;
         uint32_t a0 = (uint32_t)(bs + (g[p].r0 - rm) * st + (g[p].c0 - ca) +
                                  (g[p].r0 == last ? e : 0));
@@ -691,7 +692,8 @@ __device__ __forceinline__ WaveJobs<BUF> wave_jobs(const KParams &P, const TileH
                                        (uint64_t)(uintptr_t)P.base + (uint64_t)in_frame);
             else
                 J.src[jj] = P.cams[c] + in_frame;
-            J.w[jj] = (uint32_t)(uni(h.base[k]) + row * stride) | ((uint32_t)(stride >> 4) << 16);
+            J.w[jj] = (uint32_t)(uni(h.base[k]) + row * (stride & 0xffff)) |
+                      ((uint32_t)stride & 0xffff0000u);
             J.n = jj + 1;
         }
     }
@@ -809,7 +811,8 @@ __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *til
                 const int k = (int)((w >> 26) & 3u);
                 const uint32_t e = (w & kCwLastRow1) ? ((uint32_t)h.last_shift >> (8 * k)) & 255u
                                                      : 0u;
-                const uint32_t a1 = (w & kCwOneRow) ? a0 : a0 + (uint32_t)h.stride[k] + e;
+                const uint32_t a1 =
+                    (w & kCwOneRow) ? a0 : a0 + ((uint32_t)h.stride[k] & 0xffffu) + e;
                 d0 = a0 | (a1 << 16);
                 d1 = w2x((32u - fx) * (32u - fy) * 32u) | (w2x(fx * (32u - fy) * 32u) << 16);
                 d2 = w2x((32u - fx) * fy * 32u) | (w2x(fx * fy * 32u) << 16);

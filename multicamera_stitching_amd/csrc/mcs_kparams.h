@@ -103,6 +103,7 @@ constexpr uint32_t kCwOneRow = 1u << 31;     // fy = 0: row 1 unused (= row 0)
 struct TileHdr {
     int fits;                      // 1: LDS path, 0: listed for the direct-gather launch
     int ncam, njobs, ring, buf_bytes;
+    // stride[k]: LDS row pitch (bits 0-15) | 16-byte DMA chunks per row (bits 16-23)
     int cam[kTileCams], rmin[kTileCams], cal[kTileCams], stride[kTileCams], base[kTileCams];
     int jobstart[kTileCams + 1];
     // per camera slot k, byte k: how far the DMA of the camera frame's LAST row starts earlier
@@ -314,6 +315,15 @@ constexpr int kMaxRing = 6;
 #endif
 constexpr int lds_stream_bytes(int cn) { return cn >= 3 ? MCS_STREAM_LDS : 40960; }
 constexpr int lds_ring_bytes(int cn) { return lds_stream_bytes(cn) - (int)sizeof(TileHdr); }
+// LDS row pitch of a footprint row of `bytes` DMA bytes.  The 32 lanes of an output row read
+// dwords ~3 apart (C = 3, 4 pixels per lane: a permutation of the 32 ds_read_b32 banks); where
+// the source row changes inside the lane group (a rotated map), the lanes past the change read
+// one pitch further -- conflict-free only when the pitch is a multiple of 128 bytes (32 banks).
+// MCS_STREAM_PITCH128=0: packed rows (pitch = bytes).
+#ifndef MCS_STREAM_PITCH128
+#define MCS_STREAM_PITCH128 1
+#endif
+constexpr int lds_row_pitch(int bytes) { return MCS_STREAM_PITCH128 ? (bytes + 127) & ~127 : bytes; }
 
 
 // Seam-finder inputs (mcs_plan_find_seams): per point of the 2^k grid the distance owner's
