@@ -172,8 +172,9 @@ int mcs_plan_set_blend(mcs_plan *plan, int mode);
  * (cost: colour difference of the two cameras, OpenCV GraphCutSeamFinder COST_COLOR style) on
  * the 2^scale_log2-subsampled panorama of this capture (cams: host frames at calibrated sizes),
  * then every pixel takes its grid point's camera when that camera covers it.  Once per plan
- * (calibration time: device sampling + host max-flow); drops the prepared tables.  The exact
- * rules: oracle/orc_seam.c.  scale_log2: 0..4. */
+ * (calibration time: device sampling + device push-relabel max-flows, MCS_SEAM_FLOW=host: the
+ * host Dinic; both give the same cut); drops the prepared tables.  The exact rules:
+ * oracle/orc_seam.c.  scale_log2: 0..4. */
 enum { MCS_SEAM_DISTANCE = 0, MCS_SEAM_GRAPHCUT = 1 };
 int mcs_plan_find_seams(mcs_plan *plan, const uint8_t *const *cams, int method, int scale_log2);
 /* The current seam labels (camera per grid point, 255 = none): *w, *h = grid size (0 when the
@@ -184,6 +185,14 @@ int mcs_plan_seam_labels(const mcs_plan *plan, uint8_t *out, int *w, int *h);
  * samples [camera][point][channels].  grid gw x gh, up to 16 cameras. */
 int mcs_seam_graphcut_host(int n_cams, int gw, int gh, uint8_t *labels, const uint16_t *cover,
                            const uint8_t *samples, int channels);
+/* The same pairwise cuts on the device (push-relabel, the path mcs_plan_find_seams takes by
+ * default; MCS_SEAM_FLOW=host selects the host Dinic there): host arrays in, labels updated in
+ * place.  stats (5, may be NULL): pairs with a graph, push launches, relabel launches, global
+ * relabels, microseconds of the max-flows. */
+int mcs_seam_graphcut_device(int n_cams, int gw, int gh, uint8_t *labels, const uint16_t *cover,
+                             const uint8_t *samples, int channels, int device, int64_t *stats);
+/* The device max-flow's counts of the plan's last mcs_plan_find_seams (as above). */
+int mcs_plan_seam_stats(const mcs_plan *plan, int64_t *stats);
 
 /* Stitcher.stitch on host arrays (drop-in path, :114-136): cams[i] is the i-th camera in
  * sorted-label order, dense HxWxC u8 of the calibrated size; out is a dense out_h x out_w x C

@@ -48,6 +48,7 @@ EXPORTS = (
     "mcs_stitch_direct", "mcs_orb_detect_device", "mcs_group_unique_id", "mcs_group_create",
     "mcs_group_gather", "mcs_group_destroy", "mcs_rccl_library", "mcs_rig_job_create",
     "mcs_rig_job_submit", "mcs_rig_job_wait", "mcs_rig_job_counts", "mcs_rig_job_destroy",
+    "mcs_seam_graphcut_device", "mcs_plan_seam_stats",
 )
 MCS_GROUP_ID_BYTES = 128
 
@@ -214,6 +215,10 @@ def load() -> ctypes.CDLL:
         L.mcs_rig_job_submit.restype = I
         L.mcs_rig_job_wait.argtypes = [P, P, P, P, P, P]
         L.mcs_rig_job_wait.restype = I
+        L.mcs_seam_graphcut_device.argtypes = [I, I, I, P, P, P, I, I, P]
+        L.mcs_seam_graphcut_device.restype = I
+        L.mcs_plan_seam_stats.argtypes = [P, P]
+        L.mcs_plan_seam_stats.restype = I
         L.mcs_rig_job_counts.argtypes = [P, P, P]
         L.mcs_rig_job_counts.restype = I
         L.mcs_rig_job_destroy.argtypes = [P]
@@ -453,6 +458,13 @@ class Plan:
         check(self._lib.mcs_plan_seam_labels(self._h, out.ctypes.data_as(ctypes.c_void_p),
                                              ctypes.byref(w), ctypes.byref(h)))
         return out
+
+    def seam_stats(self):
+        """The device max-flow's counts of the last find_seams: (pairs with a graph, push
+        launches, relabel launches, global relabels, microseconds of the max-flows)."""
+        st = np.zeros(5, np.int64)
+        check(self._lib.mcs_plan_seam_stats(self._h, st.ctypes.data_as(ctypes.c_void_p)))
+        return tuple(int(v) for v in st)
 
     def stitch_device(self, cam_ptrs, cam_frame_strides, out_ptr: int, out_pitch: int,
                       out_frame_stride: int, n_frames: int, stream: int = 0):
@@ -846,6 +858,22 @@ def seam_graphcut_host(labels, cover, samples):
                                    cov.ctypes.data_as(ctypes.c_void_p),
                                    smp.ctypes.data_as(ctypes.c_void_p), C))
     return lab
+
+
+def seam_graphcut_device(labels, cover, samples, device: int = 0, with_stats: bool = False):
+    """mcs_seam_graphcut_device: the cut of seam_graphcut_host by push-relabel on the GPU
+    (same arrays); with_stats: also (pairs, push launches, relabel launches, global relabels,
+    microseconds)."""
+    L = load()
+    lab = np.ascontiguousarray(labels, np.uint8).copy()
+    cov = np.ascontiguousarray(cover, np.uint16)
+    smp = np.ascontiguousarray(samples, np.uint8)
+    n, gh, gw = smp.shape[0], lab.shape[0], lab.shape[1]
+    C = 1 if smp.ndim == 3 else smp.shape[3]
+    st = np.zeros(5, np.int64)
+    check(L.mcs_seam_graphcut_device(n, gw, gh, lab.ctypes.data, cov.ctypes.data,
+                                     smp.ctypes.data, C, device, st.ctypes.data))
+    return (lab, tuple(int(v) for v in st)) if with_stats else lab
 
 
 def undistort_map_host(K, dist, w: int, h: int) -> np.ndarray:

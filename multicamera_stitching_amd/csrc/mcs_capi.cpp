@@ -75,6 +75,8 @@ struct mcs_plan {
     // graph-cut seam labels (mcs_plan_find_seams): host copy and device grid
     std::vector<uint8_t> seam_lab;
     int seam_w = 0, seam_h = 0, seam_k = 0;
+    // device max-flow: pairs, push / relabel launches, global relabels, microseconds
+    int64_t seam_stats[5] = {0, 0, 0, 0, 0};
     uint8_t *d_seam = nullptr;
     // single-camera remap plans (warp / undistort): blend modes refused; table plans' map
     bool single = false;
@@ -1559,7 +1561,7 @@ int mcs_plan_find_seams(mcs_plan *p, const uint8_t *const *cams, int method, int
     a.gw = gw;
     a.gh = gh;
     a.k = kk;
-    std::vector<uint8_t> lab(np), smp(np * C * n);
+    std::vector<uint8_t> lab(np), smp;   // (smp: host Dinic only)
     std::vector<uint16_t> cov(np);
     hipError_t e = A->hipMalloc((void **)&a.label, np);
     if (e == hipSuccess) e = A->hipMalloc((void **)&a.cov, np * sizeof(uint16_t));
@@ -1570,24 +1572,42 @@ int mcs_plan_find_seams(mcs_plan *p, const uint8_t *const *cams, int method, int
                          256, 1, &a, sizeof(a), p->stream);
         if (rc) e = hipErrorLaunchFailure;
     }
-    if (e == hipSuccess)
-        e = A->hipMemcpyAsync(lab.data(), a.label, np, hipMemcpyDeviceToHost, p->stream);
+    // the pairwise cuts: push-relabel on the device (default), or the host Dinic
+    // (MCS_SEAM_FLOW=host; the checker of the device path)
+    static const bool host_flow =
+        getenv("MCS_SEAM_FLOW") && !strcmp(getenv("MCS_SEAM_FLOW"), "host");
     if (e == hipSuccess)
         e = A->hipMemcpyAsync(cov.data(), a.cov, np * 2, hipMemcpyDeviceToHost, p->stream);
-    if (e == hipSuccess)
-        e = A->hipMemcpyAsync(smp.data(), a.samples, np * C * n, hipMemcpyDeviceToHost,
-                              p->stream);
+    if (host_flow) {
+        if (e == hipSuccess)
+            e = A->hipMemcpyAsync(lab.data(), a.label, np, hipMemcpyDeviceToHost, p->stream);
+        smp.resize(np * C * n);
+        if (e == hipSuccess)
+            e = A->hipMemcpyAsync(smp.data(), a.samples, np * C * n, hipMemcpyDeviceToHost,
+                                  p->stream);
+    }
     if (e == hipSuccess) e = A->hipStreamSynchronize(p->stream);
-    for (void *q : {(void *)a.label, (void *)a.cov, (void *)a.samples})
+    if (e == hipSuccess && rc == MCS_OK) {
+        if (host_flow) {
+            rc = mcs::seam_graphcut(n, gw, gh, lab.data(), cov.data(), smp.data(), C);
+            if (rc == MCS_OK)
+                e = A->hipMemcpyAsync(a.label, lab.data(), np, hipMemcpyHostToDevice, p->stream);
+        } else {
+            rc = mcs::seam_graphcut_device(p->device, p->stream, n, gw, gh, a.label, a.cov,
+                                           a.samples, C, cov.data(), p->seam_stats);
+            if (rc == MCS_OK)
+                e = A->hipMemcpyAsync(lab.data(), a.label, np, hipMemcpyDeviceToHost, p->stream);
+        }
+        if (e == hipSuccess) e = A->hipStreamSynchronize(p->stream);
+    }
+    for (void *q : {(void *)a.cov, (void *)a.samples})
         if (q) (void)A->hipFree(q);
-    if (rc) return rc;
-    if (e != hipSuccess)
-        return mcs::fail(MCS_E_HIP, "seam sampling: %s", A->hipGetErrorString(e));
-    rc = mcs::seam_graphcut(n, gw, gh, lab.data(), cov.data(), smp.data(), C);
-    if (rc) return rc;
-    HIP_TRY(A->hipMalloc((void **)&p->d_seam, np));
-    HIP_TRY(A->hipMemcpyAsync(p->d_seam, lab.data(), np, hipMemcpyHostToDevice, p->stream));
-    HIP_TRY(A->hipStreamSynchronize(p->stream));
+    if (rc || e != hipSuccess) {
+        if (a.label) (void)A->hipFree(a.label);
+        if (rc) return rc;
+        return mcs::fail(MCS_E_HIP, "seam finding: %s", A->hipGetErrorString(e));
+    }
+    p->d_seam = a.label;   // the device labels (the seam grid the stitch kernels read)
     p->seam_lab.swap(lab);
     p->seam_w = gw;
     p->seam_h = gh;
@@ -1608,6 +1628,52 @@ int mcs_seam_graphcut_host(int n_cams, int gw, int gh, uint8_t *labels, const ui
         return mcs::fail(MCS_E_INVALID, "n_cams %d, grid %dx%d, channels %d", n_cams, gw, gh,
                          channels);
     return mcs::seam_graphcut(n_cams, gw, gh, labels, cover, samples, channels);
+}
+
+int mcs_seam_graphcut_device(int n_cams, int gw, int gh, uint8_t *labels, const uint16_t *cover,
+                             const uint8_t *samples, int channels, int device, int64_t *stats)
+{
+    mcs::clear_error();
+    if (!labels || !cover || !samples) return mcs::fail(MCS_E_INVALID, "NULL input");
+    if (n_cams < 1 || n_cams > 16 || gw < 1 || gh < 1 || channels < 1 || channels > 4 ||
+        (int64_t)gw * gh > (int64_t)1 << 28)
+        return mcs::fail(MCS_E_INVALID, "n_cams %d, grid %dx%d, channels %d", n_cams, gw, gh,
+                         channels);
+    const Api *A = mcs::rt::api();
+    if (!A) return MCS_E_HIP;
+    DeviceGuard g(A, device);
+    if (g.err != hipSuccess)
+        return mcs::fail(MCS_E_HIP, "hipSetDevice(%d): %s", device, A->hipGetErrorString(g.err));
+    const size_t np = (size_t)gw * gh, sb = np * n_cams * channels;
+    uint8_t *buf = nullptr;
+    hipStream_t s = nullptr;
+    HIP_TRY(A->hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    hipError_t e = A->hipMalloc((void **)&buf, np * 3 + sb + 16);
+    uint8_t *d_lab = buf, *d_smp = buf + np * 3 + 16;
+    uint16_t *d_cov = reinterpret_cast<uint16_t *>(buf + ((np + 7) & ~(size_t)7));
+    if (e == hipSuccess) e = A->hipMemcpyAsync(d_lab, labels, np, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = A->hipMemcpyAsync(d_cov, cover, np * 2, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = A->hipMemcpyAsync(d_smp, samples, sb, hipMemcpyHostToDevice, s);
+    int rc = MCS_OK;
+    if (e == hipSuccess)
+        rc = mcs::seam_graphcut_device(device, s, n_cams, gw, gh, d_lab, d_cov, d_smp, channels,
+                                       cover, stats);
+    if (e == hipSuccess && rc == MCS_OK)
+        e = A->hipMemcpyAsync(labels, d_lab, np, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = A->hipStreamSynchronize(s);
+    (void)A->hipStreamSynchronize(s);
+    if (buf) (void)A->hipFree(buf);
+    (void)A->hipStreamDestroy(s);
+    if (rc) return rc;
+    if (e != hipSuccess) return mcs::fail(MCS_E_HIP, "seam graph cut: %s", A->hipGetErrorString(e));
+    return MCS_OK;
+}
+
+int mcs_plan_seam_stats(const mcs_plan *p, int64_t *stats)
+{
+    if (!p || !stats) return mcs::fail(MCS_E_INVALID, "NULL plan/stats");
+    for (int j = 0; j < 5; j++) stats[j] = p->seam_stats[j];
+    return MCS_OK;
 }
 
 int mcs_plan_seam_labels(const mcs_plan *p, uint8_t *out, int *w, int *h)

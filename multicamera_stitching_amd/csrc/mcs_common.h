@@ -41,6 +41,13 @@ int module_function(const rt::Api *A, int device, Module m, const char *name, hi
 // + 10 Levenberg-Marquardt iterations; H (9 doubles) holds the RANSAC model on entry.
 void homography_refine(const float *src_xy, const float *dst_xy, int n, const uint8_t *mask,
                        double *H);
+// The same cut on the device (push-relabel, mcs_features.hip mcs_seam_flow_*): labels / cov /
+// samples already in device memory (d_lab updated in place, on stream s, synchronised); cov is
+// the host copy of d_cov (the pairs' boxes).  stats (may be NULL): [0] pairs with a graph, [1]
+// push launches, [2] relabel launches, [3] global relabels, [4] microseconds.
+int seam_graphcut_device(int device, hipStream_t s, int n_cams, int gw, int gh, uint8_t *d_lab,
+                         const uint16_t *d_cov, const uint8_t *d_smp, int cn, const uint16_t *cov,
+                         int64_t *stats);
 // Orders the calling thread's feature-workspace stream on `device` (the stream its ORB / match /
 // RANSAC calls run on, mcs_features.cpp) after `event`: a GPU-side wait, no host round trip.
 int features_stream_wait(int device, void *event);

@@ -23,6 +23,9 @@ struct FeatureKernels {
     hipFunction_t l2_prep = nullptr, l2_i8 = nullptr, l2_f32 = nullptr, l2_finalize = nullptr;
     hipFunction_t rig_knn2 = nullptr, rig_match = nullptr, rig_ransac = nullptr,
                   rig_best = nullptr;
+    hipFunction_t seam_init = nullptr, seam_hinit = nullptr, seam_relabel = nullptr,
+                  seam_push = nullptr, seam_active = nullptr, seam_label = nullptr,
+                  seam_relabel_lds = nullptr;
 };
 int feature_kernels(const rt::Api *A, int device, const FeatureKernels **out);
 // hipModuleLaunchKernel with the argument block passed by value (grid gx x gy x gz).

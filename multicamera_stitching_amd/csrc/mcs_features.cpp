@@ -122,7 +122,13 @@ int mcs::feat::feature_kernels(const Api *A, int device, const FeatureKernels **
                    {"mcs_l2_prep", &k.l2_prep},       {"mcs_l2_knn2_i8", &k.l2_i8},
                    {"mcs_l2_knn2_f32", &k.l2_f32},    {"mcs_l2_knn2_finalize", &k.l2_finalize},
                    {"mcs_rig_knn2", &k.rig_knn2},     {"mcs_rig_match", &k.rig_match},
-                   {"mcs_rig_ransac", &k.rig_ransac}, {"mcs_rig_best", &k.rig_best}};
+                   {"mcs_rig_ransac", &k.rig_ransac}, {"mcs_rig_best", &k.rig_best},
+                   {"mcs_seam_flow_init", &k.seam_init}, {"mcs_seam_flow_hinit", &k.seam_hinit},
+                   {"mcs_seam_flow_relabel", &k.seam_relabel},
+                   {"mcs_seam_flow_push", &k.seam_push},
+                   {"mcs_seam_flow_active", &k.seam_active},
+                   {"mcs_seam_flow_label", &k.seam_label},
+                   {"mcs_seam_flow_relabel_lds", &k.seam_relabel_lds}};
         for (const auto &o : orb)
             if (rc == MCS_OK) rc = mcs::module_function(A, device, mcs::kModFeatures, o.name, o.f);
         if (rc) return rc;

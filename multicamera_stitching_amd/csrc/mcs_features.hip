@@ -885,3 +885,256 @@ extern "C" __global__ __launch_bounds__(1024) void mcs_rig_best(const mcs::KRigA
         mask[i] = rs_inlier(h, q[0], q[1], q[2], q[3], a.t2) ? 1 : 0;
     }
 }
+
+// ---- Graph-cut seams: push-relabel on one camera pair's overlap graph (KSeamFlowArgs) ----------
+// grid (ceil(bw / 16), ceil(bh / 16)), block 256: one thread per grid point of the pair's box.
+namespace mcs {
+
+__device__ __forceinline__ bool seam_box_point(const KSeamFlowArgs &a, int &X, int &Y, int64_t &q)
+{
+    X = a.x0 + (int)blockIdx.x * kSeamTile + (int)(threadIdx.x % kSeamTile);
+    Y = a.y0 + (int)blockIdx.y * kSeamTile + (int)(threadIdx.x / kSeamTile);
+    q = (int64_t)Y * a.gw + X;
+    return X < a.x0 + a.bw && Y < a.y0 + a.bh;
+}
+
+__device__ __forceinline__ bool seam_in(const KSeamFlowArgs &a, int64_t q)
+{
+    const uint32_t c = a.cov[q], l = a.lab[q];
+    return ((c >> a.a) & 1u) && ((c >> a.b) & 1u) && (l == (uint32_t)a.a || l == (uint32_t)a.b);
+}
+
+__device__ __forceinline__ int32_t seam_cost(const KSeamFlowArgs &a, int64_t q)
+{
+    const uint8_t *pa = a.smp + ((int64_t)a.a * a.np + q) * a.cn;
+    const uint8_t *pb = a.smp + ((int64_t)a.b * a.np + q) * a.cn;
+    int32_t s = 0;
+    for (int k = 0; k < a.cn; k++) s += abs((int)pa[k] - (int)pb[k]);
+    return s;
+}
+
+// neighbour d of (X, Y) inside the grid, -1 outside
+__device__ __forceinline__ int64_t seam_nb(const KSeamFlowArgs &a, int X, int Y, int64_t q, int d)
+{
+    switch (d) {
+    case 0: return X + 1 < a.gw ? q + 1 : -1;
+    case 1: return X > 0 ? q - 1 : -1;
+    case 2: return Y + 1 < a.gh ? q + a.gw : -1;
+    default: return Y > 0 ? q - a.gw : -1;
+    }
+}
+
+template <class T>
+__device__ __forceinline__ T seam_ld(const T *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+}  // namespace mcs
+
+// The pair's graph: node mask, arc capacities e(q) + e(r) + 1 (e = sum over channels of
+// |I_a - I_b|), terminals from the neighbours outside the graph (next to a's region: the
+// original source arc -> here an arc to the sink; next to b's region: the original sink arc ->
+// here the source's arc, saturated at once: excess kSeamBig).
+extern "C" __global__ __launch_bounds__(256) void mcs_seam_flow_init(const mcs::KSeamFlowArgs a)
+{
+    using namespace mcs;
+    int X, Y;
+    int64_t q;
+    if (!seam_box_point(a, X, Y, q)) return;
+    const bool in = seam_in(a, q);
+    a.in[q] = in ? 1 : 0;
+    a.h[q] = kSeamHInf;
+    long long sk = 0, e0 = 0;
+    const int32_t eq = in ? seam_cost(a, q) : 0;
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+        const int64_t r = seam_nb(a, X, Y, q, d);
+        int32_t c = 0;
+        if (in && r >= 0) {
+            if (seam_in(a, r)) {
+                c = eq + seam_cost(a, r) + 1;
+            } else {
+                if (a.lab[r] == (uint8_t)a.a) sk = kSeamBig;
+                if (a.lab[r] == (uint8_t)a.b) e0 = kSeamBig;
+            }
+        }
+        a.cap[d * a.np + q] = c;
+    }
+    a.snk[q] = sk;
+    a.ex[q] = e0;
+}
+
+// Global relabel, first step: height 1 next to the sink, kSeamHInf elsewhere.
+extern "C" __global__ __launch_bounds__(256) void mcs_seam_flow_hinit(const mcs::KSeamFlowArgs a)
+{
+    using namespace mcs;
+    int X, Y;
+    int64_t q;
+    if (!seam_box_point(a, X, Y, q)) return;
+    a.h[q] = a.in[q] && a.snk[q] > 0 ? 1 : kSeamHInf;
+}
+
+// Global relabel: `iters` rounds of h(u) = 1 + min h(v) over residual arcs u -> v (atomicMin:
+// heights only fall), flag[0] set on any change.  A launch without a change is the fixpoint:
+// the exact residual distances to the sink.
+extern "C" __global__ __launch_bounds__(256) void mcs_seam_flow_relabel(const mcs::KSeamFlowArgs a)
+{
+    using namespace mcs;
+    int X, Y;
+    int64_t q;
+    const bool live = seam_box_point(a, X, Y, q) && a.in[q];
+    bool changed = false;
+    for (int it = 0; it < a.iters; it++) {
+        if (live) {
+            int32_t hm = kSeamHInf;
+#pragma unroll
+            for (int d = 0; d < 4; d++) {
+                if (seam_ld(&a.cap[d * a.np + q]) <= 0) continue;
+                const int64_t r = seam_nb(a, X, Y, q, d);
+                hm = min(hm, seam_ld(&a.h[r]));
+            }
+            if (hm < kSeamHInf && hm + 1 < seam_ld(&a.h[q])) {
+                atomicMin(&a.h[q], hm + 1);
+                changed = true;
+            }
+        }
+        __syncthreads();
+    }
+    if (changed) atomicOr(&a.flag[0], 1);
+}
+
+// Global relabel, tiled: the block's 16 x 16 heights and their one-point ring staged in LDS,
+// `iters` relaxation rounds there (LDS latency per round instead of an L2 round trip; the ring
+// is the value other blocks had at the launch's start), then every lowered height written back
+// with atomicMin and flag[0] set.  Launched until a launch changes nothing: the same fixpoint
+// (exact residual distances to the sink) as mcs_seam_flow_relabel.
+extern "C" __global__ __launch_bounds__(256) void mcs_seam_flow_relabel_lds(
+    const mcs::KSeamFlowArgs a)
+{
+    using namespace mcs;
+    constexpr int T = kSeamTile, R = kSeamTile + 2;
+    __shared__ int32_t hl[R * R];
+    __shared__ uint8_t arc[T * T];   // bit d: residual arc toward neighbour d (bit 4: the sink)
+    int X, Y;
+    int64_t q;
+    const bool live = seam_box_point(a, X, Y, q) && a.in[q];
+    const int tx = (int)(threadIdx.x % T), ty = (int)(threadIdx.x / T);
+    // stage the tile and its ring (points outside the box or the graph: kSeamHInf)
+    for (int i = threadIdx.x; i < R * R; i += 256) {
+        const int lx = i % R - 1, ly = i / R - 1;
+        const int gx = a.x0 + (int)blockIdx.x * T + lx, gy = a.y0 + (int)blockIdx.y * T + ly;
+        int32_t v = kSeamHInf;
+        if (gx >= 0 && gy >= 0 && gx < a.gw && gy < a.gh) {
+            const int64_t r = (int64_t)gy * a.gw + gx;
+            v = seam_ld(&a.h[r]);
+        }
+        hl[i] = v;
+    }
+    uint32_t m = 0;
+    if (live) {
+#pragma unroll
+        for (int d = 0; d < 4; d++) m |= seam_ld(&a.cap[d * a.np + q]) > 0 ? 1u << d : 0u;
+        m |= a.snk[q] > 0 ? 16u : 0u;
+    }
+    arc[threadIdx.x] = (uint8_t)m;
+    __syncthreads();
+    const int c = (ty + 1) * R + tx + 1;
+    const int32_t h0 = hl[c];
+    for (int it = 0; it < a.iters; it++) {
+        if (live) {
+            int32_t hm = (m & 16u) ? 0 : kSeamHInf;
+            if (m & 1u) hm = min(hm, hl[c + 1]);
+            if (m & 2u) hm = min(hm, hl[c - 1]);
+            if (m & 4u) hm = min(hm, hl[c + R]);
+            if (m & 8u) hm = min(hm, hl[c - R]);
+            if (hm < kSeamHInf && hm + 1 < hl[c]) hl[c] = hm + 1;
+        }
+        __syncthreads();
+    }
+    if (live && hl[c] < h0) {
+        atomicMin(&a.h[q], hl[c]);
+        atomicOr(&a.flag[0], 1);
+    }
+}
+
+// Push-relabel rounds (Hong's lock-free rule).  A node's own height changes only here (by its
+// own thread) and in the global relabel, so it stays in a register for the launch; each round
+// issues all of its loads at once (excess, sink and arc residuals, the four neighbours'
+// heights): one L2 round trip per round.
+extern "C" __global__ __launch_bounds__(256) void mcs_seam_flow_push(const mcs::KSeamFlowArgs a)
+{
+    using namespace mcs;
+    int X, Y;
+    int64_t q;
+    const bool live = seam_box_point(a, X, Y, q) && a.in[q];
+    int64_t nb[4];
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+        const int64_t r = live ? seam_nb(a, X, Y, q, d) : -1;
+        nb[d] = r >= 0 ? r : q;
+    }
+    int32_t hu = live ? a.h[q] : kSeamHInf;
+    for (int it = 0; it < a.iters; it++) {
+        if (live && hu < kSeamHInf) {
+            const long long e = seam_ld(&a.ex[q]);
+            const long long sk = seam_ld(&a.snk[q]);
+            int32_t c[4], hv[4];
+#pragma unroll
+            for (int d = 0; d < 4; d++) {
+                c[d] = seam_ld(&a.cap[d * a.np + q]);
+                hv[d] = seam_ld(&a.h[nb[d]]);
+            }
+            if (e > 0) {
+                // the lowest residual target: the sink (height 0) or a neighbour
+                int best = sk > 0 ? 4 : -1;
+                int32_t hm = sk > 0 ? 0 : kSeamHInf;
+#pragma unroll
+                for (int d = 0; d < 4; d++)
+                    if (c[d] > 0 && hv[d] < hm) hm = hv[d], best = d;
+                if (best < 0 || hm >= a.hmax - 1) {
+                    hu = kSeamHInf;                        // no way to the sink
+                    atomicExch(&a.h[q], hu);
+                } else if (hu > hm) {
+                    if (best == 4) {
+                        const long long dl = min(e, sk);
+                        atomicAdd((unsigned long long *)&a.snk[q], (unsigned long long)(-dl));
+                        atomicAdd((unsigned long long *)&a.ex[q], (unsigned long long)(-dl));
+                    } else {
+                        const long long dl = min(e, (long long)c[best]);
+                        const int64_t rb = nb[best];
+                        atomicSub(&a.cap[best * a.np + q], (int32_t)dl);
+                        atomicAdd(&a.cap[(best ^ 1) * a.np + rb], (int32_t)dl);
+                        atomicAdd((unsigned long long *)&a.ex[rb], (unsigned long long)dl);
+                        atomicAdd((unsigned long long *)&a.ex[q], (unsigned long long)(-dl));
+                    }
+                } else {
+                    hu = hm + 1;                           // relabel
+                    atomicExch(&a.h[q], hu);
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// Nodes with excess that can still reach the sink (after a global relabel) -> flag[1].
+extern "C" __global__ __launch_bounds__(256) void mcs_seam_flow_active(const mcs::KSeamFlowArgs a)
+{
+    using namespace mcs;
+    int X, Y;
+    int64_t q;
+    const bool act = seam_box_point(a, X, Y, q) && a.in[q] && a.ex[q] > 0 && a.h[q] < kSeamHInf;
+    const unsigned long long b = __ballot(act);
+    if ((threadIdx.x & 63) == 0 && b) atomicAdd(&a.flag[1], (int)__popcll(b));
+}
+
+// The cut: nodes that reach the sink (the a side) keep camera a, the others take b.
+extern "C" __global__ __launch_bounds__(256) void mcs_seam_flow_label(const mcs::KSeamFlowArgs a)
+{
+    using namespace mcs;
+    int X, Y;
+    int64_t q;
+    if (!seam_box_point(a, X, Y, q) || !a.in[q]) return;
+    a.lab[q] = (uint8_t)(a.h[q] < kSeamHInf ? a.a : a.b);
+}

@@ -164,4 +164,33 @@ struct KRigArgs {
     uint32_t seed;
 };
 
+// Graph-cut seams on the device (mcs_seam.cpp; spec oracle/orc_seam.c): the
+// maximum flow of one camera pair's 4-connected overlap graph on the 2^k seam grid by
+// push-relabel, run on the REVERSED graph (source = the b-side terminal, sink = the a side), so
+// that the nodes which can still reach its sink in the residual graph of a maximum preflow are
+// exactly the source side of the original graph's minimal minimum cut (the host Dinic's
+// residual-reachable set, unique for every maximum flow).  Per grid point q of the pair's box:
+// in[q] (node of this pair's graph), cap[d * np + q] the residual capacity toward neighbour d
+// (0 +x, 1 -x, 2 +y, 3 -y), snk[q] toward the sink, ex[q] the excess, h[q] the height
+// (kSeamHInf: cannot reach the sink).  Heights come from global relabels (Bellman-Ford
+// relaxation from the sink to a fixpoint); pushes follow Hong's lock-free rule (push to the
+// lowest residual neighbour when higher than it, else relabel), all updates atomic.
+constexpr int kSeamTile = 16;                 // 16 x 16 grid points per block
+constexpr int32_t kSeamHInf = 1 << 30;
+constexpr long long kSeamBig = 1LL << 40;     // terminal capacity (the host Dinic's kBig)
+struct KSeamFlowArgs {
+    uint8_t *lab;             // gw x gh labels (camera index; 255 = none)
+    const uint16_t *cov;      // covering cameras per point
+    const uint8_t *smp;       // n_cams x np x cn samples
+    uint8_t *in;
+    int32_t *cap;             // 4 x np
+    long long *snk, *ex;      // np
+    int32_t *h;               // np
+    int32_t *flag;            // [0] a height changed / [1] active nodes
+    long long np;
+    int gw, gh, cn, a, b;
+    int x0, y0, bw, bh;       // the pair's box on the grid
+    int iters, hmax;          // inner rounds per launch; heights >= hmax cannot reach the sink
+};
+
 }  // namespace mcs

@@ -1,15 +1,21 @@
 // mcs_seam.cpp -- graph-cut seam labels (include/mcs.h
-// mcs_plan_find_seams).  Calibration-time host work, once per plan (as OpenCV's seam finders run
-// once on reduced images): the per-point inputs come from the plan's device kernels
-// (mcs_seam_sample_*), the pairwise minimum cuts run here with Dinic's algorithm on the
-// 4-connected overlap graph.  Specification in oracle/orc_seam.c (restated there with a
-// different max-flow algorithm; both return the source side of the minimal minimum cut, which
-// every maximum flow shares).
+// mcs_plan_find_seams).  Calibration time, once per plan (as OpenCV's seam finders run once on
+// reduced images): the per-point inputs come from the plan's device kernels
+// (mcs_seam_sample_*), then one minimum cut per camera pair on its 4-connected overlap graph --
+// on the device by push-relabel (seam_graphcut_device, kernels mcs_seam_flow_* in
+// mcs_features.hip), or here on the host with Dinic's algorithm (seam_graphcut: the C-ABI's
+// mcs_seam_graphcut_host, and the cross-check of the device path).  Specification in
+// oracle/orc_seam.c (restated there with a third max-flow algorithm); all return the source side
+// of the minimal minimum cut, which every maximum flow shares.
 #include <algorithm>
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
 #include <cstdint>
 #include <vector>
 
 #include "mcs_common.h"
+#include "mcs_feat_int.h"
 
 namespace {
 
@@ -150,6 +156,142 @@ int seam_graphcut(int n_cams, int gw, int gh, uint8_t *lab, const uint16_t *cov,
             for (int64_t q = 0; q < np; q++)
                 if (id[q] >= 0) lab[q] = (uint8_t)(reach[id[q]] ? a : b);
         }
+    return MCS_OK;
+}
+
+}  // namespace mcs
+
+namespace mcs {
+
+int seam_graphcut_device(int device, hipStream_t s, int n_cams, int gw, int gh, uint8_t *d_lab,
+                         const uint16_t *d_cov, const uint8_t *d_smp, int cn, const uint16_t *cov,
+                         int64_t *stats)
+{
+    using rt::Api;
+    const Api *A = rt::api();
+    if (!A) return MCS_E_HIP;
+    const feat::FeatureKernels *k = nullptr;
+    int rc = feat::feature_kernels(A, device, &k);
+    if (rc) return rc;
+    const int64_t np = (int64_t)gw * gh;
+    // each pair's box: the points both cameras cover
+    const int NP = n_cams * n_cams;
+    std::vector<int> bx0(NP, gw), by0(NP, gh), bx1(NP, -1), by1(NP, -1);
+    for (int64_t q = 0; q < np; q++) {
+        const uint32_t c = cov[q];
+        if ((c & (c - 1)) == 0) continue;
+        const int X = (int)(q % gw), Y = (int)(q / gw);
+        for (int a = 0; a < n_cams; a++) {
+            if (!((c >> a) & 1)) continue;
+            for (int b = a + 1; b < n_cams; b++) {
+                if (!((c >> b) & 1)) continue;
+                const int i = a * n_cams + b;
+                bx0[i] = std::min(bx0[i], X), bx1[i] = std::max(bx1[i], X);
+                by0[i] = std::min(by0[i], Y), by1[i] = std::max(by1[i], Y);
+            }
+        }
+    }
+    int64_t st[5] = {0, 0, 0, 0, 0};
+    const auto t0 = std::chrono::steady_clock::now();
+    uint8_t *buf = nullptr;
+    int32_t *hflag = nullptr;
+    const size_t bytes = (size_t)np * (1 + 4 * 4 + 8 + 8 + 4) + 64;
+    HIP_TRY(A->hipMalloc((void **)&buf, bytes));
+    hipError_t e = A->hipHostMalloc((void **)&hflag, 2 * sizeof(int32_t), 0);
+    mcs::KSeamFlowArgs fa;
+    std::memset(&fa, 0, sizeof(fa));
+    fa.lab = d_lab;
+    fa.cov = d_cov;
+    fa.smp = d_smp;
+    fa.ex = reinterpret_cast<long long *>(buf);
+    fa.snk = fa.ex + np;
+    fa.cap = reinterpret_cast<int32_t *>(fa.snk + np);
+    fa.h = fa.cap + 4 * np;
+    fa.flag = fa.h + np;
+    fa.in = reinterpret_cast<uint8_t *>(fa.flag + 16);
+    fa.np = np;
+    fa.gw = gw;
+    fa.gh = gh;
+    fa.cn = cn;
+    // push-relabel rounds between global relabels / relaxation rounds per relabel launch;
+    // a round bound far beyond any grid's need (a run-away loop fails loudly instead of hanging)
+    // (MCS_SEAM_PUSH_LAUNCHES / _PUSH_ITERS / _RELABEL_ITERS: tuning experiments)
+    auto knob = [](const char *name, int dflt) {
+        const char *v = getenv(name);
+        return v && atoi(v) > 0 ? atoi(v) : dflt;
+    };
+    static const int kPushLaunches = knob("MCS_SEAM_PUSH_LAUNCHES", 8);
+    static const int kPushIters = knob("MCS_SEAM_PUSH_ITERS", 16);
+    static const int kRelabelIters = knob("MCS_SEAM_RELABEL_ITERS", 64);
+    // global relabels in LDS tiles (default) or with L2 round trips (MCS_SEAM_RELABEL_LDS=0)
+    static const bool relabel_lds =
+        !getenv("MCS_SEAM_RELABEL_LDS") || strcmp(getenv("MCS_SEAM_RELABEL_LDS"), "0");
+    static const int kRelabelLdsIters = knob("MCS_SEAM_RELABEL_LDS_ITERS", 32);
+    static const int kRelabelBatch = knob("MCS_SEAM_RELABEL_BATCH", 8);
+    constexpr int64_t kMaxRounds = 1 << 20;
+    auto launch = [&](hipFunction_t f, unsigned gx, unsigned gy) {
+        return feat::launch(A, f, gx, gy, 256, &fa, sizeof(fa), s);
+    };
+    auto read_flags = [&]() -> hipError_t {
+        hipError_t r = A->hipMemcpyAsync(hflag, fa.flag, 2 * sizeof(int32_t),
+                                         hipMemcpyDeviceToHost, s);
+        return r == hipSuccess ? A->hipStreamSynchronize(s) : r;
+    };
+    for (int a = 0; a < n_cams && e == hipSuccess && rc == MCS_OK; a++)
+        for (int b = a + 1; b < n_cams && e == hipSuccess && rc == MCS_OK; b++) {
+            const int i = a * n_cams + b;
+            if (bx1[i] < 0) continue;
+            fa.a = a;
+            fa.b = b;
+            fa.x0 = bx0[i], fa.y0 = by0[i];
+            fa.bw = bx1[i] - bx0[i] + 1, fa.bh = by1[i] - by0[i] + 1;
+            fa.hmax = (int)std::min<int64_t>((int64_t)fa.bw * fa.bh + 2, kSeamHInf - 1);
+            const unsigned gx = (unsigned)((fa.bw + kSeamTile - 1) / kSeamTile);
+            const unsigned gy = (unsigned)((fa.bh + kSeamTile - 1) / kSeamTile);
+            st[0]++;
+            rc = launch(k->seam_init, gx, gy);
+            for (int64_t round = 0; rc == MCS_OK && e == hipSuccess; round++) {
+                if (round >= kMaxRounds) {
+                    rc = mcs::fail(MCS_E_HIP, "seam max-flow: no convergence after %lld rounds",
+                                   (long long)round);
+                    break;
+                }
+                // global relabel: exact residual distances to the sink
+                st[3]++;
+                rc = launch(k->seam_hinit, gx, gy);
+                // batches of relabel launches, the flag reset before each: the flag read after a
+                // batch is its last launch's, zero only at the fixpoint
+                fa.iters = relabel_lds ? kRelabelLdsIters : kRelabelIters;
+                for (;;) {
+                    for (int j = 0; j < kRelabelBatch && e == hipSuccess && rc == MCS_OK; j++) {
+                        e = A->hipMemsetAsync(fa.flag, 0, 2 * sizeof(int32_t), s);
+                        if (e == hipSuccess)
+                            rc = launch(relabel_lds ? k->seam_relabel_lds : k->seam_relabel, gx,
+                                        gy);
+                        st[2]++;
+                    }
+                    if (e == hipSuccess && rc == MCS_OK) e = read_flags();
+                    if (e != hipSuccess || rc != MCS_OK || hflag[0] == 0) break;
+                }
+                if (e == hipSuccess && rc == MCS_OK) rc = launch(k->seam_active, gx, gy);
+                if (e == hipSuccess && rc == MCS_OK) e = read_flags();
+                if (e != hipSuccess || rc != MCS_OK || hflag[1] == 0) break;   // maximum preflow
+                fa.iters = kPushIters;
+                for (int j = 0; j < kPushLaunches && rc == MCS_OK; j++, st[1]++)
+                    rc = launch(k->seam_push, gx, gy);
+            }
+            if (rc == MCS_OK && e == hipSuccess) rc = launch(k->seam_label, gx, gy);
+        }
+    if (e == hipSuccess && rc == MCS_OK) e = A->hipStreamSynchronize(s);
+    (void)A->hipStreamSynchronize(s);
+    if (hflag) (void)A->hipHostFree(hflag);
+    (void)A->hipFree(buf);
+    if (rc) return rc;
+    if (e != hipSuccess) return mcs::fail(MCS_E_HIP, "seam max-flow: %s", A->hipGetErrorString(e));
+    st[4] = std::chrono::duration_cast<std::chrono::microseconds>(
+                std::chrono::steady_clock::now() - t0).count();
+    if (stats)
+        for (int j = 0; j < 5; j++) stats[j] = st[j];
     return MCS_OK;
 }
 

@@ -76,3 +76,37 @@ def test_cylinder_c4_full_size_graphcut():
     want, lab = ref(frames, 2, 2)
     assert np.array_equal(plan.seam_labels(), lab)
     assert _diff(plan.stitch_host(frames).reshape(want.shape), want) == 0
+
+
+def _synthetic_seam_grid(gw, gh, n, seed, noise):
+    """A cylinder-like grid: n cameras, each covering its column band plus overlaps, owner = the
+    nearest band centre; samples = one world + per-camera noise (noise 0: flat costs)."""
+    rng = np.random.default_rng(seed)
+    cols = np.arange(gw)
+    per = gw / n
+    ov = max(2, int(per * 0.4))
+    cov = np.zeros((gh, gw), np.uint16)
+    dist = []
+    for i in range(n):
+        c = i * per + per / 2
+        d = (cols - c + gw / 2) % gw - gw / 2
+        cov[:, np.abs(d) <= per / 2 + ov] |= np.uint16(1 << i)
+        dist.append(np.abs(d))
+    lab = np.repeat(np.argmin(np.stack(dist), 0).astype(np.uint8)[None, :], gh, 0)
+    world = rng.integers(0, 256, (gh, gw, 3), dtype=np.int32)
+    smp = np.stack([np.clip(world + rng.integers(-noise, noise + 1, world.shape), 0, 255)
+                    .astype(np.uint8) for _ in range(n)])
+    return lab, cov, smp
+
+
+@pytest.mark.parametrize("gw,gh,n,seed,noise", [(96, 40, 4, 0, 30), (160, 64, 6, 1, 60),
+                                                 (64, 64, 3, 2, 0), (200, 90, 8, 3, 20)])
+def test_device_maxflow_equals_host_dinic(gw, gh, n, seed, noise):
+    """The device push-relabel cut (mcs_seam_graphcut_device) = the host Dinic's
+    (mcs_seam_graphcut_host): the minimal minimum cut is unique."""
+    from multicamera_stitching_amd import _capi
+    lab, cov, smp = _synthetic_seam_grid(gw, gh, n, seed, noise)
+    want = _capi.seam_graphcut_host(lab, cov, smp)
+    got, st = _capi.seam_graphcut_device(lab, cov, smp, with_stats=True)
+    assert st[0] > 0
+    assert np.array_equal(got, want), (int((got != want).sum()), st)
