@@ -66,6 +66,9 @@ def parse():
                     help="CPU rehearsal of the multi-rank orchestration (gloo, a stub step): "
                          "no GPU, no libmcs; tests/test_bench_dist.py")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-also", action="store_true",
+                    help="skip the companion lines (C4 cylinder, C3 estimate + stitch, matcher, "
+                         "C4 seams) that a 1-GPU run appends under 'also'")
     ap.add_argument("--no-paste-ref", action="store_true",
                     help="skip the paste-only reference launch (PMC passes: one plan's dispatches)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
@@ -350,11 +353,51 @@ def main():
             },
             "cpu_baseline": cpu,
         }
+        if world == 1 and not args.no_also and not cyl and args.blend == "multiband":
+            result["also"] = companion_lines()
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
     return result
+
+
+def _child_line(cmd, timeout, keep):
+    """Runs one companion benchmark as a child process (its own GPU context) and keeps `keep`
+    fields of its JSON line; an error string instead of failing the headline line."""
+    import subprocess
+    try:
+        r = subprocess.run([sys.executable] + cmd, cwd=ROOT, capture_output=True, text=True,
+                           timeout=timeout)
+        line = json.loads(r.stdout.strip().splitlines()[-1])
+        return {k: line.get(k) for k in keep if k in line}
+    except Exception as e:   # noqa: BLE001 -- recorded, the headline line stands
+        return {"error": f"{type(e).__name__}: {str(e)[:200]}"}
+
+
+def companion_lines():
+    """SURVEY.md 8 configs beside the headline C2 line, measured in the same driver run: C4 (8-cam
+    cylinder, multi-band, bench.py --rig cylinder), C3 (per-capture estimation + stitch through
+    the rig jobs, frames uploaded every capture, tools/estimate_bench.py), the Hamming matcher's
+    pairs/s (tools/match_bench.py) and the C4 graph-cut seams per plan (tools/seam_bench.py)."""
+    return {
+        "c4_cylinder_multiband": _child_line(
+            ["bench.py", "--rig", "cylinder", "--no-cpu-baseline", "--no-also"], 400,
+            ("metric", "value", "unit", "ms_per_step", "max_abs_diff", "config", "roofline",
+             "kernels")),
+        "c3_estimate_and_stitch": _child_line(
+            ["tools/estimate_bench.py", "--stitch", "--pipelined", "--overlap", "--depth", "4",
+             "--steps", "300", "--warmup", "20", "--no-cpu-baseline"], 300,
+            ("metric", "value", "unit", "ms_per_step", "stitched_mpix_per_s", "config",
+             "latency_ms_upload_to_homographies", "max_reproj_err_px_vs_truth",
+             "max_abs_diff_vs_cpu_render")),
+        "hamming_matcher": _child_line(["tools/match_bench.py"], 200,
+                                       ("metric", "unit", "sizes", "ops_per_pair",
+                                        "peak_lane_ops_per_s")),
+        "c4_seams": _child_line(["tools/seam_bench.py", "--no-check"], 200,
+                                ("metric", "ms_per_plan", "grid", "max_flow",
+                                 "stats_pairs_push_relabel_globalrelabels_us")),
+    }
 
 
 def gather_all(d_out, args, shard, torch, dev, reps: int = 3):
