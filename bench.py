@@ -379,7 +379,8 @@ def companion_lines():
     """SURVEY.md 8 configs beside the headline C2 line, measured in the same driver run: C4 (8-cam
     cylinder, multi-band, bench.py --rig cylinder), C3 (per-capture estimation + stitch through
     the rig jobs, frames uploaded every capture, tools/estimate_bench.py), the Hamming matcher's
-    pairs/s (tools/match_bench.py) and the C4 graph-cut seams per plan (tools/seam_bench.py)."""
+    pairs/s (tools/match_bench.py), the C4 graph-cut seams per plan (tools/seam_bench.py) and the
+    C5 4K stream (host frames in, host mosaics out, tools/stream_bench.py)."""
     return {
         "c4_cylinder_multiband": _child_line(
             ["bench.py", "--rig", "cylinder", "--no-cpu-baseline", "--no-also"], 400,
@@ -397,6 +398,9 @@ def companion_lines():
         "c4_seams": _child_line(["tools/seam_bench.py", "--no-check"], 200,
                                 ("metric", "ms_per_plan", "grid", "max_flow",
                                  "stats_pairs_push_relabel_globalrelabels_us")),
+        "c5_stream_4k": _child_line(["tools/stream_bench.py", "--sizes", "3840x2160",
+                                     "--frames", "200", "--summary"], 300,
+                                    ("metric", "unit", "lines")),
     }
 
 

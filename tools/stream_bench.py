@@ -112,9 +112,12 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=200)
     ap.add_argument("--sizes", default="1920x1080,3840x2160")
+    ap.add_argument("--summary", action="store_true",
+                    help="also print one closing JSON line holding every configuration's line")
     a = ap.parse_args()
     import torch
     torch.cuda.set_device(0)
+    lines = []
     for size in a.sizes.split(","):
         w, h = (int(v) for v in size.split("x"))
         in_b = 4 * w * h * 3
@@ -122,7 +125,12 @@ if __name__ == "__main__":
         link = link_probe(in_b, out_b)
         link.update(cams=f"4x{w}x{h}x3", host_memcpy_gbs=host_copy_gbs(in_b))
         print(json.dumps({"link_probe": link}), flush=True)
+        lines.append({"link_probe": link})
         for blend in (0, 2):
             for depth, graphs, zc in ((1, False, False), (3, True, False), (3, True, True)):
-                print(json.dumps(run(w, h, blend, depth, a.frames, graphs, zc, link)),
-                      flush=True)
+                r = run(w, h, blend, depth, a.frames, graphs, zc, link)
+                print(json.dumps(r), flush=True)
+                lines.append(r)
+    if a.summary:
+        print(json.dumps({"metric": "streamed rig captures/s (C5: host frames in, host mosaics "
+                                    "out, mcs_stream_*)", "unit": "fps", "lines": lines}))
