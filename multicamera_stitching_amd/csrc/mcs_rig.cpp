@@ -11,7 +11,9 @@
 // pairs (mcs_rig_* kernels, every count read on the device), then one copy back of the counts,
 // best models, inlier masks and matched positions; the host only runs findHomography's LM
 // refinement (mcs_refine.cpp) per pair.  The same kernels and arithmetic as the per-call entry
-// points, so the same homographies, bit for bit.
+// points, so the same homographies, bit for bit.  The chain is captured once as a hipGraph and
+// replayed while the job is fed the same frame pointers (one graph launch per capture; a new
+// frame set re-captures it; MCS_RIG_GRAPH=0: plain launches).
 //
 // Per-call path (a capture whose ORB ranking overflowed on the device -- more than kOrbSelMax
 // candidates on a level --, or MCS_RIG_PATH=calls): the C-ABI's own steps
@@ -110,6 +112,10 @@ struct RigDevice {
     mcs::KOrbSelArgs sa;
     mcs::KOrbDescArgs da;
     mcs::KRigArgs ra;
+    // the chain captured as a hipGraph for the frame pointers it was captured with (a job is
+    // usually fed the same frame set every time: one per capture slot in flight)
+    hipGraphExec_t exec = nullptr;
+    std::vector<const uint8_t *> graph_frames;
 };
 
 }  // namespace
@@ -373,33 +379,24 @@ void device_release(mcs_rig_job *j)
     if (!A) return;
     mcs::DeviceGuard dg(A, j->device);
     if (d.s) (void)A->hipStreamSynchronize(d.s);
+    if (d.exec) (void)A->hipGraphExecDestroy(d.exec);
     if (d.buf) (void)A->hipFree(d.buf);
     if (d.host) (void)A->hipHostFree(d.host);
     if (d.s) (void)A->hipStreamDestroy(d.s);
     d = RigDevice();
 }
 
-// The capture's launch chain and its one copy back (see the file comment).  Returns MCS_OK
-// with *overflow set when a camera's device ranking overflowed (nothing else is valid then).
-int device_capture(mcs_rig_job *j, bool *overflow)
+// The capture's launch chain on stream s (its one copy back included): issued directly or
+// recorded into the job's graph.
+int enqueue_chain(mcs_rig_job *j, const mcs::rt::Api *A, const mcs::feat::FeatureKernels *k,
+                  hipStream_t s)
 {
-    *overflow = false;
-    int rc = MCS_OK;
-    const mcs::rt::Api *A = api_for(j->device, &rc);
-    if (rc) return rc;
-    if (!j->dev.ready && (rc = device_setup(j)) != MCS_OK) return rc;
     RigDevice &d = j->dev;
-    const mcs::feat::FeatureKernels *k = nullptr;
-    mcs::DeviceGuard dg(A, j->device);
-    if (dg.err != hipSuccess)
-        return mcs::fail(MCS_E_HIP, "hipSetDevice(%d): %s", j->device, A->hipGetErrorString(dg.err));
-    if ((rc = mcs::feat::feature_kernels(A, j->device, &k)) != MCS_OK) return rc;
+    using mcs::feat::launch;
     const int C = j->n_cams, P = j->n_cams - 1, L = j->nlevels;
     const mcs::feat::OrbGeom &g = d.geo;
     const size_t pix = g.off[L];
-    hipStream_t s = d.s;
-    using mcs::feat::launch;
-    if (j->wait_event) HIP_TRY(A->hipStreamWaitEvent(s, (hipEvent_t)j->wait_event, 0));
+    int rc = MCS_OK;
     HIP_TRY(A->hipMemsetAsync(d.buf + d.o_cnt, 0, d.cnt_bytes, s));
     HIP_TRY(A->hipMemsetAsync(d.buf + d.o_keys, 0xff, d.keys_bytes, s));
     if (j->channels == 3) {
@@ -438,9 +435,60 @@ int device_capture(mcs_rig_job *j, bool *overflow)
         rc = launch(A, k->rig_ransac, (unsigned)j->iters, (unsigned)P, mcs::kRansacBlock, &d.ra,
                     sizeof(d.ra), s);
     if (rc == MCS_OK) rc = launch(A, k->rig_best, (unsigned)P, 1, 1024, &d.ra, sizeof(d.ra), s);
-    hipError_t e = hipSuccess;
     if (rc == MCS_OK)
-        e = A->hipMemcpyAsync(d.host, d.buf + d.o_blob, d.blob_bytes, hipMemcpyDeviceToHost, s);
+        HIP_TRY(A->hipMemcpyAsync(d.host, d.buf + d.o_blob, d.blob_bytes, hipMemcpyDeviceToHost,
+                                  s));
+    return rc;
+}
+
+// The capture's launch chain and its one copy back (see the file comment).  Returns MCS_OK
+// with *overflow set when a camera's device ranking overflowed (nothing else is valid then).
+int device_capture(mcs_rig_job *j, bool *overflow)
+{
+    *overflow = false;
+    int rc = MCS_OK;
+    const mcs::rt::Api *A = api_for(j->device, &rc);
+    if (rc) return rc;
+    if (!j->dev.ready && (rc = device_setup(j)) != MCS_OK) return rc;
+    RigDevice &d = j->dev;
+    const mcs::feat::FeatureKernels *k = nullptr;
+    mcs::DeviceGuard dg(A, j->device);
+    if (dg.err != hipSuccess)
+        return mcs::fail(MCS_E_HIP, "hipSetDevice(%d): %s", j->device, A->hipGetErrorString(dg.err));
+    if ((rc = mcs::feat::feature_kernels(A, j->device, &k)) != MCS_OK) return rc;
+    const int C = j->n_cams, P = j->n_cams - 1;
+    hipStream_t s = d.s;
+    if (j->wait_event) HIP_TRY(A->hipStreamWaitEvent(s, (hipEvent_t)j->wait_event, 0));
+    // MCS_RIG_GRAPH=0: plain launches every capture
+    static const bool graphs = !getenv("MCS_RIG_GRAPH") || strcmp(getenv("MCS_RIG_GRAPH"), "0");
+    hipError_t e = hipSuccess;
+    if (graphs && d.pyr_blocks > 0) {
+        if (!d.exec || d.graph_frames != j->frames) {
+            if (d.exec) (void)A->hipGraphExecDestroy(d.exec);
+            d.exec = nullptr;
+            hipGraph_t graph = nullptr;
+            HIP_TRY(A->hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+            rc = enqueue_chain(j, A, k, s);
+            const hipError_t ec = A->hipStreamEndCapture(s, &graph);
+            if (rc == MCS_OK && ec != hipSuccess)
+                rc = mcs::fail(MCS_E_HIP, "rig capture graph: %s", A->hipGetErrorString(ec));
+            if (rc == MCS_OK) {
+                const hipError_t ei =
+                    A->hipGraphInstantiate(&d.exec, graph, nullptr, nullptr, 0);
+                if (ei != hipSuccess) {
+                    d.exec = nullptr;
+                    rc = mcs::fail(MCS_E_HIP, "rig graph instantiate: %s",
+                                   A->hipGetErrorString(ei));
+                }
+            }
+            if (graph) (void)A->hipGraphDestroy(graph);
+            if (rc) return rc;
+            d.graph_frames = j->frames;
+        }
+        e = A->hipGraphLaunch(d.exec, s);
+    } else {
+        rc = enqueue_chain(j, A, k, s);
+    }
     const hipError_t e2 = A->hipStreamSynchronize(s);   // (drains the queued work on error too)
     if (rc) return rc;
     if (e != hipSuccess || e2 != hipSuccess)
