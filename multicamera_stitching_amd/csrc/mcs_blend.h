@@ -1160,7 +1160,7 @@ __device__ __forceinline__ int mb_band_of_block(const KMbBandArgs &a)
 }
 
 template <int CN, int FR, bool BR>
-__device__ __forceinline__ void mb_bands(const KMbBandArgs &a, int bl)
+__device__ __forceinline__ void mb_bands(const KMbBandArgs &a, int bi)
 {
     typedef __attribute__((address_space(1))) const uint8_t gu8;
     struct __attribute__((packed)) U2 {
@@ -1170,7 +1170,6 @@ __device__ __forceinline__ void mb_bands(const KMbBandArgs &a, int bl)
     typedef __attribute__((address_space(1))) uint2 g2u;
     const KParams &P = a.P;
     const int l = threadIdx.x;
-    const int bi = a.band0 + bl;
     const MbBand B = a.bands[bi];
     const int fl0 = blockIdx.y * FR;
     if (fl0 >= a.nf) return;
@@ -1440,7 +1439,7 @@ __device__ __forceinline__ void mb_blend_tile(const KMbArgs &a, const MbGeo &G, 
 {
     const KParams &P = a.P;
     const int tid = threadIdx.x, nt = blockDim.x;
-    const int32_t *tab = a.tab + (int64_t)blockIdx.x * mb_tab_words(a.slots);
+    const int32_t *tab = a.tab + (int64_t)(a.list0 + (int)blockIdx.x) * mb_tab_words(a.slots);
     const int32_t *t_m1 = tab, *t_m2 = tab + a.slots * kMbNRX * kMbNRY;
     const int32_t *t_d1 = t_m2 + a.slots * kMbN2X * kMbN2Y, *t_d2 = t_d1 + kMbNRX * kMbNRY;
     // (24-bit multiplies: full-rate v_mul_u32_u24 instead of quarter-rate v_mul_lo_u32)
@@ -1585,7 +1584,7 @@ __device__ __forceinline__ void mb_blend(const KMbArgs &a, MbBlLds<CN, S> &L)
     typedef __attribute__((address_space(1))) const uint2 cgu2;
     typedef __attribute__((address_space(1))) const int32_t cgi32;
     const KParams &P = a.P;
-    const int bt = blockIdx.x, fl = blockIdx.y, tid = threadIdx.x;
+    const int bt = a.list0 + (int)blockIdx.x, fl = blockIdx.y, tid = threadIdx.x;
     const uint32_t mask = (uint32_t)a.list[2 + 2 * bt];
     const int ns = __popc(mask), f = a.f0 + fl;
     const MbGeo G = mb_geo(P, a.list[1 + 2 * bt]);

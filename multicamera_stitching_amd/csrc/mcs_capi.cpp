@@ -65,6 +65,13 @@ struct mcs_plan {
     // multi-band band pass: bands (the first n_bands_in reach no bottom / right mosaic edge),
     // blend-tile grid -> list index, descriptors; without bands mb_levels computes the levels
     int n_bands = 0, n_bands_in = 0, gxb = 0;
+    // the band pass and blend in row chunks (prepare_bands): chunk c = interior bands [i0, i1),
+    // edge bands [b0, b1), blend list entries [l0, l1) -- the blend of chunk c needs only the
+    // bands of its tile rows, so it runs beside the next chunk's bands
+    struct MbChunk { int i0, i1, b0, b1, l0, l1; };
+    std::vector<MbChunk> mb_chunks;
+    hipStream_t side3 = nullptr;
+    std::vector<hipEvent_t> ev_band;
     mcs::MbBand *d_bands = nullptr;
     int *d_tile_bt = nullptr;
     uint64_t *d_bdesc = nullptr;
@@ -271,6 +278,8 @@ void mb_args(const mcs_plan *p, const mcs::KParams &P, mcs::KMbArgs &a)
     a.chunk = p->mb_chunk;
     a.f0 = 0;
     a.nf = 0;
+    a.list0 = 0;
+    a.pad_ = 0;
 }
 
 void band_args(const mcs_plan *p, const mcs::KParams &P, mcs::KMbBandArgs &a)
@@ -289,6 +298,8 @@ void band_args(const mcs_plan *p, const mcs::KParams &P, mcs::KMbBandArgs &a)
     a.gxb = p->gxb;
     a.band0 = 0;
     a.n_in = p->n_bands_in;
+    a.band1 = p->n_bands_in;
+    a.pad_ = 0;
     a.xcd = 0;
 }
 
@@ -494,9 +505,51 @@ int prepare_bands(const Api *A, mcs_plan *p, const Kernels *k, hipStream_t s)
         return b.row * mcs::kBlendTileH - mcs::kBlendHalo + mcs::kMbFirst + mcs::kMbUsedY > H ||
                b.c0 + mcs::kMbBandLanes > W;
     };
+    std::stable_sort(bands.begin(), bands.end(),
+                     [](const mcs::MbBand &a, const mcs::MbBand &b) { return a.row < b.row; });
     std::stable_partition(bands.begin(), bands.end(), [&](const mcs::MbBand &b) { return !br(b); });
     p->n_bands_in = (int)(std::find_if(bands.begin(), bands.end(), br) - bands.begin());
     const size_t nb = bands.size();
+    {
+        // row chunks with about equal numbers of blend tiles (MCS_MB_ROW_CHUNKS; default 1 = one
+        // band launch, one blend launch.  Measured, same box, two alternations: C2 2 / 3 chunks
+        // 0.954 / 0.950 ms vs 0.956-0.961 unchunked -- noise --, 4 / 6 chunks 1.00-1.03 ms; C4 3
+        // chunks 1.559 vs 1.523 ms: the launch is bound by the passes' contention with the
+        // streaming kernel, not by the band -> blend order)
+        static const int want = getenv("MCS_MB_ROW_CHUNKS") ? atoi(getenv("MCS_MB_ROW_CHUNKS"))
+                                                            : 1;
+        const int K = std::max(1, std::min(want, n));
+        std::vector<int> row_end;   // first tile row past each chunk
+        for (int c = 1; c < K; c++) {
+            const int i = (int)((int64_t)n * c / K);
+            row_end.push_back(list[1 + 2 * i] / p->gxb);
+        }
+        row_end.push_back(gyb);
+        p->mb_chunks.clear();
+        int r0 = 0;
+        for (int r1 : row_end) {
+            if (r1 <= r0) continue;
+            mcs_plan::MbChunk ch{};
+            auto in_rows = [&](int row) { return row >= r0 && row < r1; };
+            ch.i0 = ch.i1 = ch.b0 = ch.b1 = ch.l0 = ch.l1 = -1;
+            for (int i = 0; i < (int)nb; i++) {
+                if (!in_rows(bands[i].row)) continue;
+                int &lo = i < p->n_bands_in ? ch.i0 : ch.b0, &hi = i < p->n_bands_in ? ch.i1 : ch.b1;
+                if (lo < 0) lo = i;
+                hi = i + 1;
+            }
+            for (int i = 0; i < n; i++) {
+                if (!in_rows(list[1 + 2 * i] / p->gxb)) continue;
+                if (ch.l0 < 0) ch.l0 = i;
+                ch.l1 = i + 1;
+            }
+            if (ch.i0 < 0) ch.i0 = ch.i1 = 0;
+            if (ch.b0 < 0) ch.b0 = ch.b1 = p->n_bands_in;
+            if (ch.l0 < 0) ch.l0 = ch.l1 = 0;
+            p->mb_chunks.push_back(ch);
+            r0 = r1;
+        }
+    }
     HIP_TRY(A->hipMalloc((void **)&p->d_bands, nb * sizeof(mcs::MbBand)));
     HIP_TRY(A->hipMalloc((void **)&p->d_tile_bt, tile_bt.size() * sizeof(int)));
     HIP_TRY(A->hipMalloc((void **)&p->d_bdesc,
@@ -586,6 +639,21 @@ int prepare_blend(const Api *A, mcs_plan *p, const Kernels *k, hipStream_t s)
     HIP_TRY(A->hipStreamSynchronize(s));
     // tail[0]: multi-band tiles with more than kBlendSlots owners (degraded to the feather rule),
     // tail[2]: those of them with pixels to feather (listed in d_dense)
+    if (n > 1) {
+        // the list in tile order (classify appends in arrival order): the multi-band passes
+        // walk it in row chunks
+        std::vector<int> l(1 + 2 * (size_t)n);
+        HIP_TRY(A->hipMemcpyAsync(l.data(), p->d_blist, l.size() * sizeof(int),
+                                  hipMemcpyDeviceToHost, s));
+        HIP_TRY(A->hipStreamSynchronize(s));
+        std::vector<std::pair<int, int>> e((size_t)n);
+        for (int i = 0; i < n; i++) e[i] = {l[1 + 2 * i], l[2 + 2 * i]};
+        std::sort(e.begin(), e.end());
+        for (int i = 0; i < n; i++) l[1 + 2 * i] = e[i].first, l[2 + 2 * i] = e[i].second;
+        HIP_TRY(A->hipMemcpyAsync(p->d_blist, l.data(), l.size() * sizeof(int),
+                                  hipMemcpyHostToDevice, s));
+        HIP_TRY(A->hipStreamSynchronize(s));
+    }
     p->mb_slots = tail[1];
     p->n_degraded = p->blend == MCS_BLEND_MULTIBAND ? tail[0] : 0;
     p->n_dense = tail[2];
@@ -601,6 +669,8 @@ void release_tables(const Api *A, mcs_plan *p)
     if (p->stream) (void)A->hipStreamSynchronize(p->stream);
     if (p->side) (void)A->hipStreamSynchronize(p->side);
     if (p->side2) (void)A->hipStreamSynchronize(p->side2);
+    if (p->side3) (void)A->hipStreamSynchronize(p->side3);
+    p->mb_chunks.clear();
     for (void *q : {(void *)p->d_tiles, (void *)p->d_desc, (void *)p->d_desc4,
                     (void *)p->d_fallback,
                     (void *)p->d_owner, (void *)p->d_binfo, (void *)p->d_blist,
@@ -759,6 +829,26 @@ int launch_mb_levels(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KMb
     return MCS_OK;
 }
 
+// One row chunk of the band pass (captures [f0, f0 + nf)): interior bands [i0, i1) and edge
+// bands [b0, b1) in one fused launch on stream s.
+int launch_band_chunk(const Api *A, const mcs_plan *p, const Kernels *k, const mcs::KParams &P,
+                      const mcs_plan::MbChunk &c, int f0, int nf, hipStream_t s)
+{
+    const int n = (c.i1 - c.i0) + (c.b1 - c.b0);
+    if (n <= 0) return MCS_OK;
+    mcs::KMbBandArgs b;
+    band_args(p, P, b);
+    b.f0 = f0;
+    b.nf = nf;
+    b.band0 = c.i0;
+    b.n_in = c.i1 - c.i0;
+    b.band1 = c.b0;
+    const unsigned gx = band_grid(b, n);
+    const unsigned gy = (unsigned)((nf + mcs::kMbBandFrames - 1) / mcs::kMbBandFrames);
+    return launch_args(A, k->mb_bands[p->fd.channels][2], gx, gy, mcs::kMbBandLanes, 1, &b,
+                       sizeof(b), s);
+}
+
 // Multi-band tiles degraded to the feather rule (more than kBlendSlots owners in their
 // neighbourhood): the feather kernel over d_dense, on stream s after the mosaic is written.
 int launch_dense(const Api *A, const mcs_plan *p, const Kernels *k, const mcs::KParams &P,
@@ -814,7 +904,18 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
     // remaining streaming tiles.  MCS_MB_SPLIT=0 (experiments): the blend after everything.
     static const bool split_on = !getenv("MCS_MB_SPLIT") || strcmp(getenv("MCS_MB_SPLIT"), "0");
     const bool split = mb && split_on && p->d_order && p->n_early > 0 && n_frames <= p->mb_chunk;
-    if (mb) {
+    // row-chunked band pass + blend (split launches with a band pass of 2+ chunks): the blend of
+    // a chunk on side3 as soon as its bands are done, beside the next chunk's bands on side2
+    const bool chunked = split && p->n_bands > 0 && p->mb_chunks.size() > 1 && p->side3 &&
+                         p->ev_band.size() >= p->mb_chunks.size();
+    if (chunked) {
+        HIP_TRY(A->hipStreamWaitEvent(p->side2, p->ev_fork, 0));
+        for (size_t c = 0; c < p->mb_chunks.size(); c++) {
+            const int rc = launch_band_chunk(A, p, k, m.P, p->mb_chunks[c], 0, n_frames, p->side2);
+            if (rc) return rc;
+            HIP_TRY(A->hipEventRecord(p->ev_band[c], p->side2));
+        }
+    } else if (mb) {
         HIP_TRY(A->hipStreamWaitEvent(p->side2, p->ev_fork, 0));
         const int rc = launch_mb_levels(A, p, k, m, 0, std::min(p->mb_chunk, n_frames), p->side2);
         if (rc) return rc;
@@ -848,6 +949,35 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
     static const unsigned lds_late =
         getenv("MCS_STREAM_LDS_LATE") ? (unsigned)atoi(getenv("MCS_STREAM_LDS_LATE")) : 0u;
     const int n_tiles = p->gx * p->gy;
+    if (chunked) {
+        int rc = stream_launch(p->d_order, p->n_early, lds);
+        if (rc) return rc;
+        HIP_TRY(A->hipEventRecord(p->ev_early, s));
+        HIP_TRY(A->hipStreamWaitEvent(p->side3, p->ev_early, 0));
+        if (p->n_fallback > 0) HIP_TRY(A->hipStreamWaitEvent(p->side3, p->ev_join, 0));
+        m.f0 = 0;
+        m.nf = n_frames;
+        const int v = p->mb_slots <= 2 ? 0 : (p->mb_slots <= 4 ? 1 : 2);
+        for (size_t c = 0; c < p->mb_chunks.size(); c++) {
+            const mcs_plan::MbChunk &ch = p->mb_chunks[c];
+            HIP_TRY(A->hipStreamWaitEvent(p->side3, p->ev_band[c], 0));
+            if (ch.l1 <= ch.l0) continue;
+            m.list0 = ch.l0;
+            rc = launch_args(A, k->mb_blend[p->fd.channels][v], (unsigned)(ch.l1 - ch.l0),
+                             (unsigned)n_frames, mcs::kMbBlThreads, 1, &m, sizeof(m), p->side3);
+            if (rc) return rc;
+        }
+        m.list0 = 0;
+        HIP_TRY(A->hipEventRecord(p->ev_join2, p->side3));
+        if (p->n_list > p->n_early) {
+            rc = stream_launch(p->d_order + p->n_early, p->n_list - p->n_early,
+                               std::max(lds, lds_late));
+            if (rc) return rc;
+        }
+        if (p->n_fallback > 0) HIP_TRY(A->hipStreamWaitEvent(s, p->ev_join, 0));
+        HIP_TRY(A->hipStreamWaitEvent(s, p->ev_join2, 0));
+        return launch_dense(A, p, k, P, n_frames, s);
+    }
     if (split) {
         int rc = stream_launch(p->d_order, p->n_early, lds);
         if (rc) return rc;
@@ -921,6 +1051,14 @@ int ensure_side(const Api *A, mcs_plan *p)
     if (p->n_fallback > 0 && !p->side) {
         HIP_TRY(A->hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming));
         HIP_TRY(A->hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking));
+    }
+    if (mb && p->mb_chunks.size() > 1) {
+        if (!p->side3) HIP_TRY(A->hipStreamCreateWithFlags(&p->side3, hipStreamNonBlocking));
+        while (p->ev_band.size() < p->mb_chunks.size()) {
+            hipEvent_t e = nullptr;
+            HIP_TRY(A->hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            p->ev_band.push_back(e);
+        }
     }
     if (mb && !p->side2) {
         HIP_TRY(A->hipEventCreateWithFlags(&p->ev_join2, hipEventDisableTiming));
@@ -1247,6 +1385,9 @@ int mcs_plan_destroy(mcs_plan *p)
             if (p->stream) (void)A->hipStreamDestroy(p->stream);
             if (p->side) (void)A->hipStreamDestroy(p->side);
             if (p->side2) (void)A->hipStreamDestroy(p->side2);
+            if (p->side3) (void)A->hipStreamSynchronize(p->side3);
+            if (p->side3) (void)A->hipStreamDestroy(p->side3);
+            for (hipEvent_t e : p->ev_band) (void)A->hipEventDestroy(e);
             if (p->ev_fork) (void)A->hipEventDestroy(p->ev_fork);
             if (p->ev_join) (void)A->hipEventDestroy(p->ev_join);
             if (p->ev_join2) (void)A->hipEventDestroy(p->ev_join2);

@@ -1118,21 +1118,21 @@ extern "C" __global__ __launch_bounds__(256) void mcs_blend_classify(const mcs::
         const mcs::KMbBandArgs a)                                                              \
     {                                                                                          \
         const int bl = mcs::mb_band_of_block(a);                                               \
-        if (bl >= 0) mcs::mb_bands<CN, mcs::kMbBandFrames, false>(a, bl);                      \
+        if (bl >= 0) mcs::mb_bands<CN, mcs::kMbBandFrames, false>(a, a.band0 + bl);            \
     }                                                                                          \
     extern "C" __global__ __launch_bounds__(64) void mcs_mb_bands_br_c##CN(                    \
         const mcs::KMbBandArgs a)                                                              \
     {                                                                                          \
         const int bl = mcs::mb_band_of_block(a);                                               \
-        if (bl >= 0) mcs::mb_bands<CN, mcs::kMbBandFrames, true>(a, bl);                       \
+        if (bl >= 0) mcs::mb_bands<CN, mcs::kMbBandFrames, true>(a, a.band0 + bl);             \
     }                                                                                          \
     extern "C" __global__ __launch_bounds__(64) void mcs_mb_bands_all_c##CN(                   \
         const mcs::KMbBandArgs a)                                                              \
     {                                                                                          \
         const int bl = mcs::mb_band_of_block(a);                                               \
         if (bl < 0) return;                                                                    \
-        if (bl < a.n_in) mcs::mb_bands<CN, mcs::kMbBandFrames, false>(a, bl);                  \
-        else mcs::mb_bands<CN, mcs::kMbBandFrames, true>(a, bl);                               \
+        if (bl < a.n_in) mcs::mb_bands<CN, mcs::kMbBandFrames, false>(a, a.band0 + bl);        \
+        else mcs::mb_bands<CN, mcs::kMbBandFrames, true>(a, a.band1 + bl - a.n_in);            \
     }                                                                                          \
     extern "C" __global__ __launch_bounds__(MCS_MB_BL_THREADS) MCS_MB_BL_ATTR void             \
         mcs_mb_blend_c##CN##_s2(                                                               \

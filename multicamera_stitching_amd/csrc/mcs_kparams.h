@@ -227,6 +227,7 @@ struct KMbArgs {
     int slots;                     // owners per tile (the tables' slot dimension)
     int chunk;                     // scratch capture stride
     int f0, nf;                    // captures [f0, f0 + nf) of this launch
+    int list0, pad_;               // blend: first list entry of this launch (block x: list0 + x)
 };
 
 // Band pass of the multi-band levels (mcs_mb_bands_c*): one wave per (band, kMbBandFrames
@@ -280,7 +281,10 @@ struct KMbBandArgs {
     int slots, chunk, f0, nf;
     int gxb;                       // blend tiles per mosaic row
     int band0;                     // first band of this launch
-    int n_in;                      // mcs_mb_bands_all: bands below n_in take the interior path
+    int n_in;                      // mcs_mb_bands_all: blocks below n_in take the interior path
+                                   // (band band0 + block), the others the _br path (band
+                                   // band1 + block - n_in)
+    int band1, pad_;
     // band -> block mapping: 0 = block x is band x (consecutive bands round-robin over the 8
     // XCDs); n > 0 = XCD-contiguous: the launch's n bands are dealt to the XCDs in contiguous
     // slices (block b -> band (b % 8) * ceil(n / 8) + b / 8; the grid is padded to a multiple
