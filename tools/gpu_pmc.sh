@@ -14,6 +14,6 @@ for c in "FETCH_SIZE" "WRITE_SIZE" \
          "TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
   echo "$c" > "$R/gpurun_out/pmc/pass$i.txt"
-  timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d "$R/gpurun_out/pmc/pass$i" -o run -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-paste-ref "$@" > "$R/gpurun_out/pmc/pass$i.log" 2>&1 || exit $?
+  timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d "$R/gpurun_out/pmc/pass$i" -o run -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-paste-ref --no-also "$@" > "$R/gpurun_out/pmc/pass$i.log" 2>&1 || exit $?
 done
 echo done
