@@ -505,8 +505,10 @@ int prepare_bands(const Api *A, mcs_plan *p, const Kernels *k, hipStream_t s)
         return b.row * mcs::kBlendTileH - mcs::kBlendHalo + mcs::kMbFirst + mcs::kMbUsedY > H ||
                b.c0 + mcs::kMbBandLanes > W;
     };
-    std::stable_sort(bands.begin(), bands.end(),
-                     [](const mcs::MbBand &a, const mcs::MbBand &b) { return a.row < b.row; });
+    static const bool sort_on = !getenv("MCS_MB_SORT") || strcmp(getenv("MCS_MB_SORT"), "0");
+    if (sort_on)
+        std::stable_sort(bands.begin(), bands.end(),
+                         [](const mcs::MbBand &a, const mcs::MbBand &b) { return a.row < b.row; });
     std::stable_partition(bands.begin(), bands.end(), [&](const mcs::MbBand &b) { return !br(b); });
     p->n_bands_in = (int)(std::find_if(bands.begin(), bands.end(), br) - bands.begin());
     const size_t nb = bands.size();
@@ -639,7 +641,8 @@ int prepare_blend(const Api *A, mcs_plan *p, const Kernels *k, hipStream_t s)
     HIP_TRY(A->hipStreamSynchronize(s));
     // tail[0]: multi-band tiles with more than kBlendSlots owners (degraded to the feather rule),
     // tail[2]: those of them with pixels to feather (listed in d_dense)
-    if (n > 1) {
+    static const bool sort_on = !getenv("MCS_MB_SORT") || strcmp(getenv("MCS_MB_SORT"), "0");
+    if (n > 1 && sort_on) {
         // the list in tile order (classify appends in arrival order): the multi-band passes
         // walk it in row chunks
         std::vector<int> l(1 + 2 * (size_t)n);
