@@ -1,5 +1,5 @@
 # C2 / C4 multi-band bench lines for settings of one environment variable, alternating twice:
-#   bash tools/gpu_env_ab.sh VAR value1 value2 ...   ("-" = unset)
+#   bash tools/experiments/gpu_env_ab.sh VAR value1 value2 ...   ("-" = unset)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out

@@ -1,4 +1,4 @@
-"""Summarise tools/gpu_pmc_c3.sh: per kernel family of the C3 estimation path, dispatches and
+"""Summarise tools/experiments/gpu_pmc_c3.sh: per kernel family of the C3 estimation path, dispatches and
 per-dispatch counter averages, HBM bytes (FETCH_SIZE x 2 per the gfx950 correction + WRITE_SIZE)
 and the derived ratios of pmc_summary.  Writes profiles/r02_pmc_c3.json (argv[1] overrides)."""
 import json
