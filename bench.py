@@ -390,8 +390,8 @@ def companion_lines():
             ["tools/estimate_bench.py", "--stitch", "--pipelined", "--overlap", "--depth", "4",
              "--steps", "300", "--warmup", "20", "--no-cpu-baseline"], 300,
             ("metric", "value", "unit", "ms_per_step", "stitched_mpix_per_s", "config",
-             "latency_ms_upload_to_homographies", "max_reproj_err_px_vs_truth",
-             "max_abs_diff_vs_cpu_render")),
+             "latency_ms_upload_to_homographies", "h2d_gb_per_s", "h2d_link_ceiling_gb_per_s",
+             "frac_of_h2d_link", "max_reproj_err_px_vs_truth", "max_abs_diff_vs_cpu_render")),
         "hamming_matcher": _child_line(["tools/match_bench.py"], 200,
                                        ("metric", "unit", "sizes", "ops_per_pair",
                                         "peak_lane_ops_per_s")),

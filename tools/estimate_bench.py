@@ -328,6 +328,22 @@ def pipelined_main(args, frames, truth, W, Hh, N):
     t0 = time.perf_counter()
     mpix, pair_H, plan, slot = run(args.steps)
     elapsed = time.perf_counter() - t0
+    # the host link's H2D ceiling for the same transfers (pinned frames -> device, back to back
+    # on the upload stream): the uploaded form's bound
+    link = None
+    if not args.resident:
+        with torch.cuda.stream(up):
+            for _ in range(2):
+                for t, h in zip(d[0], host):
+                    t.copy_(h, non_blocking=True)
+            torch.cuda.synchronize()
+            tl = time.perf_counter()
+            reps = 20
+            for _ in range(reps):
+                for t, h in zip(d[0], host):
+                    t.copy_(h, non_blocking=True)
+            torch.cuda.synchronize()
+            link = reps * sum(h.numel() for h in host) / (time.perf_counter() - tl) / 1e9
     ow, oh = plan.out_w, plan.out_h
     got = out[slot][:oh, :ow * 3].cpu().numpy().reshape(oh, ow, 3)
     want = oracle.flat_stitch(plan.describe(), frames)
@@ -353,6 +369,11 @@ def pipelined_main(args, frames, truth, W, Hh, N):
                    "pipeline_depth": D, "rig_jobs": bool(args.overlap),
                    "host_threads": args.threads},
         "frames_resident_in_hbm": bool(args.resident),
+        "h2d_gb_per_s": None if link is None else
+        round(args.steps * sum(h.numel() for h in host) / elapsed / 1e9, 2),
+        "h2d_link_ceiling_gb_per_s": None if link is None else round(link, 2),
+        "frac_of_h2d_link": None if link is None else
+        round(args.steps * sum(h.numel() for h in host) / elapsed / 1e9 / link, 3),
         "latency_ms_upload_to_homographies": round(float(np.mean(lat)) * 1e3, 3),
         "keypoints": est.stats.get("keypoints"), "matches": est.stats.get("matches"),
         "inliers": est.stats.get("inliers"), "max_reproj_err_px_vs_truth": errs,
