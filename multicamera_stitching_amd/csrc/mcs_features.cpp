@@ -678,7 +678,8 @@ int orb_detect(const uint8_t *image, bool on_device, int w, int h, int channels,
             pa.w[l] = lw[l];
             pa.h[l] = lh[l];
             pa.cap[l] = (int)cap[l];
-            pa.bstart[l + 1] = pa.bstart[l] + (lw[l] + 63) / 64 * ((lh[l] + 15) / 16);
+            pa.bstart[l + 1] = pa.bstart[l] + (lw[l] + mcs::kOrbTileW - 1) / mcs::kOrbTileW *
+                                            ((lh[l] + mcs::kOrbTileH - 1) / mcs::kOrbTileH);
         }
         rc = launch(A, k->orb_level, (unsigned)pa.bstart[nlevels], 1, 256, &pa, sizeof(pa), s);
     }

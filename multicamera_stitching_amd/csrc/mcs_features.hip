@@ -449,7 +449,7 @@ __device__ __forceinline__ int orb_refl(int i, int n)
 //     on the staged image) run on full waves, and appended to the level's candidates (their
 //     order is irrelevant: the level is ranked afterwards by response, y, x).
 // Same values as the four per-pixel passes it replaces (blur_h, blur_v, fast, nms).
-constexpr int kOrbTX = 64, kOrbTY = 16, kOrbHalo = 4;
+constexpr int kOrbTX = mcs::kOrbTileW, kOrbTY = mcs::kOrbTileH, kOrbHalo = 4;
 constexpr int kOrbLX = kOrbTX + 2 * kOrbHalo, kOrbLY = kOrbTY + 2 * kOrbHalo;   // 72 x 24
 constexpr int kOrbSX = kOrbTX + 2, kOrbSY = kOrbTY + 2;                         // score ring
 

@@ -77,6 +77,12 @@ struct OrbCand {
     int x, y;
     double response;
 };
+// mcs_orb_level's tile: kOrbTileW x kOrbTileH pixels of a level per block (MCS_ORB_TILE_H: 16 or
+// 32 rows)
+#ifndef MCS_ORB_TILE_H
+#define MCS_ORB_TILE_H 16
+#endif
+constexpr int kOrbTileW = 64, kOrbTileH = MCS_ORB_TILE_H;
 // All levels of one frame in one launch (mcs_orb_level): grid (bstart[nlevels]) blocks of 256
 // threads, level l owning blocks [bstart[l], bstart[l + 1]), one block per 64 x 16 tile (row-major
 // over the level).  Level buffers are the bases + off[l] (pixels) and cand + coff[l].

@@ -311,7 +311,8 @@ int device_setup(mcs_rig_job *j)
         d.pa.w[l] = g.lw[l];
         d.pa.h[l] = g.lh[l];
         d.pa.cap[l] = (int)g.cap[l];
-        d.pa.bstart[l + 1] = d.pa.bstart[l] + (g.lw[l] + 63) / 64 * ((g.lh[l] + 15) / 16);
+        d.pa.bstart[l + 1] = d.pa.bstart[l] + (g.lw[l] + mcs::kOrbTileW - 1) / mcs::kOrbTileW *
+                                                ((g.lh[l] + mcs::kOrbTileH - 1) / mcs::kOrbTileH);
     }
 
     std::memset(&d.sa, 0, sizeof(d.sa));
