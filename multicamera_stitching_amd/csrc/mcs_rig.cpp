@@ -387,8 +387,20 @@ void device_release(mcs_rig_job *j)
     d = RigDevice();
 }
 
-// The capture's launch chain on stream s (its one copy back included): issued directly or
-// recorded into the job's graph.
+// The per-capture resets (candidate counts, kNN-2 keys): stream-ordered memsets issued before
+// the chain or its graph (measured: memset nodes captured into the graph did not reset the counts
+// on replay -- the ranking then overflowed and every capture fell back to the per-call path).
+int enqueue_resets(mcs_rig_job *j, const mcs::rt::Api *A, hipStream_t s)
+{
+    RigDevice &d = j->dev;
+    HIP_TRY(A->hipMemsetAsync(d.buf + d.o_cnt, 0, d.cnt_bytes, s));
+    HIP_TRY(A->hipMemsetAsync(d.buf + d.o_keys, 0xff, d.keys_bytes, s));
+    return MCS_OK;
+}
+
+// The capture's launch chain on stream s (its one copy back included; after enqueue_resets):
+// issued directly or recorded into the job's graph.  Every argument block lives in the job (a
+// graph's kernel nodes keep their arguments for replays).
 int enqueue_chain(mcs_rig_job *j, const mcs::rt::Api *A, const mcs::feat::FeatureKernels *k,
                   hipStream_t s)
 {
@@ -398,13 +410,10 @@ int enqueue_chain(mcs_rig_job *j, const mcs::rt::Api *A, const mcs::feat::Featur
     const mcs::feat::OrbGeom &g = d.geo;
     const size_t pix = g.off[L];
     int rc = MCS_OK;
-    HIP_TRY(A->hipMemsetAsync(d.buf + d.o_cnt, 0, d.cnt_bytes, s));
-    HIP_TRY(A->hipMemsetAsync(d.buf + d.o_keys, 0xff, d.keys_bytes, s));
     if (j->channels == 3) {
-        mcs::KGrayArgs ga = d.ga;
-        for (int c = 0; c < C; c++) ga.bgr[c] = j->frames[c];
-        rc = launch(A, k->orb_gray, (unsigned)((j->w * j->h + 1023) / 1024), C, 256, &ga,
-                    sizeof(ga), s);
+        for (int c = 0; c < C; c++) d.ga.bgr[c] = j->frames[c];
+        rc = launch(A, k->orb_gray, (unsigned)((j->w * j->h + 1023) / 1024), C, 256, &d.ga,
+                    sizeof(d.ga), s);
     } else {
         for (int c = 0; c < C; c++)
             HIP_TRY(A->hipMemcpyAsync(d.ga.gray + c * pix, j->frames[c], (size_t)j->w * j->h,
@@ -463,6 +472,7 @@ int device_capture(mcs_rig_job *j, bool *overflow)
     // MCS_RIG_GRAPH=0: plain launches every capture
     static const bool graphs = !getenv("MCS_RIG_GRAPH") || strcmp(getenv("MCS_RIG_GRAPH"), "0");
     hipError_t e = hipSuccess;
+    if ((rc = enqueue_resets(j, A, s)) != MCS_OK) return rc;
     if (graphs && d.pyr_blocks > 0) {
         if (!d.exec || d.graph_frames != j->frames) {
             if (d.exec) (void)A->hipGraphExecDestroy(d.exec);

@@ -98,6 +98,13 @@ def test_rig_job_equals_python_issued_steps():
             assert np.array_equal(a, b) and np.array_equal(a, c)
         # every capture ran as the one launch chain (no ranking overflow at this size)
         assert est._jobs[0].counts() == (2, 0) and est._jobs[1].counts() == (1, 0)
+        # replays of the job's captured graph (same frames): the same result every time, still
+        # on the device path (per-capture state reset before each replay)
+        for _ in range(4):
+            again = est.estimate(ptrs)
+            for a, b in zip(job, again):
+                assert np.array_equal(a, b)
+        assert est._jobs[0].counts() == (6, 0)
     finally:
         est.close()
 
