@@ -400,13 +400,36 @@ __device__ __forceinline__ MbSrc mb_src(const KParams &P, int s, int x, int y)
 // where d = bytes both windows start earlier so that row b's window ends inside the frame (the
 // taps then sit at bytes d and d + CN).  Every capture's load is then unconditional.  Frames
 // with (h - 1) * w * CN < 16 bytes take load8's guarded path instead.
+// Bits 15..18 of .y: the band pass's dword-aligned form (mb_bands<.., AL>): both tap rows read as
+// 12-byte windows starting sh bytes before tap a, at a 4-byte boundary (sh <= 12 - 2 CN: the
+// taps' 2 CN bytes inside the window; chosen so that row b's window ends inside the frame);
+// 15 = no such window.  Valid wherever the host enables
+// that form (band_aligned: pitch and frame bytes multiples of 4, frames of >= pitch + 12 bytes).
 template <int CN>
 __device__ __forceinline__ uint2 mb_desc(const MbSrc &q, int w, int h)
 {
     const int64_t pitch = (int64_t)w * CN, fbytes = pitch * h;
     const int64_t oa = q.ya * pitch + (int64_t)q.c * CN, ob = oa + (q.yb > q.ya ? pitch : 0);
     const uint32_t d = (uint32_t)min(max(ob + 8 - fbytes, (int64_t)0), (int64_t)7);
-    return make_uint2((uint32_t)oa | (q.yb > q.ya ? 0x80000000u : 0u), q.meta | (d << 12));
+    const int64_t e = fbytes - (ob - oa) - 12;   // last start of row a's window
+    int64_t o4 = oa & ~(int64_t)3;
+    if (o4 > e) o4 = e & ~(int64_t)3;
+    const uint32_t sh = (e >= 0 && oa - o4 <= 12 - 2 * CN) ? (uint32_t)(oa - o4) : 15u;
+    return make_uint2((uint32_t)oa | (q.yb > q.ya ? 0x80000000u : 0u),
+                      q.meta | (d << 12) | (sh << 15));
+}
+
+// The 8 bytes starting sh (<= 10) bytes into a 12-byte window, zero past its end (v_alignbyte
+// funnel shifts).
+template <int CN>
+__device__ __forceinline__ uint2 mb_win_shift(uint3 v, uint32_t sh)
+{
+    const uint32_t s = sh & 3u;
+    const uint32_t a = __builtin_amdgcn_alignbyte(v.y, v.x, s);
+    const uint32_t b = __builtin_amdgcn_alignbyte(v.z, v.y, s);
+    const uint32_t c = __builtin_amdgcn_alignbyte(0u, v.z, s);
+    if (CN <= 2 && (sh & 8u)) return make_uint2(c, 0u);   // (sh > 6 only for 1 or 2 channels)
+    return (sh & 4u) ? make_uint2(b, c) : make_uint2(a, b);
 }
 
 // Source footprint of one (tile, owner) staged in LDS per capture (mb_levels): rows
@@ -1159,14 +1182,22 @@ __device__ __forceinline__ int mb_band_of_block(const KMbBandArgs &a)
     return i < a.xcd ? i : -1;
 }
 
-template <int CN, int FR, bool BR>
+// AL: the windows are read as dword-aligned 12-byte loads (mb_desc's sh) and funnel-shifted in
+// registers, instead of unaligned 8-byte loads (which the texture addresser splits: serial band
+// pass 270 -> ~200 us with aligned windows, tools/experiments/gpu_r03_bandalign.sh).
+template <int CN, int FR, bool BR, bool AL>
 __device__ __forceinline__ void mb_bands(const KMbBandArgs &a, int bi)
 {
     typedef __attribute__((address_space(1))) const uint8_t gu8;
     struct __attribute__((packed)) U2 {
         uint32_t x, y;
     };
+    struct U3 {
+        uint32_t x, y, z;
+    };
     typedef __attribute__((address_space(1))) const U2 gu2;
+    typedef __attribute__((address_space(1))) const U3 gu3;
+    typedef std::conditional_t<AL, uint3, uint2> Win;
     typedef __attribute__((address_space(1))) uint2 g2u;
     const KParams &P = a.P;
     const int l = threadIdx.x;
@@ -1248,8 +1279,9 @@ __device__ __forceinline__ void mb_bands(const KMbBandArgs &a, int bi)
 #pragma unroll
         for (int i = 0; i < FR; i++) hl[i][BR ? 3 : 0] = hh[i][BR ? 3 : 0] = 0u;
     }
-    auto load_win = [&](uint64_t dv, uint2 (&r0)[FR], uint2 (&r1)[FR]) {
-        const uint32_t dx = (uint32_t)dv, d = (uint32_t)(dv >> 44) & 7u;
+    auto load_win = [&](uint64_t dv, Win (&r0)[FR], Win (&r1)[FR]) {
+        const uint32_t dx = (uint32_t)dv;
+        const uint32_t d = AL ? (uint32_t)(dv >> 47) & 15u : (uint32_t)(dv >> 44) & 7u;
         uint32_t o = (dx & 0x7fffffffu) - d, ob = o + ((dx >> 31) ? pitch : 0u);
 #ifdef MCS_MB_BAND_ALIGNED_TEST
         o &= ~7u;   // (timing experiment only: wrong pixels)
@@ -1257,9 +1289,15 @@ __device__ __forceinline__ void mb_bands(const KMbBandArgs &a, int bi)
 #endif
 #pragma unroll
         for (int i = 0; i < FR; i++) {
-            const U2 ra = *(const gu2 *)(fb[i] + o), rb = *(const gu2 *)(fb[i] + ob);
-            r0[i] = make_uint2(ra.x, ra.y);
-            r1[i] = make_uint2(rb.x, rb.y);
+            if constexpr (AL) {
+                const U3 ra = *(const gu3 *)(fb[i] + o), rb = *(const gu3 *)(fb[i] + ob);
+                r0[i] = make_uint3(ra.x, ra.y, ra.z);
+                r1[i] = make_uint3(rb.x, rb.y, rb.z);
+            } else {
+                const U2 ra = *(const gu2 *)(fb[i] + o), rb = *(const gu2 *)(fb[i] + ob);
+                r0[i] = make_uint2(ra.x, ra.y);
+                r1[i] = make_uint2(rb.x, rb.y);
+            }
         }
     };
     // Finished entries wait one row in registers before they are stored: gfx9 counts stores
@@ -1360,7 +1398,7 @@ __device__ __forceinline__ void mb_bands(const KMbBandArgs &a, int bi)
     // at the loop's back edge).
     constexpr int NB = kMbBandBufs, A = kMbBandAhead, ND = kMbBandDescRing;
     uint64_t dq[ND];
-    uint2 wq0[NB][FR], wq1[NB][FR];
+    Win wq0[NB][FR], wq1[NB][FR];
 #pragma unroll
     for (int i = 0; i < ND; i++) dq[i] = dsc[i * kMbBandLanes];
 #pragma unroll
@@ -1371,15 +1409,24 @@ __device__ __forceinline__ void mb_bands(const KMbBandArgs &a, int bi)
             const int r = r12 + ph;
             constexpr int b0 = ph % NB, bA = (ph + A) % NB, d0 = ph % ND, dA = (ph + A) % ND;
             uint32_t wa, wb;
-            const uint32_t meta = (uint32_t)(dq[d0] >> 32), dd = (meta >> 12) & 7u;
+            const uint32_t meta = (uint32_t)(dq[d0] >> 32);
+            const uint32_t dd = AL ? 0u : (meta >> 12) & 7u;
             mb_weights(meta, wa, wb);
             uint32_t v[FR];
 #pragma unroll
             for (int f = 0; f < FR; f++) {
+                uint2 r0, r1;
+                if constexpr (AL) {
+                    const uint32_t sh = (meta >> 15) & 15u;
+                    r0 = mb_win_shift<CN>(wq0[b0][f], sh);
+                    r1 = mb_win_shift<CN>(wq1[b0][f], sh);
+                } else {
+                    r0 = wq0[b0][f];
+                    r1 = wq1[b0][f];
+                }
                 v[f] = 0;
 #pragma unroll
-                for (int c = 0; c < CN; c++)
-                    v[f] |= mb_tap<CN>(wq0[b0][f], wq1[b0][f], wa, wb, c, dd) << (8 * c);
+                for (int c = 0; c < CN; c++) v[f] |= mb_tap<CN>(r0, r1, wa, wb, c, dd) << (8 * c);
             }
             // the previous row's finished entries (after this row's window wait), then the loads:
             // windows of row r + A (its descriptor arrived a row ago), descriptor of row r + A + 1

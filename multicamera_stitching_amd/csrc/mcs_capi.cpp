@@ -115,7 +115,8 @@ struct Kernels {
     hipFunction_t mb_prep[5][2] = {};     // [channels][interp]
     hipFunction_t mb_levels[5] = {};      // [channels]
     hipFunction_t mb_blend[5][3] = {};    // [channels][<= 2 owners, <= 4, <= 8]
-    hipFunction_t mb_bands[5][3] = {};    // [channels][interior, bottom / right edge, both]
+    // [channels][unaligned / dword-aligned windows][interior, bottom / right edge, both]
+    hipFunction_t mb_bands[5][2][3] = {};
     hipFunction_t mb_bdesc[5][2] = {};    // [channels][interp]
 };
 Kernels g_k[kMaxDevices];
@@ -142,12 +143,15 @@ int kernels(const Api *A, int device, const Kernels **out)
             if (rc == MCS_OK) rc = fn(name, &k.resize[c]);
             snprintf(name, sizeof(name), "mcs_mb_levels_c%d", c);
             if (rc == MCS_OK) rc = fn(name, &k.mb_levels[c]);
-            snprintf(name, sizeof(name), "mcs_mb_bands_c%d", c);
-            if (rc == MCS_OK) rc = fn(name, &k.mb_bands[c][0]);
-            snprintf(name, sizeof(name), "mcs_mb_bands_br_c%d", c);
-            if (rc == MCS_OK) rc = fn(name, &k.mb_bands[c][1]);
-            snprintf(name, sizeof(name), "mcs_mb_bands_all_c%d", c);
-            if (rc == MCS_OK) rc = fn(name, &k.mb_bands[c][2]);
+            for (int al = 0; al < 2; al++) {
+                const char *sfx = al ? "_a" : "";
+                snprintf(name, sizeof(name), "mcs_mb_bands%s_c%d", sfx, c);
+                if (rc == MCS_OK) rc = fn(name, &k.mb_bands[c][al][0]);
+                snprintf(name, sizeof(name), "mcs_mb_bands_br%s_c%d", sfx, c);
+                if (rc == MCS_OK) rc = fn(name, &k.mb_bands[c][al][1]);
+                snprintf(name, sizeof(name), "mcs_mb_bands_all%s_c%d", sfx, c);
+                if (rc == MCS_OK) rc = fn(name, &k.mb_bands[c][al][2]);
+            }
             snprintf(name, sizeof(name), "mcs_mb_blend_c%d_s2", c);
             if (rc == MCS_OK) rc = fn(name, &k.mb_blend[c][0]);
             snprintf(name, sizeof(name), "mcs_mb_blend_c%d_s4", c);
@@ -301,6 +305,27 @@ void band_args(const mcs_plan *p, const mcs::KParams &P, mcs::KMbBandArgs &a)
     a.band1 = p->n_bands_in;
     a.pad_ = 0;
     a.xcd = 0;
+}
+
+// The band pass's dword-aligned window form (mb_bands AL, mb_desc's sh) applies when every used
+// camera's rows and frames are multiples of 4 bytes, its frames start at 4-byte boundaries and hold
+// at least pitch + 12 bytes.  MCS_MB_BAND_ALIGNED=0 (experiments): the unaligned 8-byte form.
+int band_form(const mcs_plan *p, const mcs::KParams &P)
+{
+    static const bool off =
+        getenv("MCS_MB_BAND_ALIGNED") && !strcmp(getenv("MCS_MB_BAND_ALIGNED"), "0");
+    if (off) return 0;
+    bool need[MCS_MAX_CAMS];
+    need_mask(p->fd, need);
+    const int C = p->fd.channels;
+    for (int i = 0; i < p->fd.n_cams; i++) {
+        if (!need[i]) continue;
+        const int64_t pitch = (int64_t)p->fd.cam_w[i] * C, fb = pitch * p->fd.cam_h[i];
+        if (pitch % 4 || fb % 4 || fb < pitch + 12 || P.cam_fstride[i] % 4 ||
+            (uintptr_t)P.cams[i] % 4)
+            return 0;
+    }
+    return 1;
 }
 
 // Grid width of a band launch of n bands (XCD-contiguous mapping: padded to a multiple of 8).
@@ -805,20 +830,20 @@ int launch_mb_levels(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KMb
             !getenv("MCS_MB_BANDS_FUSED") || strcmp(getenv("MCS_MB_BANDS_FUSED"), "0") != 0;
         if (fused && p->n_bands_in > 0 && p->n_bands > p->n_bands_in) {
             const unsigned gx = band_grid(b, p->n_bands);
-            return launch_args(A, k->mb_bands[p->fd.channels][2], gx, gy, mcs::kMbBandLanes, 1,
-                               &b, sizeof(b), s);
+            return launch_args(A, k->mb_bands[p->fd.channels][band_form(p, b.P)][2], gx, gy,
+                               mcs::kMbBandLanes, 1, &b, sizeof(b), s);
         }
         int rc = MCS_OK;
         if (p->n_bands_in > 0) {
             const unsigned gx = band_grid(b, p->n_bands_in);
-            rc = launch_args(A, k->mb_bands[p->fd.channels][0], gx, gy, mcs::kMbBandLanes, 1, &b,
-                             sizeof(b), s);
+            rc = launch_args(A, k->mb_bands[p->fd.channels][band_form(p, b.P)][0], gx, gy,
+                             mcs::kMbBandLanes, 1, &b, sizeof(b), s);
         }
         b.band0 = p->n_bands_in;
         if (rc == MCS_OK && p->n_bands > p->n_bands_in) {
             const unsigned gx = band_grid(b, p->n_bands - p->n_bands_in);
-            rc = launch_args(A, k->mb_bands[p->fd.channels][1], gx, gy, mcs::kMbBandLanes, 1, &b,
-                             sizeof(b), s);
+            rc = launch_args(A, k->mb_bands[p->fd.channels][band_form(p, b.P)][1], gx, gy,
+                             mcs::kMbBandLanes, 1, &b, sizeof(b), s);
         }
         return rc;
     }
@@ -848,8 +873,8 @@ int launch_band_chunk(const Api *A, const mcs_plan *p, const Kernels *k, const m
     b.band1 = c.b0;
     const unsigned gx = band_grid(b, n);
     const unsigned gy = (unsigned)((nf + mcs::kMbBandFrames - 1) / mcs::kMbBandFrames);
-    return launch_args(A, k->mb_bands[p->fd.channels][2], gx, gy, mcs::kMbBandLanes, 1, &b,
-                       sizeof(b), s);
+    return launch_args(A, k->mb_bands[p->fd.channels][band_form(p, b.P)][2], gx, gy,
+                       mcs::kMbBandLanes, 1, &b, sizeof(b), s);
 }
 
 // Multi-band tiles degraded to the feather rule (more than kBlendSlots owners in their

@@ -1107,6 +1107,33 @@ extern "C" __global__ __launch_bounds__(256) void mcs_blend_classify(const mcs::
 #ifndef MCS_MB_WAVES
 #define MCS_MB_WAVES 4
 #endif
+// band pass entry points: interior, bottom / right edge, both in one grid; SFX _a = the
+// dword-aligned window form (mb_bands AL).  Up to 3 channels at most 128 VGPRs: 4 waves per SIMD.
+#define MCS_MB_BAND_ATTR(CN) __attribute__((amdgpu_waves_per_eu((CN) <= 3 ? 4 : 3)))
+#define MCS_MB_BANDS_ENTRY(CN, SFX, AL)                                                        \
+    extern "C" __global__ __launch_bounds__(64) MCS_MB_BAND_ATTR(CN) void                     \
+        mcs_mb_bands##SFX##_c##CN(                                                             \
+        const mcs::KMbBandArgs a)                                                              \
+    {                                                                                          \
+        const int bl = mcs::mb_band_of_block(a);                                               \
+        if (bl >= 0) mcs::mb_bands<CN, mcs::kMbBandFrames, false, AL>(a, a.band0 + bl);        \
+    }                                                                                          \
+    extern "C" __global__ __launch_bounds__(64) MCS_MB_BAND_ATTR(CN) void                     \
+        mcs_mb_bands_br##SFX##_c##CN(                                                          \
+        const mcs::KMbBandArgs a)                                                              \
+    {                                                                                          \
+        const int bl = mcs::mb_band_of_block(a);                                               \
+        if (bl >= 0) mcs::mb_bands<CN, mcs::kMbBandFrames, true, AL>(a, a.band0 + bl);         \
+    }                                                                                          \
+    extern "C" __global__ __launch_bounds__(64) MCS_MB_BAND_ATTR(CN) void                     \
+        mcs_mb_bands_all##SFX##_c##CN(                                                         \
+        const mcs::KMbBandArgs a)                                                              \
+    {                                                                                          \
+        const int bl = mcs::mb_band_of_block(a);                                               \
+        if (bl < 0) return;                                                                    \
+        if (bl < a.n_in) mcs::mb_bands<CN, mcs::kMbBandFrames, false, AL>(a, a.band0 + bl);    \
+        else mcs::mb_bands<CN, mcs::kMbBandFrames, true, AL>(a, a.band1 + bl - a.n_in);        \
+    }
 #define MCS_MB_ENTRY(CN)                                                                       \
     extern "C" __global__ __launch_bounds__(MCS_MB_LV_THREADS) __attribute__((amdgpu_waves_per_eu(MCS_MB_WAVES))) \
     void mcs_mb_levels_c##CN(const mcs::KMbArgs a)                                             \
@@ -1114,26 +1141,8 @@ extern "C" __global__ __launch_bounds__(256) void mcs_blend_classify(const mcs::
         __shared__ mcs::MbLvLds<CN> lds;                                                       \
         mcs::mb_levels<CN>(a, lds);                                                            \
     }                                                                                          \
-    extern "C" __global__ __launch_bounds__(64) void mcs_mb_bands_c##CN(                       \
-        const mcs::KMbBandArgs a)                                                              \
-    {                                                                                          \
-        const int bl = mcs::mb_band_of_block(a);                                               \
-        if (bl >= 0) mcs::mb_bands<CN, mcs::kMbBandFrames, false>(a, a.band0 + bl);            \
-    }                                                                                          \
-    extern "C" __global__ __launch_bounds__(64) void mcs_mb_bands_br_c##CN(                    \
-        const mcs::KMbBandArgs a)                                                              \
-    {                                                                                          \
-        const int bl = mcs::mb_band_of_block(a);                                               \
-        if (bl >= 0) mcs::mb_bands<CN, mcs::kMbBandFrames, true>(a, a.band0 + bl);             \
-    }                                                                                          \
-    extern "C" __global__ __launch_bounds__(64) void mcs_mb_bands_all_c##CN(                   \
-        const mcs::KMbBandArgs a)                                                              \
-    {                                                                                          \
-        const int bl = mcs::mb_band_of_block(a);                                               \
-        if (bl < 0) return;                                                                    \
-        if (bl < a.n_in) mcs::mb_bands<CN, mcs::kMbBandFrames, false>(a, a.band0 + bl);        \
-        else mcs::mb_bands<CN, mcs::kMbBandFrames, true>(a, a.band1 + bl - a.n_in);            \
-    }                                                                                          \
+    MCS_MB_BANDS_ENTRY(CN, , false)                                                            \
+    MCS_MB_BANDS_ENTRY(CN, _a, true)                                                           \
     extern "C" __global__ __launch_bounds__(MCS_MB_BL_THREADS) MCS_MB_BL_ATTR void             \
         mcs_mb_blend_c##CN##_s2(                                                               \
         const mcs::KMbArgs a)                                                                  \
