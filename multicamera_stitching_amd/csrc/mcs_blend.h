@@ -1182,12 +1182,18 @@ __device__ __forceinline__ int mb_band_of_block(const KMbBandArgs &a)
     return i < a.xcd ? i : -1;
 }
 
-// AL: the windows are read as dword-aligned 12-byte loads (mb_desc's sh) and funnel-shifted in
-// registers, instead of unaligned 8-byte loads (which the texture addresser splits: serial band
-// pass 270 -> ~200 us with aligned windows, tools/experiments/gpu_r03_bandalign.sh).
-template <int CN, int FR, bool BR, bool AL>
-__device__ __forceinline__ void mb_bands(const KMbBandArgs &a, int bi)
+// Window modes (WM): 0 = unaligned 8-byte global loads; 1 (AL) = dword-aligned 12-byte global
+// loads (mb_desc's sh), funnel-shifted in registers (the texture addresser splits unaligned
+// loads: serial band pass 270 -> ~220 us, tools/experiments/gpu_r03_bandalign.sh); 2 = the
+// band's source rows staged in an LDS ring by LDS-DMA, 4 rows per wave instruction (KMbBandArgs
+// bgrp), the windows read from LDS (descriptor .x = the two windows' ring offsets): one 16-byte
+// chunk per lane instead of four 12-byte gathers per lane and row.  Mode 2 needs a band whose
+// source rows advance with its rows (mcs_capi.cpp band_lds_tables checks the ring schedule);
+// the other bands of an aligned launch take mode 1.
+template <int CN, int FR, bool BR, int WM>
+__device__ __forceinline__ void mb_bands_body(const KMbBandArgs &a, int bi, lds_u8 *ring)
 {
+    constexpr bool AL = WM >= 1, LD = WM == 2;
     typedef __attribute__((address_space(1))) const uint8_t gu8;
     struct __attribute__((packed)) U2 {
         uint32_t x, y;
@@ -1280,6 +1286,7 @@ __device__ __forceinline__ void mb_bands(const KMbBandArgs &a, int bi)
         for (int i = 0; i < FR; i++) hl[i][BR ? 3 : 0] = hh[i][BR ? 3 : 0] = 0u;
     }
     auto load_win = [&](uint64_t dv, Win (&r0)[FR], Win (&r1)[FR]) {
+        if constexpr (LD) return;
         const uint32_t dx = (uint32_t)dv;
         const uint32_t d = AL ? (uint32_t)(dv >> 47) & 15u : (uint32_t)(dv >> 44) & 7u;
         uint32_t o = (dx & 0x7fffffffu) - d, ob = o + ((dx >> 31) ? pitch : 0u);
@@ -1399,6 +1406,27 @@ __device__ __forceinline__ void mb_bands(const KMbBandArgs &a, int bi)
     constexpr int NB = kMbBandBufs, A = kMbBandAhead, ND = kMbBandDescRing;
     uint64_t dq[ND];
     Win wq0[NB][FR], wq1[NB][FR];
+    // LDS mode: group g = the band's source rows 4g .. 4g + 3 (from its first) into ring rows
+    // (4g .. 4g + 3) mod kMbLdsRows of every capture's ring, one LDS-DMA instruction per capture
+    // (lane = 16-byte chunk, byte offsets in the frame from bgrp); groups 0 .. kMbLdsLead / 4 before
+    // the loop, group r / 4 + kMbLdsLead / 4 + 1 after row r (r % 4 == 0).  The descriptor loads
+    // that follow every group DMA (one per row) make `s_waitcnt vmcnt(kMbLdsWait)` before a row's
+    // LDS reads cover every group the schedule lets that row read.
+    const uint32_t *grp = a.bgrp + (int64_t)bi * kMbLdsGroups * kMbBandLanes + l;
+    uint32_t gq = 0;
+    auto issue_group = [&](int g, uint32_t off) {
+#pragma unroll
+        for (int f = 0; f < FR; f++)
+            __builtin_amdgcn_global_load_lds(fb[f] + off,
+                                             ring + f * kMbLdsRingBytes + ((4 * g) % kMbLdsRows) * kMbLdsSpan,
+                                             16, 0, 0);
+        asm volatile("" ::: "memory");   // (the next row's descriptor load stays after the DMAs)
+    };
+    if constexpr (LD) {
+#pragma unroll
+        for (int g = 0; g <= kMbLdsLead / 4; g++) issue_group(g, grp[g * kMbBandLanes]);
+        gq = grp[(kMbLdsLead / 4 + 1) * kMbBandLanes];
+    }
 #pragma unroll
     for (int i = 0; i < ND; i++) dq[i] = dsc[i * kMbBandLanes];
 #pragma unroll
@@ -1413,10 +1441,18 @@ __device__ __forceinline__ void mb_bands(const KMbBandArgs &a, int bi)
             const uint32_t dd = AL ? 0u : (meta >> 12) & 7u;
             mb_weights(meta, wa, wb);
             uint32_t v[FR];
+            if constexpr (LD) asm volatile("s_waitcnt vmcnt(" MCS_STR(MCS_MB_LDS_WAIT) ")" ::: "memory");
 #pragma unroll
             for (int f = 0; f < FR; f++) {
                 uint2 r0, r1;
-                if constexpr (AL) {
+                if constexpr (LD) {
+                    typedef __attribute__((address_space(3))) const uint32_t lu32;
+                    const uint32_t dx = (uint32_t)dq[d0], sh = (meta >> 15) & 15u;
+                    const lu32 *pa = (const lu32 *)(ring + f * kMbLdsRingBytes + (dx & 0xffffu));
+                    const lu32 *pb = (const lu32 *)(ring + f * kMbLdsRingBytes + (dx >> 16));
+                    r0 = mb_win_shift<CN>(make_uint3(pa[0], pa[1], pa[2]), sh);
+                    r1 = mb_win_shift<CN>(make_uint3(pb[0], pb[1], pb[2]), sh);
+                } else if constexpr (AL) {
                     const uint32_t sh = (meta >> 15) & 15u;
                     r0 = mb_win_shift<CN>(wq0[b0][f], sh);
                     r1 = mb_win_shift<CN>(wq1[b0][f], sh);
@@ -1432,6 +1468,12 @@ __device__ __forceinline__ void mb_bands(const KMbBandArgs &a, int bi)
             // windows of row r + A (its descriptor arrived a row ago), descriptor of row r + A + 1
             flush();
             load_win(dq[dA], wq0[bA], wq1[bA]);
+            if constexpr (LD) {
+                if constexpr (ph % 4 == 0) {
+                    issue_group(r / 4 + kMbLdsLead / 4 + 1, gq);
+                    gq = grp[(r / 4 + kMbLdsLead / 4 + 2) * kMbBandLanes];
+                }
+            }
             dq[d0] = dsc[(r + ND) * kMbBandLanes];
             // level-0 row r = 2k + (ph & 1), k % 3 = K3; level-1 row k - 2 = 2m + P2, m % 3 = M3
             constexpr int K3 = (ph / 2) % 3;
@@ -1461,6 +1503,19 @@ __device__ __forceinline__ void mb_bands(const KMbBandArgs &a, int bi)
         });
     }
     flush();
+}
+
+// The band pass of band bi: the aligned launch (AL) runs bands flagged for the LDS ring (MbBand
+// pad_ bit 0, band_lds_tables) in mode 2, the others in mode 1.
+template <int CN, int FR, bool BR, bool AL>
+__device__ __forceinline__ void mb_bands(const KMbBandArgs &a, int bi, lds_u8 *ring)
+{
+    if constexpr (AL) {
+        if (__builtin_amdgcn_readfirstlane(a.bands[bi].pad_) & 1) mb_bands_body<CN, FR, BR, 2>(a, bi, ring);
+        else mb_bands_body<CN, FR, BR, 1>(a, bi, ring);
+    } else {
+        mb_bands_body<CN, FR, BR, 0>(a, bi, ring);
+    }
 }
 
 // ---- blend: grid (listed tiles, nf), block kMbBlThreads ------------------------------------------

@@ -75,6 +75,8 @@ struct mcs_plan {
     mcs::MbBand *d_bands = nullptr;
     int *d_tile_bt = nullptr;
     uint64_t *d_bdesc = nullptr;
+    uint32_t *d_bgrp = nullptr;    // LDS-ring band pass: group source offsets (band_lds_tables)
+    int n_bands_lds = 0;
     // cylindrical plans: per-column (sin, cos) and per-row h, host copy and device table
     bool cyl = false;
     std::vector<double> cyl_tab;
@@ -293,6 +295,7 @@ void band_args(const mcs_plan *p, const mcs::KParams &P, mcs::KMbBandArgs &a)
     a.tile_bt = p->d_tile_bt;
     a.bands = p->d_bands;
     a.bdesc = p->d_bdesc;
+    a.bgrp = p->d_bgrp;
     a.g1 = p->d_mbg1;
     a.g2 = p->d_mbg2;
     a.slots = p->mb_slots;
@@ -402,6 +405,8 @@ std::vector<int> launch_list(const std::vector<int> &tiles)
 // the windows' sample descriptors (once).  Mosaics under 128 px a side (a unit would reach past
 // two opposite edges) and plans whose camera frames are too small for the 8-byte window loads
 // stay with mb_levels.
+int band_lds_tables(const Api *A, mcs_plan *p, std::vector<mcs::MbBand> &bands, hipStream_t s);
+
 int prepare_bands(const Api *A, mcs_plan *p, const Kernels *k, hipStream_t s)
 {
     const int n = p->n_blend, S = p->mb_slots, C = p->fd.channels;
@@ -591,12 +596,120 @@ int prepare_bands(const Api *A, mcs_plan *p, const Kernels *k, hipStream_t s)
     int rc = launch_args(A, k->mb_bdesc[C][p->fd.interp], (unsigned)nb, 1, 256, 1, &a, sizeof(a),
                          s);
     if (rc) return rc;
+    rc = band_lds_tables(A, p, bands, s);
+    if (rc) return rc;
     // the band pass writes only the entries the blend reads: the rest of the scratch holds
     // zeros (or an earlier capture's value of the same entry), never stale garbage
     HIP_TRY(A->hipMemsetAsync(p->d_mbg1, 0,
                               (size_t)n * S * p->mb_chunk * mcs::kMbNRX * mcs::kMbNRY * 8, s));
     HIP_TRY(A->hipMemsetAsync(p->d_mbg2, 0,
                               (size_t)n * S * p->mb_chunk * mcs::kMbN2X * mcs::kMbN2Y * C * 4, s));
+    HIP_TRY(A->hipStreamSynchronize(s));
+    return MCS_OK;
+}
+
+// LDS-ring form of the band pass (mb_bands_body mode 2), once per plan: from the device-built
+// window descriptors (mb_bdesc) of every band, the band's source rows [y0, y1] (both taps of
+// every lane and row), per row the byte span its samples read and the 256-byte window of the row
+// staged for it (16-byte aligned, moved back to end inside the frame), the group table (LDS-DMA
+// source offsets of rows 4g .. 4g + 3 per lane) and the descriptors rewritten to ring offsets.
+// A band takes the ring only when its rows fit the schedule of mb_bands_body: every row's groups
+// issued >= kMbLdsWait rows before it and still resident (rows advancing with the band's rows, at
+// most kMbLdsRows in flight); the rest keep the global-window form.  MCS_MB_BAND_LDS=0: none.
+int band_lds_tables(const Api *A, mcs_plan *p, std::vector<mcs::MbBand> &bands, hipStream_t s)
+{
+    static const bool off = getenv("MCS_MB_BAND_LDS") && !strcmp(getenv("MCS_MB_BAND_LDS"), "0");
+    const size_t nb = bands.size();
+    const int C = p->fd.channels, R = mcs::kMbBandRows, DR = mcs::kMbBandDescRows;
+    const int L = mcs::kMbBandLanes, NG = mcs::kMbLdsGroups, K = mcs::kMbLdsRows;
+    const int SP = mcs::kMbLdsSpan, D4 = mcs::kMbLdsLead / 4;
+    p->n_bands_lds = 0;
+    if (off) return MCS_OK;
+    std::vector<uint64_t> desc(nb * DR * L);
+    HIP_TRY(A->hipMemcpyAsync(desc.data(), p->d_bdesc, desc.size() * sizeof(uint64_t),
+                              hipMemcpyDeviceToHost, s));
+    HIP_TRY(A->hipStreamSynchronize(s));
+    std::vector<uint32_t> grp(nb * NG * L, 0u);
+    // row r's loop position at which group g is issued (prologue groups: 4 descriptor loads and
+    // the group-offset load follow them before row 0)
+    auto issue = [&](int g) { return g <= D4 ? -4 : 4 * (g - D4 - 1); };
+    for (size_t i = 0; i < nb; i++) {
+        const int slot = bands[i].slot;
+        const int w = slot == 0 ? p->kp.cam0_w : p->kp.st[slot - 1].src_w;
+        const int h = slot == 0 ? p->kp.cam0_h : p->kp.st[slot - 1].src_h;
+        const int64_t pitch = (int64_t)w * C, fb = pitch * h;
+        if (pitch % 4 || pitch < SP) continue;
+        uint64_t *d = desc.data() + i * DR * L;
+        int y0 = INT32_MAX, y1 = -1;
+        bool ok = true;
+        for (int e = 0; e < R * L && ok; e++) {
+            const uint32_t dx = (uint32_t)d[e], sh = (uint32_t)(d[e] >> 47) & 15u;
+            const int64_t oa = dx & 0x7fffffffu;
+            const int ya = (int)(oa / pitch), yb = ya + (int)(dx >> 31);
+            ok = sh != 15u && yb < h;
+            y0 = std::min(y0, ya);
+            y1 = std::max(y1, yb);
+        }
+        if (!ok || y1 - y0 + 1 > 4 * (NG - 2)) continue;
+        const int nr = y1 - y0 + 1;
+        std::vector<int64_t> lo(nr, INT64_MAX), hi(nr, -1), bs(nr, 0);
+        std::vector<int> glo(R, INT32_MAX), ghi(R, -1);
+        for (int r = 0; r < R; r++)
+            for (int l = 0; l < L; l++) {
+                const uint32_t dx = (uint32_t)d[r * L + l];
+                const int64_t oa = dx & 0x7fffffffu, cb = oa % pitch;
+                const int ya = (int)(oa / pitch) - y0, yb = ya + (int)(dx >> 31);
+                for (int y : {ya, yb}) {
+                    lo[y] = std::min(lo[y], cb);
+                    hi[y] = std::max(hi[y], cb + 2 * C);
+                }
+                glo[r] = std::min(glo[r], ya / 4);
+                ghi[r] = std::max(ghi[r], yb / 4);
+            }
+        // staged window of every row: 16-byte aligned at its first byte, moved back so that its
+        // 256 bytes end inside the frame (4-byte steps: pitch is a multiple of 4)
+        for (int y = 0; y < nr && ok; y++) {
+            const int64_t room = fb - (int64_t)(y0 + y) * pitch - SP;
+            bs[y] = std::min(hi[y] < 0 ? 0 : lo[y] & ~(int64_t)15, room);
+            ok = bs[y] >= 0 && (hi[y] < 0 || hi[y] - bs[y] <= SP);
+        }
+        for (int r = 0; r < R && ok; r++)
+            ok = issue(ghi[r]) <= r - mcs::kMbLdsWait && issue(glo[r] + K / 4) >= r;
+        if (!ok) continue;
+        // group table: lane l loads chunk l % 16 of row 4g + l / 16 (rows past the band or the
+        // frame: the band's last row, never read)
+        uint32_t *gt = grp.data() + i * NG * L;
+        for (int g = 0; g < NG; g++)
+            for (int l = 0; l < L; l++) {
+                const int y = std::min(4 * g + l / 16, nr - 1);
+                gt[g * L + l] = (uint32_t)((int64_t)(y0 + y) * pitch + bs[y] + 16 * (l % 16));
+            }
+        // descriptors: .x = ring offsets of the tap-a / tap-b windows (4-byte aligned), .y keeps
+        // the weights and takes the window shift sh = tap byte & 3
+        for (int r = 0; r < DR; r++)
+            for (int l = 0; l < L; l++) {
+                const uint64_t v = d[std::min(r, R - 1) * L + l];
+                const uint32_t dx = (uint32_t)v, dy = (uint32_t)(v >> 32);
+                const int64_t oa = dx & 0x7fffffffu, cb = oa % pitch;
+                const int ya = (int)(oa / pitch) - y0, yb = ya + (int)(dx >> 31);
+                const uint32_t wa = (uint32_t)((ya % K) * SP + ((cb & ~(int64_t)3) - bs[ya]));
+                const uint32_t wb = (uint32_t)((yb % K) * SP + ((cb & ~(int64_t)3) - bs[yb]));
+                const uint32_t ny = (dy & ~(15u << 15)) | ((uint32_t)(cb & 3) << 15);
+                d[r * L + l] = (uint64_t)(wa | (wb << 16)) | ((uint64_t)ny << 32);
+            }
+        bands[i].pad_ |= 1;
+        p->n_bands_lds++;
+    }
+    if (getenv("MCS_DEBUG_BANDS"))
+        fprintf(stderr, "bands %zu, LDS-ring form %d\n", nb, p->n_bands_lds);
+    if (p->n_bands_lds == 0) return MCS_OK;
+    HIP_TRY(A->hipMalloc((void **)&p->d_bgrp, grp.size() * sizeof(uint32_t)));
+    HIP_TRY(A->hipMemcpyAsync(p->d_bgrp, grp.data(), grp.size() * sizeof(uint32_t),
+                              hipMemcpyHostToDevice, s));
+    HIP_TRY(A->hipMemcpyAsync(p->d_bdesc, desc.data(), desc.size() * sizeof(uint64_t),
+                              hipMemcpyHostToDevice, s));
+    HIP_TRY(A->hipMemcpyAsync(p->d_bands, bands.data(), nb * sizeof(mcs::MbBand),
+                              hipMemcpyHostToDevice, s));
     HIP_TRY(A->hipStreamSynchronize(s));
     return MCS_OK;
 }
@@ -704,8 +817,10 @@ void release_tables(const Api *A, mcs_plan *p)
                     (void *)p->d_owner, (void *)p->d_binfo, (void *)p->d_blist,
                     (void *)p->d_mbdesc, (void *)p->d_mbtab, (void *)p->d_mbfoot, (void *)p->d_mbg1,
                     (void *)p->d_mbg2, (void *)p->d_bands, (void *)p->d_tile_bt,
-                    (void *)p->d_bdesc, (void *)p->d_order})
+                    (void *)p->d_bdesc, (void *)p->d_bgrp, (void *)p->d_order})
         if (q) (void)A->hipFree(q);
+    p->d_bgrp = nullptr;
+    p->n_bands_lds = 0;
     p->d_order = nullptr;
     p->n_early = p->n_list = 0;
     p->d_bands = nullptr;

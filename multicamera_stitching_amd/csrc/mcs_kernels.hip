@@ -1110,29 +1110,36 @@ extern "C" __global__ __launch_bounds__(256) void mcs_blend_classify(const mcs::
 // band pass entry points: interior, bottom / right edge, both in one grid; SFX _a = the
 // dword-aligned window form (mb_bands AL).  Up to 3 channels at most 128 VGPRs: 4 waves per SIMD.
 #define MCS_MB_BAND_ATTR(CN) __attribute__((amdgpu_waves_per_eu((CN) <= 3 ? 4 : 3)))
+// (the aligned entries hold the LDS ring of mode 2; the others none)
+#define MCS_MB_BAND_RING(AL)                                                                   \
+    __shared__ __attribute__((aligned(16))) uint8_t ring_[(AL) ? mcs::kMbLdsBytes : 16];       \
+    mcs::lds_u8 *const ring = (mcs::lds_u8 *)ring_
 #define MCS_MB_BANDS_ENTRY(CN, SFX, AL)                                                        \
     extern "C" __global__ __launch_bounds__(64) MCS_MB_BAND_ATTR(CN) void                     \
         mcs_mb_bands##SFX##_c##CN(                                                             \
         const mcs::KMbBandArgs a)                                                              \
     {                                                                                          \
+        MCS_MB_BAND_RING(AL);                                                                  \
         const int bl = mcs::mb_band_of_block(a);                                               \
-        if (bl >= 0) mcs::mb_bands<CN, mcs::kMbBandFrames, false, AL>(a, a.band0 + bl);        \
+        if (bl >= 0) mcs::mb_bands<CN, mcs::kMbBandFrames, false, AL>(a, a.band0 + bl, ring);  \
     }                                                                                          \
     extern "C" __global__ __launch_bounds__(64) MCS_MB_BAND_ATTR(CN) void                     \
         mcs_mb_bands_br##SFX##_c##CN(                                                          \
         const mcs::KMbBandArgs a)                                                              \
     {                                                                                          \
+        MCS_MB_BAND_RING(AL);                                                                  \
         const int bl = mcs::mb_band_of_block(a);                                               \
-        if (bl >= 0) mcs::mb_bands<CN, mcs::kMbBandFrames, true, AL>(a, a.band0 + bl);         \
+        if (bl >= 0) mcs::mb_bands<CN, mcs::kMbBandFrames, true, AL>(a, a.band0 + bl, ring);   \
     }                                                                                          \
     extern "C" __global__ __launch_bounds__(64) MCS_MB_BAND_ATTR(CN) void                     \
         mcs_mb_bands_all##SFX##_c##CN(                                                         \
         const mcs::KMbBandArgs a)                                                              \
     {                                                                                          \
+        MCS_MB_BAND_RING(AL);                                                                  \
         const int bl = mcs::mb_band_of_block(a);                                               \
         if (bl < 0) return;                                                                    \
-        if (bl < a.n_in) mcs::mb_bands<CN, mcs::kMbBandFrames, false, AL>(a, a.band0 + bl);    \
-        else mcs::mb_bands<CN, mcs::kMbBandFrames, true, AL>(a, a.band1 + bl - a.n_in);        \
+        if (bl < a.n_in) mcs::mb_bands<CN, mcs::kMbBandFrames, false, AL>(a, a.band0 + bl, ring); \
+        else mcs::mb_bands<CN, mcs::kMbBandFrames, true, AL>(a, a.band1 + bl - a.n_in, ring);  \
     }
 #define MCS_MB_ENTRY(CN)                                                                       \
     extern "C" __global__ __launch_bounds__(MCS_MB_LV_THREADS) __attribute__((amdgpu_waves_per_eu(MCS_MB_WAVES))) \

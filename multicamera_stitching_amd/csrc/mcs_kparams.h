@@ -270,6 +270,23 @@ constexpr int kMbBandStride = 52;  // window step: consecutive windows' level-2 
 #define MCS_MB_BAND_FRAMES 2
 #endif
 constexpr int kMbBandFrames = MCS_MB_BAND_FRAMES;
+// LDS-ring band pass (mb_bands_body mode 2): per capture a ring of kMbLdsRows source rows of
+// kMbLdsSpan bytes each; groups of 4 rows, kMbLdsLead rows loaded before the first row;
+// `s_waitcnt vmcnt(MCS_MB_LDS_WAIT)` before each row's LDS reads
+#define MCS_STR_(x) #x
+#define MCS_STR(x) MCS_STR_(x)
+#ifndef MCS_MB_LDS_WAIT
+#define MCS_MB_LDS_WAIT 2
+#endif
+constexpr int kMbLdsSpan = 256;
+constexpr int kMbLdsRows = 20;
+constexpr int kMbLdsLead = 8;
+constexpr int kMbLdsWait = MCS_MB_LDS_WAIT;
+constexpr int kMbLdsRingBytes = kMbLdsRows * kMbLdsSpan;
+constexpr int kMbLdsBytes = kMbBandFrames * kMbLdsRingBytes + 16;   // (+ the last window's tail)
+constexpr int kMbLdsGroups = kMbBandRows / 4 + kMbLdsLead / 4 + 3;  // group offsets per band
+static_assert(kMbLdsRows % 4 == 0 && kMbLdsLead % 4 == 0 && kMbLdsRows / 4 > kMbLdsLead / 4 + 1,
+              "LDS band ring: whole groups, the prologue's groups never evicted by the loop's first");
 struct KMbBandArgs {
     KParams P;
     const int *list;               // blend tile list (tile, mask)
@@ -278,6 +295,7 @@ struct KMbBandArgs {
     uint64_t *bdesc;               // [bands][kMbBandDescRows][kMbBandLanes] window descriptors
     uint16_t *g1;                  // scratch, as KMbArgs
     int32_t *g2;
+    const uint32_t *bgrp;          // [bands][kMbLdsGroups][kMbBandLanes] LDS-ring group offsets
     int slots, chunk, f0, nf;
     int gxb;                       // blend tiles per mosaic row
     int band0;                     // first band of this launch

@@ -1,5 +1,5 @@
 # PMC passes over the serial multi-band launch (band kernel alone); per-kernel averages with
-#   MCS_PMC_DIR=gpurun_out/pmc_bands python tools/pmc_kernel.py mcs_mb_bands_c3
+#   MCS_PMC_DIR=gpurun_out/pmc_bands python tools/pmc_kernel.py mcs_mb_bands_all_a_c3
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
@@ -10,6 +10,7 @@ i=0
 for c in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU" \
          "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_SMEM" \
          "TA_BUSY_avr TA_BUSY_max" \
+         "TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_PENDING_STALL_CYCLES_sum" \
          "FETCH_SIZE"; do
   i=$((i+1))
   echo "$c" > "$R/gpurun_out/pmc_bands/pass$i.txt"
