@@ -1182,6 +1182,57 @@ __device__ __forceinline__ int mb_band_of_block(const KMbBandArgs &a)
     return i < a.xcd ? i : -1;
 }
 
+// CN consecutive ints by one buffer store (offset past the range: nothing written).
+template <int CN>
+__device__ __forceinline__ void mb_buffer_store_ch(__amdgpu_buffer_rsrc_t rs, uint32_t off,
+                                                   const int (&v)[CN])
+{
+    typedef unsigned int u2v __attribute__((ext_vector_type(2)));
+    typedef unsigned int u3v __attribute__((ext_vector_type(3)));
+    typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+    if constexpr (CN == 1) {
+        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v[0], rs, off, 0, 0);
+    } else if constexpr (CN == 2) {
+        const u2v t = {(uint32_t)v[0], (uint32_t)v[CN > 1 ? 1 : 0]};
+        __builtin_amdgcn_raw_buffer_store_b64(t, rs, off, 0, 0);
+    } else if constexpr (CN == 3) {
+        const u3v t = {(uint32_t)v[0], (uint32_t)v[CN > 1 ? 1 : 0], (uint32_t)v[CN > 2 ? 2 : 0]};
+        __builtin_amdgcn_raw_buffer_store_b96(t, rs, off, 0, 0);
+    } else {
+        const u4v t = {(uint32_t)v[0], (uint32_t)v[CN > 1 ? 1 : 0], (uint32_t)v[CN > 2 ? 2 : 0],
+                       (uint32_t)v[CN > 3 ? 3 : 0]};
+        __builtin_amdgcn_raw_buffer_store_b128(t, rs, off, 0, 0);
+    }
+}
+
+// LDS band pass: vector memory operations issued at body row ph (after its LDS reads): the
+// stores of the entries finished by the previous row (2 targets per capture: level 1 after odd
+// rows, level 2 after rows 4j + 1), the group DMAs (rows 4j, one per capture), the descriptor DMA.
+template <int FR>
+constexpr int mb_lds_ops(int ph)
+{
+    return ((ph & 1) ? 2 * FR : 0) + (ph % 4 == 1 ? 2 * FR : 0) + (ph % 4 == 0 ? FR : 0) + 1;
+}
+// The vmcnt bound before row ph's LDS reads: no more operations outstanding than were issued after
+// the latest one that row needs -- its descriptor (issued NL rows earlier, last in that row) and
+// its source groups (issued >= kMbLdsGLead rows earlier, before that row's descriptor).  First
+// body pass, ph < NL: the descriptor came in the prologue, followed by the prologue's later
+// descriptors and this pass's rows (the groups those rows may read are all prologue groups).
+template <int FR, int NL>
+constexpr int mb_lds_wait(int ph, bool first)
+{
+    int d = 0, g = 1;
+    for (int j = 1; j < NL; j++) d += mb_lds_ops<FR>((ph - j + 12) % 12);
+    for (int j = 1; j < kMbLdsGLead; j++) g += mb_lds_ops<FR>((ph - j + 12) % 12);
+    int w = d < g ? d : g;
+    if (first) {
+        int w0 = NL - 1 - ph;
+        for (int j = 0; j < ph; j++) w0 += mb_lds_ops<FR>(j);
+        w = w0 < w ? w0 : w;
+    }
+    return w > 63 ? 63 : w;
+}
+
 // Window modes (WM): 0 = unaligned 8-byte global loads; 1 (AL) = dword-aligned 12-byte global
 // loads (mb_desc's sh), funnel-shifted in registers (the texture addresser splits unaligned
 // loads: serial band pass 270 -> ~220 us, tools/experiments/gpu_r03_bandalign.sh); 2 = the
@@ -1189,7 +1240,10 @@ __device__ __forceinline__ int mb_band_of_block(const KMbBandArgs &a)
 // bgrp), the windows read from LDS (descriptor .x = the two windows' ring offsets): one 16-byte
 // chunk per lane instead of four 12-byte gathers per lane and row.  Mode 2 needs a band whose
 // source rows advance with its rows (mcs_capi.cpp band_lds_tables checks the ring schedule);
-// the other bands of an aligned launch take mode 1.
+// the other bands of an aligned launch take mode 1.  In mode 2 the descriptors come by LDS-DMA
+// too (16 B per lane and row: windows, meta, the offset of the group issued after that row), so
+// the loop holds no ordinary global load: the compiler's own vmcnt waits for ordinary loads
+// would otherwise drain the LDS-DMAs every row.
 template <int CN, int FR, bool BR, int WM>
 __device__ __forceinline__ void mb_bands_body(const KMbBandArgs &a, int bi, lds_u8 *ring)
 {
@@ -1313,6 +1367,43 @@ __device__ __forceinline__ void mb_bands_body(const KMbBandArgs &a, int bi, lds_
     int pend1 = -1, pend2 = -1;   // array row of the pending level-1 / level-2 entries (-1: none)
     uint32_t p1l[FR], p1h[FR];
     int p2[FR][CN];
+    // LDS mode: the entries of every level-1 / level-2 row are stored, at fixed rows of the body
+    // (level 1 after odd rows, level 2 after rows 4j + 1), as buffer stores whose lanes without a
+    // target (or rows outside the arrays: ok1 / ok2 false) carry an out-of-range offset and write
+    // nothing -- so every row issues a fixed number of vector memory operations and the waits
+    // before its LDS reads can count them (mb_lds_wait)
+    bool ok1 = false, ok2 = false;
+    const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc((void *)a.g1, 0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs2 = __builtin_amdgcn_make_buffer_rsrc((void *)a.g2, 0, 0x7fffffff, 0x00020000);
+    auto flush_ld = [&](auto PHc) {
+        constexpr int ph = decltype(PHc)::value;
+        constexpr uint32_t none = 0xfffffff0u;
+        if constexpr (ph & 1) {
+#pragma unroll
+            for (int f = 0; f < FR; f++) {
+                const uint32_t ro =
+                    (uint32_t)(f * (kMbNRX * kMbNRY) + mb_g1_at(0, pend1 - kMbRS)) * 8u;
+                typedef unsigned int u2v __attribute__((ext_vector_type(2)));
+                const u2v v = {p1l[f], p1h[f]};
+#pragma unroll
+                for (int k = 0; k < 2; k++)
+                    __builtin_amdgcn_raw_buffer_store_b64(
+                        v, rs1, (ok1 && f < nst && T1.base[k] >= 0) ? o1[k] + ro : none, 0, 0);
+            }
+        }
+        if constexpr (ph % 4 == 1) {
+#pragma unroll
+            for (int f = 0; f < FR; f++) {
+                const uint32_t ro =
+                    (uint32_t)(f * (kMbN2X * kMbN2Y * CN) + mb_g2_at<CN>(0, pend2, 0)) * 4u;
+#pragma unroll
+                for (int q = 0; q < 2; q++) {
+                    const uint32_t off = (ok2 && f < nst && T2.base[q] >= 0) ? o2[q] + ro : none;
+                    mb_buffer_store_ch<CN>(rs2, off, p2[f]);
+                }
+            }
+        }
+    };
     auto flush = [&]() {
         if (pend1 >= 0) {
 #pragma unroll
@@ -1350,7 +1441,12 @@ __device__ __forceinline__ void mb_bands_body(const KMbBandArgs &a, int bi, lds_
         uint32_t gl = (l2 + r2) + 4u * (l1 + r1) + 6u * vl;
         uint32_t gh = (h2_ + s2) + 4u * (h1_ + s1) + 6u * vh;
         const int qy = Y1 + i;
-        if (qy >= 0 && qy < h1 && i >= kMbRS && i < kMbRS + kMbNRY) {
+        if constexpr (LD) {
+            pend1 = i;
+            ok1 = qy >= 0 && qy < h1 && i >= kMbRS && i < kMbRS + kMbNRY;
+            p1l[f] = gl;
+            p1h[f] = gh;
+        } else if (qy >= 0 && qy < h1 && i >= kMbRS && i < kMbRS + kMbNRY) {
             pend1 = i;   // (stored at the next row, see flush)
             p1l[f] = gl;
             p1h[f] = gh;
@@ -1376,7 +1472,11 @@ __device__ __forceinline__ void mb_bands_body(const KMbBandArgs &a, int bi, lds_
 #pragma unroll
             for (int k = 0; k < CN; k++) V2[f][(M3 + 1) % 3][k] += g[k];   // row m - 2 done
             const int e = (i >> 1) - 2, zy = Y2 + e;
-            if (e >= 0 && e < kMbN2Y && zy < h2) {
+            if (LD) {
+                pend2 = e;
+                ok2 = e >= 0 && e < kMbN2Y && zy < h2;
+            }
+            if (LD || (e >= 0 && e < kMbN2Y && zy < h2)) {
                 pend2 = e;
 #pragma unroll
                 for (int k = 0; k < CN; k++) {
@@ -1409,11 +1509,19 @@ __device__ __forceinline__ void mb_bands_body(const KMbBandArgs &a, int bi, lds_
     // LDS mode: group g = the band's source rows 4g .. 4g + 3 (from its first) into ring rows
     // (4g .. 4g + 3) mod kMbLdsRows of every capture's ring, one LDS-DMA instruction per capture
     // (lane = 16-byte chunk, byte offsets in the frame from bgrp); groups 0 .. kMbLdsLead / 4 before
-    // the loop, group r / 4 + kMbLdsLead / 4 + 1 after row r (r % 4 == 0).  The descriptor loads
-    // that follow every group DMA (one per row) make `s_waitcnt vmcnt(kMbLdsWait)` before a row's
-    // LDS reads cover every group the schedule lets that row read.
+    // the loop, group r / 4 + kMbLdsLead / 4 + 1 after row r (r % 4 == 0); descriptor row r + NL
+    // after row r.  No ordinary global load in the loop: `s_waitcnt vmcnt(mb_lds_wait)` before a
+    // row's LDS reads counts the fixed operations issued after everything that row reads.
     const uint32_t *grp = a.bgrp + (int64_t)bi * kMbLdsGroups * kMbBandLanes + l;
-    uint32_t gq = 0;
+    typedef __attribute__((address_space(3))) const uint32_t lu32;
+    lds_u8 *const dring = ring + kMbLdsDescOff;
+    constexpr int NL = kMbLdsDescRing;
+    const uint4 *d16 = a.bdesc16 + (int64_t)bi * kMbLdsDescRows * kMbBandLanes + l;
+    auto issue_desc = [&](int row) {   // descriptor row `row` into ring slot row % NL
+        __builtin_amdgcn_global_load_lds(d16 + row * kMbBandLanes,
+                                         dring + (row % NL) * kMbBandLanes * 16, 16, 0, 0);
+        asm volatile("" ::: "memory");
+    };
     auto issue_group = [&](int g, uint32_t off) {
 #pragma unroll
         for (int f = 0; f < FR; f++)
@@ -1423,12 +1531,17 @@ __device__ __forceinline__ void mb_bands_body(const KMbBandArgs &a, int bi, lds_
         asm volatile("" ::: "memory");   // (the next row's descriptor load stays after the DMAs)
     };
     if constexpr (LD) {
+        uint32_t go[kMbLdsLead / 4 + 1];
 #pragma unroll
-        for (int g = 0; g <= kMbLdsLead / 4; g++) issue_group(g, grp[g * kMbBandLanes]);
-        gq = grp[(kMbLdsLead / 4 + 1) * kMbBandLanes];
+        for (int g = 0; g <= kMbLdsLead / 4; g++) go[g] = grp[g * kMbBandLanes];
+#pragma unroll
+        for (int g = 0; g <= kMbLdsLead / 4; g++) issue_group(g, go[g]);
+#pragma unroll
+        for (int i = 0; i < NL; i++) issue_desc(i);
+    } else {
+#pragma unroll
+        for (int i = 0; i < ND; i++) dq[i] = dsc[i * kMbBandLanes];
     }
-#pragma unroll
-    for (int i = 0; i < ND; i++) dq[i] = dsc[i * kMbBandLanes];
 #pragma unroll
     for (int i = 0; i < A; i++) load_win(dq[i], wq0[i], wq1[i]);
     for (int r12 = 0; r12 < kMbBandRows; r12 += 12) {
@@ -1436,18 +1549,27 @@ __device__ __forceinline__ void mb_bands_body(const KMbBandArgs &a, int bi, lds_
             constexpr int ph = decltype(PHc)::value;
             const int r = r12 + ph;
             constexpr int b0 = ph % NB, bA = (ph + A) % NB, d0 = ph % ND, dA = (ph + A) % ND;
-            uint32_t wa, wb;
-            const uint32_t meta = (uint32_t)(dq[d0] >> 32);
+            uint32_t wa, wb, meta, dxr;
+            if constexpr (LD) {
+                if (ph < NL && r12 == 0)
+                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(mb_lds_wait<FR, NL>(ph, true)) : "memory");
+                else
+                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(mb_lds_wait<FR, NL>(ph, false)) : "memory");
+                const lu32 *dd = (const lu32 *)(dring + (ph % NL) * kMbBandLanes * 16 + l * 16);
+                dxr = dd[0];
+                meta = dd[1];
+            } else {
+                dxr = (uint32_t)dq[d0];
+                meta = (uint32_t)(dq[d0] >> 32);
+            }
             const uint32_t dd = AL ? 0u : (meta >> 12) & 7u;
             mb_weights(meta, wa, wb);
             uint32_t v[FR];
-            if constexpr (LD) asm volatile("s_waitcnt vmcnt(" MCS_STR(MCS_MB_LDS_WAIT) ")" ::: "memory");
 #pragma unroll
             for (int f = 0; f < FR; f++) {
                 uint2 r0, r1;
                 if constexpr (LD) {
-                    typedef __attribute__((address_space(3))) const uint32_t lu32;
-                    const uint32_t dx = (uint32_t)dq[d0], sh = (meta >> 15) & 15u;
+                    const uint32_t dx = dxr, sh = (meta >> 15) & 15u;
                     const lu32 *pa = (const lu32 *)(ring + f * kMbLdsRingBytes + (dx & 0xffffu));
                     const lu32 *pb = (const lu32 *)(ring + f * kMbLdsRingBytes + (dx >> 16));
                     r0 = mb_win_shift<CN>(make_uint3(pa[0], pa[1], pa[2]), sh);
@@ -1466,15 +1588,18 @@ __device__ __forceinline__ void mb_bands_body(const KMbBandArgs &a, int bi, lds_
             }
             // the previous row's finished entries (after this row's window wait), then the loads:
             // windows of row r + A (its descriptor arrived a row ago), descriptor of row r + A + 1
-            flush();
+            if constexpr (LD) flush_ld(PHc);
+            else flush();
             load_win(dq[dA], wq0[bA], wq1[bA]);
             if constexpr (LD) {
                 if constexpr (ph % 4 == 0) {
-                    issue_group(r / 4 + kMbLdsLead / 4 + 1, gq);
-                    gq = grp[(r / 4 + kMbLdsLead / 4 + 2) * kMbBandLanes];
+                    const lu32 *dd = (const lu32 *)(dring + (ph % NL) * kMbBandLanes * 16 + l * 16);
+                    issue_group(r / 4 + kMbLdsLead / 4 + 1, dd[2]);
                 }
+                issue_desc(r + NL);
+            } else {
+                dq[d0] = dsc[(r + ND) * kMbBandLanes];
             }
-            dq[d0] = dsc[(r + ND) * kMbBandLanes];
             // level-0 row r = 2k + (ph & 1), k % 3 = K3; level-1 row k - 2 = 2m + P2, m % 3 = M3
             constexpr int K3 = (ph / 2) % 3;
             constexpr int q = ph / 2 - 2, P2 = q & 1, M3 = ((q - P2) / 2 + 3) % 3;
@@ -1502,7 +1627,7 @@ __device__ __forceinline__ void mb_bands_body(const KMbBandArgs &a, int bi, lds_
             }
         });
     }
-    flush();
+    if constexpr (!LD) flush();   // (LD: the last row stored everything pending)
 }
 
 // The band pass of band bi: the aligned launch (AL) runs bands flagged for the LDS ring (MbBand

@@ -76,6 +76,7 @@ struct mcs_plan {
     int *d_tile_bt = nullptr;
     uint64_t *d_bdesc = nullptr;
     uint32_t *d_bgrp = nullptr;    // LDS-ring band pass: group source offsets (band_lds_tables)
+    uint4 *d_bdesc16 = nullptr;    // LDS-ring band pass: descriptors + group offsets per row
     int n_bands_lds = 0;
     // cylindrical plans: per-column (sin, cos) and per-row h, host copy and device table
     bool cyl = false;
@@ -296,6 +297,7 @@ void band_args(const mcs_plan *p, const mcs::KParams &P, mcs::KMbBandArgs &a)
     a.bands = p->d_bands;
     a.bdesc = p->d_bdesc;
     a.bgrp = p->d_bgrp;
+    a.bdesc16 = p->d_bdesc16;
     a.g1 = p->d_mbg1;
     a.g2 = p->d_mbg2;
     a.slots = p->mb_slots;
@@ -614,7 +616,7 @@ int prepare_bands(const Api *A, mcs_plan *p, const Kernels *k, hipStream_t s)
 // staged for it (16-byte aligned, moved back to end inside the frame), the group table (LDS-DMA
 // source offsets of rows 4g .. 4g + 3 per lane) and the descriptors rewritten to ring offsets.
 // A band takes the ring only when its rows fit the schedule of mb_bands_body: every row's groups
-// issued >= kMbLdsWait rows before it and still resident (rows advancing with the band's rows, at
+// issued >= kMbLdsGLead rows before it and still resident (rows advancing with the band's rows, at
 // most kMbLdsRows in flight); the rest keep the global-window form.  MCS_MB_BAND_LDS=0: none.
 int band_lds_tables(const Api *A, mcs_plan *p, std::vector<mcs::MbBand> &bands, hipStream_t s)
 {
@@ -630,9 +632,11 @@ int band_lds_tables(const Api *A, mcs_plan *p, std::vector<mcs::MbBand> &bands, 
                               hipMemcpyDeviceToHost, s));
     HIP_TRY(A->hipStreamSynchronize(s));
     std::vector<uint32_t> grp(nb * NG * L, 0u);
-    // row r's loop position at which group g is issued (prologue groups: 4 descriptor loads and
-    // the group-offset load follow them before row 0)
-    auto issue = [&](int g) { return g <= D4 ? -4 : 4 * (g - D4 - 1); };
+    const int DL = mcs::kMbLdsDescRows;
+    std::vector<uint4> d16(nb * DL * L, make_uint4(0u, 0u, 0u, 0u));
+    // row r's loop position at which group g is issued (prologue groups: the kMbLdsDescRing
+    // descriptor DMAs of the prologue follow them before row 0)
+    auto issue = [&](int g) { return g <= D4 ? -mcs::kMbLdsDescRing : 4 * (g - D4 - 1); };
     for (size_t i = 0; i < nb; i++) {
         const int slot = bands[i].slot;
         const int w = slot == 0 ? p->kp.cam0_w : p->kp.st[slot - 1].src_w;
@@ -674,7 +678,7 @@ int band_lds_tables(const Api *A, mcs_plan *p, std::vector<mcs::MbBand> &bands, 
             ok = bs[y] >= 0 && (hi[y] < 0 || hi[y] - bs[y] <= SP);
         }
         for (int r = 0; r < R && ok; r++)
-            ok = issue(ghi[r]) <= r - mcs::kMbLdsWait && issue(glo[r] + K / 4) >= r;
+            ok = issue(ghi[r]) <= r - mcs::kMbLdsGLead && issue(glo[r] + K / 4) >= r;
         if (!ok) continue;
         // group table: lane l loads chunk l % 16 of row 4g + l / 16 (rows past the band or the
         // frame: the band's last row, never read)
@@ -697,6 +701,15 @@ int band_lds_tables(const Api *A, mcs_plan *p, std::vector<mcs::MbBand> &bands, 
                 const uint32_t ny = (dy & ~(15u << 15)) | ((uint32_t)(cb & 3) << 15);
                 d[r * L + l] = (uint64_t)(wa | (wb << 16)) | ((uint64_t)ny << 32);
             }
+        // the 16-byte descriptors the kernel stages by LDS-DMA: windows, meta, and on rows
+        // r % 4 == 0 the lane's source offset of the group issued after row r
+        for (int r = 0; r < DL; r++)
+            for (int l = 0; l < L; l++) {
+                const uint64_t v = d[std::min(r, R - 1) * L + l];
+                const int g = r / 4 + D4 + 1;
+                const uint32_t z = (r < R && r % 4 == 0 && g < NG) ? gt[g * L + l] : 0u;
+                d16[(i * DL + r) * L + l] = make_uint4((uint32_t)v, (uint32_t)(v >> 32), z, 0u);
+            }
         bands[i].pad_ |= 1;
         p->n_bands_lds++;
     }
@@ -707,6 +720,9 @@ int band_lds_tables(const Api *A, mcs_plan *p, std::vector<mcs::MbBand> &bands, 
     HIP_TRY(A->hipMemcpyAsync(p->d_bgrp, grp.data(), grp.size() * sizeof(uint32_t),
                               hipMemcpyHostToDevice, s));
     HIP_TRY(A->hipMemcpyAsync(p->d_bdesc, desc.data(), desc.size() * sizeof(uint64_t),
+                              hipMemcpyHostToDevice, s));
+    HIP_TRY(A->hipMalloc((void **)&p->d_bdesc16, d16.size() * sizeof(uint4)));
+    HIP_TRY(A->hipMemcpyAsync(p->d_bdesc16, d16.data(), d16.size() * sizeof(uint4),
                               hipMemcpyHostToDevice, s));
     HIP_TRY(A->hipMemcpyAsync(p->d_bands, bands.data(), nb * sizeof(mcs::MbBand),
                               hipMemcpyHostToDevice, s));
@@ -817,9 +833,11 @@ void release_tables(const Api *A, mcs_plan *p)
                     (void *)p->d_owner, (void *)p->d_binfo, (void *)p->d_blist,
                     (void *)p->d_mbdesc, (void *)p->d_mbtab, (void *)p->d_mbfoot, (void *)p->d_mbg1,
                     (void *)p->d_mbg2, (void *)p->d_bands, (void *)p->d_tile_bt,
-                    (void *)p->d_bdesc, (void *)p->d_bgrp, (void *)p->d_order})
+                    (void *)p->d_bdesc, (void *)p->d_bgrp, (void *)p->d_bdesc16,
+                    (void *)p->d_order})
         if (q) (void)A->hipFree(q);
     p->d_bgrp = nullptr;
+    p->d_bdesc16 = nullptr;
     p->n_bands_lds = 0;
     p->d_order = nullptr;
     p->n_early = p->n_list = 0;

@@ -271,19 +271,36 @@ constexpr int kMbBandStride = 52;  // window step: consecutive windows' level-2 
 #endif
 constexpr int kMbBandFrames = MCS_MB_BAND_FRAMES;
 // LDS-ring band pass (mb_bands_body mode 2): per capture a ring of kMbLdsRows source rows of
-// kMbLdsSpan bytes each; groups of 4 rows, kMbLdsLead rows loaded before the first row;
-// `s_waitcnt vmcnt(MCS_MB_LDS_WAIT)` before each row's LDS reads
+// kMbLdsSpan bytes each; groups of 4 rows, kMbLdsLead rows loaded before the first row; counted
+// vmcnt waits before each row's LDS reads (mb_lds_wait)
 #define MCS_STR_(x) #x
 #define MCS_STR(x) MCS_STR_(x)
-#ifndef MCS_MB_LDS_WAIT
-#define MCS_MB_LDS_WAIT 2
+#ifndef MCS_MB_LDS_DESC
+#define MCS_MB_LDS_DESC 3
+#endif
+#ifndef MCS_MB_LDS_GLEAD
+#define MCS_MB_LDS_GLEAD 3
 #endif
 constexpr int kMbLdsSpan = 256;
-constexpr int kMbLdsRows = 20;
-constexpr int kMbLdsLead = 8;
-constexpr int kMbLdsWait = MCS_MB_LDS_WAIT;
+#ifndef MCS_MB_LDS_ROWS
+#define MCS_MB_LDS_ROWS 16
+#endif
+#ifndef MCS_MB_LDS_LEAD
+#define MCS_MB_LDS_LEAD 4
+#endif
+constexpr int kMbLdsRows = MCS_MB_LDS_ROWS;
+constexpr int kMbLdsLead = MCS_MB_LDS_LEAD;
+constexpr int kMbLdsGLead = MCS_MB_LDS_GLEAD;   // rows between a group's DMA and its first reader
 constexpr int kMbLdsRingBytes = kMbLdsRows * kMbLdsSpan;
-constexpr int kMbLdsBytes = kMbBandFrames * kMbLdsRingBytes + 16;   // (+ the last window's tail)
+// per wave: the captures' rings, then the descriptor ring (kMbLdsDescRing rows of 16 B per
+// lane: the descriptor of row r + kMbLdsDescRing is staged after row r, so the kMbLdsDescRing - 1
+// descriptor DMAs after it bound the wait)
+constexpr int kMbLdsDescRing = MCS_MB_LDS_DESC;
+constexpr int kMbLdsDescRows = kMbBandRows + kMbLdsDescRing;
+constexpr int kMbLdsDescOff = kMbBandFrames * kMbLdsRingBytes;
+constexpr int kMbLdsBytes = kMbLdsDescOff + kMbLdsDescRing * kMbBandLanes * 16 + 16;
+static_assert(12 % kMbLdsDescRing == 0 && kMbLdsGLead >= 1 && kMbLdsGLead <= kMbLdsDescRing,
+              "LDS band ring: descriptor ring divides the 12-row body; groups led by <= its rows");
 constexpr int kMbLdsGroups = kMbBandRows / 4 + kMbLdsLead / 4 + 3;  // group offsets per band
 static_assert(kMbLdsRows % 4 == 0 && kMbLdsLead % 4 == 0 && kMbLdsRows / 4 > kMbLdsLead / 4 + 1,
               "LDS band ring: whole groups, the prologue's groups never evicted by the loop's first");
@@ -296,6 +313,7 @@ struct KMbBandArgs {
     uint16_t *g1;                  // scratch, as KMbArgs
     int32_t *g2;
     const uint32_t *bgrp;          // [bands][kMbLdsGroups][kMbBandLanes] LDS-ring group offsets
+    const uint4 *bdesc16;          // [bands][kMbLdsDescRows][kMbBandLanes] LDS-ring descriptors
     int slots, chunk, f0, nf;
     int gxb;                       // blend tiles per mosaic row
     int band0;                     // first band of this launch
