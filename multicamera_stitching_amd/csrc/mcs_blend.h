@@ -1636,7 +1636,11 @@ template <int CN, int FR, bool BR, bool AL>
 __device__ __forceinline__ void mb_bands(const KMbBandArgs &a, int bi, lds_u8 *ring)
 {
     if constexpr (AL) {
-        if (__builtin_amdgcn_readfirstlane(a.bands[bi].pad_) & 1) mb_bands_body<CN, FR, BR, 2>(a, bi, ring);
+        const int lds = __builtin_amdgcn_readfirstlane(a.bands[bi].pad_) & 1;
+#ifdef MCS_EXP_BAND_SKIP   // (timing experiments only: 1 = skip the global-window bands, 2 = the LDS ones)
+        if (MCS_EXP_BAND_SKIP == (lds ? 2 : 1)) return;
+#endif
+        if (lds) mb_bands_body<CN, FR, BR, 2>(a, bi, ring);
         else mb_bands_body<CN, FR, BR, 1>(a, bi, ring);
     } else {
         mb_bands_body<CN, FR, BR, 0>(a, bi, ring);
