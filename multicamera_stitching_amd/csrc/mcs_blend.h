@@ -1522,12 +1522,19 @@ __device__ __forceinline__ void mb_bands_body(const KMbBandArgs &a, int bi, lds_
                                          dring + (row % NL) * kMbBandLanes * 16, 16, 0, 0);
         asm volatile("" ::: "memory");
     };
+    // (one buffer resource per capture frame: the chunks a row's samples do not read carry an
+    // out-of-range offset and fetch nothing, while the instruction count stays fixed)
+    __amdgpu_buffer_rsrc_t rsf[FR];
+#pragma unroll
+    for (int f = 0; f < FR; f++)
+        rsf[f] = __builtin_amdgcn_make_buffer_rsrc((void *)fb[f], 0, (int)(pitch * (uint32_t)h),
+                                                   0x00020000);
     auto issue_group = [&](int g, uint32_t off) {
 #pragma unroll
         for (int f = 0; f < FR; f++)
-            __builtin_amdgcn_global_load_lds(fb[f] + off,
-                                             ring + f * kMbLdsRingBytes + ((4 * g) % kMbLdsRows) * kMbLdsSpan,
-                                             16, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                rsf[f], ring + f * kMbLdsRingBytes + ((4 * g) % kMbLdsRows) * kMbLdsSpan, 16, off, 0,
+                0, 0);
         asm volatile("" ::: "memory");   // (the next row's descriptor load stays after the DMAs)
     };
     if constexpr (LD) {

@@ -680,13 +680,16 @@ int band_lds_tables(const Api *A, mcs_plan *p, std::vector<mcs::MbBand> &bands, 
         for (int r = 0; r < R && ok; r++)
             ok = issue(ghi[r]) <= r - mcs::kMbLdsGLead && issue(glo[r] + K / 4) >= r;
         if (!ok) continue;
-        // group table: lane l loads chunk l % 16 of row 4g + l / 16 (rows past the band or the
-        // frame: the band's last row, never read)
+        // group table: lane l loads chunk l % 16 of row 4g + l / 16; chunks no sample of the row
+        // reads, rows no sample reads and rows past the band: an offset past the frame (the
+        // kernel's buffer load fetches nothing for them)
         uint32_t *gt = grp.data() + i * NG * L;
         for (int g = 0; g < NG; g++)
             for (int l = 0; l < L; l++) {
-                const int y = std::min(4 * g + l / 16, nr - 1);
-                gt[g * L + l] = (uint32_t)((int64_t)(y0 + y) * pitch + bs[y] + 16 * (l % 16));
+                const int y = 4 * g + l / 16, c = l % 16;
+                const bool need = y < nr && hi[y] >= 0 && 16 * c < hi[y] - bs[y];
+                gt[g * L + l] = need ? (uint32_t)((int64_t)(y0 + y) * pitch + bs[y] + 16 * c)
+                                     : 0xfffffff0u;
             }
         // descriptors: .x = ring offsets of the tap-a / tap-b windows (4-byte aligned), .y keeps
         // the weights and takes the window shift sh = tap byte & 3
