@@ -1994,11 +1994,12 @@ int mcs_plan_stats(const mcs_plan *p, int64_t *stats, int n)
 {
     if (!p || !stats) return mcs::fail(MCS_E_INVALID, "NULL plan/stats");
     const int64_t tiles = (int64_t)p->gx * p->gy;
-    const int64_t v[9] = {p->prepared ? 1 : 0, tiles, tiles - p->n_fallback, p->n_fallback,
-                          tiles * (int64_t)(sizeof(mcs::TileHdr) +
-                                            mcs::kTilePx * (mcs::kDescWords + 1) * 4),
-                          p->blend, p->n_blend, p->mb_slots, p->n_degraded};
-    for (int i = 0; i < n; i++) stats[i] = i < 9 ? v[i] : 0;
+    const int64_t v[11] = {p->prepared ? 1 : 0, tiles, tiles - p->n_fallback, p->n_fallback,
+                           tiles * (int64_t)(sizeof(mcs::TileHdr) +
+                                             mcs::kTilePx * (mcs::kDescWords + 1) * 4),
+                           p->blend, p->n_blend, p->mb_slots, p->n_degraded, p->n_bands,
+                           p->n_bands_lds};
+    for (int i = 0; i < n; i++) stats[i] = i < 11 ? v[i] : 0;
     return MCS_OK;
 }
 

@@ -39,6 +39,7 @@ def _diff(a, b):
     dict(n=3, w=180, h=100, ch=3, seed=7, super_mode=True, rot_deg=3.0),
     dict(n=2, w=40, h=20, ch=2, seed=8, overlap=0.5),
     dict(n=4, w=64, h=48, ch=3, seed=10, overlap=0.8),     # seams 13 px apart: 3-4 owners/tile
+    dict(n=3, w=202, h=110, ch=3, seed=13),   # rows of 606 B: the band pass's unaligned windows
 ])
 def test_blend_vs_oracle(mode, case):
     case = dict(case)
@@ -70,6 +71,10 @@ def test_multiband_c2_full_size_batch():
     for f in (0, F - 1):
         want = oracle.blend_stitch(plan.describe(), shots[f], MODES["multiband"])
         assert _diff(got[f].reshape(want.shape), want) == 0
+    # both window forms of the band pass ran in this launch: most bands on the LDS ring, the
+    # bands with reflected rows (top / bottom mosaic edge) on dword-aligned global windows
+    st = plan.stats()
+    assert 0 < st["mb_bands_lds"] < st["mb_bands"], st
 
 
 @pytest.mark.parametrize("F", [64, 70])
