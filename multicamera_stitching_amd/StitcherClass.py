@@ -176,6 +176,8 @@ class Stitcher(_Transient, Debugger):
                           "SIFT or the mcs feature kernels); pass homographies=",
                           log_type="err")
             return
+        if homographies is None:
+            _note_orb_fallback(self)
         img_result = None
         for idx, _ in enumerate(self.img_labels[:-1]):
             images = (images_dic[self.img_labels[idx]] if idx == 0 else img_result,
@@ -433,13 +435,40 @@ def _conform_cameras(owner, chain, cams):
     return cams, cam0_hw, sizes
 
 
+_orb_noted = False
+
+
+def _note_orb_fallback(owner):
+    """The reference calibrates with SIFT and refuses to run without OpenCV contrib
+    (StitcherClass.py:87-93 logs "OpenCV is not a contrib version ..." and returns).  Where SIFT
+    is absent the drop-in calibrates with the GPU ORB + Hamming + RANSAC path instead (SURVEY.md
+    8 NS-3..5), whose homographies are not SIFT's: said once per process, at the reference's
+    guard."""
+    global _orb_noted
+    from . import features
+    if _orb_noted or features.backend() != "orb":
+        return
+    _orb_noted = True
+    why = ("MCS_FEATURES=orb" if os.environ.get("MCS_FEATURES", "auto").lower() == "orb" else
+           "OpenCV is not a contrib version (no xfeatures2d SIFT)")
+    owner.debugger(DEBUG_LEVEL_0, "[STITCHER] {}: calibrating with GPU ORB features and "
+                   "Hamming matching instead of SIFT; the homographies differ from the "
+                   "reference's".format(why), log_type="warn")
+
+
+# C-ABI statuses of run-time failures (include/mcs.h), the only ones _run_chain turns into a
+# logged fallback image
+_RUNTIME_FAILURES = (-2, -3)   # MCS_E_HIP, MCS_E_NOMEM
+
+
 def _run_chain(owner, chain, cams, fallback):
     """One GPU stitch of the chain.  The reference never raises on an expected failure: it logs
     and returns a fallback image (:126-128 the last camera's image, :255-256 B).  A failure of
-    the GPU path (a C-ABI status, e.g. a device allocation that fails) is logged the same way and
-    `fallback` is returned -- the caller's thread (Qt GUI / worker) gets an image, never an
-    exception, and the log says why.  (There is no CPU stitch behind it: a missing libmcs.so
-    fails at import.)"""
+    the GPU path at run time (MCS_E_HIP, MCS_E_NOMEM: a device allocation or launch that fails) is
+    logged the same way and `fallback` is returned -- the caller's thread (Qt GUI / worker) gets
+    an image, never an exception, and the log says why.  Argument and programming errors
+    (MCS_E_INVALID, MCS_E_SHAPE, MCS_E_UNSUPPORTED) are raised: the reference has no catch for
+    them either.  (There is no CPU stitch behind it: a missing libmcs.so fails at import.)"""
     cams, cam0_hw, sizes = _conform_cameras(owner, chain, cams)
     cache = owner._cache()
     with cache.lock:
@@ -455,6 +484,8 @@ def _run_chain(owner, chain, cams, fallback):
                                    "blend".format(dense), log_type="warn")
             return out
         except _capi.McsError as e:
+            if e.code not in _RUNTIME_FAILURES:
+                raise
             cache.key = cache.plan = None     # rebuilt on the next call
             owner.debugger(DEBUG_LEVEL_0, "[STITCHER] GPU stitch failed ({}); returning the "
                            "fallback image".format(e), log_type="err")
@@ -499,12 +530,32 @@ class _StitcherUnpickler(pickle.Unpickler):
         super().__init__(f, encoding="latin1")
 
     def find_class(self, module, name):
+        """Only the globals a Stitcher_config.pkl holds (StitcherClass.py:138-177: the two
+        classes, their Debugger base, numpy arrays / scalars / dtypes and the copy_reg
+        reconstructor Python 2 writes for them); anything else -- os.system, eval, ... -- is
+        refused, so loading a pickle never runs code it names."""
         if module in ("StitcherClass", __name__, "__main__") and name in ("Stitcher",
                                                                            "StitcherBase"):
             return globals()[name]
         if module == "extended_rospylogs" and name == "Debugger":
             return Debugger
-        return super().find_class(module, name)
+        if (module, name) in _PICKLE_ALLOWED:
+            return super().find_class(module, name)
+        raise pickle.UnpicklingError(
+            "Stitcher_config.pkl names {}.{}, which a stitcher pickle never holds".format(module,
+                                                                                      name))
+
+
+# (module, name) pairs a legacy or re-saved stitcher pickle may name besides the classes above:
+# numpy's array / scalar / dtype reconstructors (numpy 1.x "core" and 2.x "_core" paths) and the
+# Python 2 copy_reg protocol-0/2 object reconstruction.
+_PICKLE_ALLOWED = frozenset(
+    [("numpy", "ndarray"), ("numpy", "dtype")] +
+    [(m + ".multiarray", n) for m in ("numpy.core", "numpy._core")
+     for n in ("_reconstruct", "scalar")] +
+    [(m + ".numeric", "_frombuffer") for m in ("numpy.core", "numpy._core")] +
+    [("copy_reg", "_reconstructor"), ("copyreg", "_reconstructor"),
+     ("__builtin__", "object"), ("builtins", "object")])
 
 
 # Pickles name the reference module so either side can read them.

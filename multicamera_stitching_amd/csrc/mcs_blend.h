@@ -1173,14 +1173,9 @@ __device__ __forceinline__ void mb_target(const KMbBandArgs &a, int s, int row, 
 // the reduces computed there are the reflected entries (reflect-101 about 0 commutes with the
 // 2x decimation).  At the bottom / right edges it does not (for even level sizes), so BR units
 // give level 2 the reflected level-1 rows (a history of four) and columns (source lanes).
-// This block's band of the launch (KMbBandArgs::xcd), -1 past the launch's bands.
-__device__ __forceinline__ int mb_band_of_block(const KMbBandArgs &a)
-{
-    if (a.xcd <= 0) return (int)blockIdx.x;
-    const int per = (a.xcd + 7) >> 3;
-    const int i = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
-    return i < a.xcd ? i : -1;
-}
+// This block's band of the launch (block x = band x: consecutive bands round-robin over the 8
+// XCDs; an XCD-contiguous mapping measured within noise, round 3).
+__device__ __forceinline__ int mb_band_of_block(const KMbBandArgs &a) { return (int)blockIdx.x; }
 
 // CN consecutive ints by one buffer store (offset past the range: nothing written).
 template <int CN>

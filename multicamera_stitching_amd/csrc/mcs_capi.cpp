@@ -65,13 +65,6 @@ struct mcs_plan {
     // multi-band band pass: bands (the first n_bands_in reach no bottom / right mosaic edge),
     // blend-tile grid -> list index, descriptors; without bands mb_levels computes the levels
     int n_bands = 0, n_bands_in = 0, gxb = 0;
-    // the band pass and blend in row chunks (prepare_bands): chunk c = interior bands [i0, i1),
-    // edge bands [b0, b1), blend list entries [l0, l1) -- the blend of chunk c needs only the
-    // bands of its tile rows, so it runs beside the next chunk's bands
-    struct MbChunk { int i0, i1, b0, b1, l0, l1; };
-    std::vector<MbChunk> mb_chunks;
-    hipStream_t side3 = nullptr;
-    std::vector<hipEvent_t> ev_band;
     mcs::MbBand *d_bands = nullptr;
     int *d_tile_bt = nullptr;
     uint64_t *d_bdesc = nullptr;
@@ -256,8 +249,7 @@ bool stream_base(const mcs_plan *p, const mcs::KParams &kp, int n_frames, const 
         lo = a < lo ? a : lo;
         hi = e > hi ? e : hi;
     }
-    static const bool off = getenv("MCS_STREAM_B32") && strcmp(getenv("MCS_STREAM_B32"), "0") == 0;
-    const bool b32 = !off && !g_force_off64 && lo <= hi && hi - lo < (uintptr_t(1) << 32);
+    const bool b32 = !g_force_off64 && lo <= hi && hi - lo < (uintptr_t(1) << 32);
     *base = b32 ? (const uint8_t *)lo : kp.base;
     return b32;
 }
@@ -309,17 +301,13 @@ void band_args(const mcs_plan *p, const mcs::KParams &P, mcs::KMbBandArgs &a)
     a.n_in = p->n_bands_in;
     a.band1 = p->n_bands_in;
     a.pad_ = 0;
-    a.xcd = 0;
 }
 
 // The band pass's dword-aligned window form (mb_bands AL, mb_desc's sh) applies when every used
 // camera's rows and frames are multiples of 4 bytes, its frames start at 4-byte boundaries and hold
-// at least pitch + 12 bytes.  MCS_MB_BAND_ALIGNED=0 (experiments): the unaligned 8-byte form.
+// at least pitch + 12 bytes; otherwise the unaligned 8-byte form.
 int band_form(const mcs_plan *p, const mcs::KParams &P)
 {
-    static const bool off =
-        getenv("MCS_MB_BAND_ALIGNED") && !strcmp(getenv("MCS_MB_BAND_ALIGNED"), "0");
-    if (off) return 0;
     bool need[MCS_MAX_CAMS];
     need_mask(p->fd, need);
     const int C = p->fd.channels;
@@ -333,71 +321,15 @@ int band_form(const mcs_plan *p, const mcs::KParams &P)
     return 1;
 }
 
-// Grid width of a band launch of n bands (XCD-contiguous mapping: padded to a multiple of 8).
-// MCS_MB_BAND_XCD=0 / 1: the mapping (KMbBandArgs::xcd; default 0 -- measured within noise,
-// multi-band launch 0.963 ms either way).
-unsigned band_grid(mcs::KMbBandArgs &b, int n)
-{
-    static const bool xcd = getenv("MCS_MB_BAND_XCD") && strcmp(getenv("MCS_MB_BAND_XCD"), "0");
-    b.xcd = xcd ? n : 0;
-    return xcd ? 8u * (((unsigned)n + 7u) / 8u) : (unsigned)n;
-}
-
-// Order of the streaming tiles in a launch list.  stream_tile deals a list to the 8 XCDs in
-// contiguous slices (XCD x: entries [x * per, (x + 1) * per)), each walked in list order, so the
-// order decides which tiles share an XCD's L2 at the same time.  MCS_STREAM_ORDER=0: row-major
-// (an XCD holds a band of whole tile rows: horizontal neighbours together, vertical ones only
-// at the band's concurrent rows); 1 (experiment): 8 vertical strips of ceil(gx / 8) tile
-// columns, each walked row by row (an XCD's resident blocks are ~16 vertically adjacent rows of
-// its strip).  Measured (same box, two alternations): strips are slower -- paste launch 0.610 ->
-// 0.627-0.639 ms, multi-band 0.972 -> 0.977 ms: the 16-byte chunk rounding at both ends of every
-// footprint row makes horizontal neighbours share more L2 lines than vertical ones share rows.
-int stream_order_mode()
-{
-    static const int mode = getenv("MCS_STREAM_ORDER") ? atoi(getenv("MCS_STREAM_ORDER")) : 0;
-    return mode;
-}
-
-void order_tiles(const mcs_plan *p, std::vector<int> &v)
-{
-    if (stream_order_mode() != 1) return;   // (lists are built row-major)
-    const int sw = (p->gx + 7) / 8;
-    std::stable_sort(v.begin(), v.end(), [&](int a, int b) {
-        const int ax = a % p->gx, ay = a / p->gx, bx = b % p->gx, by = b / p->gx;
-        if (ax / sw != bx / sw) return ax / sw < bx / sw;
-        return ay != by ? ay < by : ax < bx;
-    });
-}
-
-// Launch list of the streaming kernel for tiles in launch order (stream_tile deals a list to the
-// 8 XCDs in equal contiguous slices, each walked in order): per slice, the last MCS_STREAM_TAIL
-// tiles (experiment knob, default 0 = off) become 4 items of a quarter of the captures each,
-// ordered part by part, so the blocks that start last on an XCD finish a quarter as long after
-// the others; slices padded to one length with -1.  Measured (same box, two alternations): 96
-// tail tiles per XCD -- paste within noise (0.596 vs 0.596 ms), multi-band 2-3 % slower (0.947
-// -> 0.978 ms: its early list, split too, runs longer); 48 -- paste -0.8 %, multi-band +2 %.
+// Launch list of the streaming kernel for tiles in launch order: stream_tile deals a list to the
+// 8 XCDs in equal contiguous slices (XCD x: entries [x * per, (x + 1) * per)), each walked in
+// order, so an XCD holds a band of whole tile rows (horizontal neighbours share its L2; measured
+// faster than vertical strips, round 3); slices padded to one length with -1.
 std::vector<int> launch_list(const std::vector<int> &tiles)
 {
-    static const int tail = getenv("MCS_STREAM_TAIL") ? atoi(getenv("MCS_STREAM_TAIL")) : 0;
     const size_t n = tiles.size(), per = (n + 7) / 8;
-    std::vector<std::vector<int>> sl(8);
-    for (size_t x = 0; x < 8; x++) {
-        const size_t b = std::min(n, x * per), e = std::min(n, (x + 1) * per);
-        const size_t k = std::min(e - b, (size_t)std::max(tail, 0));
-        for (size_t i = b; i < e - k; i++) sl[x].push_back(tiles[i]);
-        for (int part = 0; part < 4 && k > 0; part++)
-            for (size_t i = e - k; i < e; i++)
-                sl[x].push_back(tiles[i] | (part << mcs::kItemPartShift) |
-                                (2 << mcs::kItemLogShift));
-    }
-    size_t len = 0;
-    for (auto &v : sl) len = std::max(len, v.size());
-    std::vector<int> out;
-    out.reserve(8 * len);
-    for (auto &v : sl) {
-        v.resize(len, -1);
-        out.insert(out.end(), v.begin(), v.end());
-    }
+    std::vector<int> out(8 * per, -1);
+    for (size_t i = 0; i < n; i++) out[i] = tiles[i];
     return out;
 }
 
@@ -449,9 +381,6 @@ int prepare_bands(const Api *A, mcs_plan *p, const Kernels *k, hipStream_t s)
         for (int j = 0; m; j++, m &= m - 1) {
             const int slot = __builtin_ctz(m);
             Need q{c[4 * j], c[4 * j + 1], c[4 * j + 2], c[4 * j + 3]};
-            if (getenv("MCS_DEBUG_BANDS"))
-                fprintf(stderr, "tile %d slot %d q1 [%d, %d] z2 [%d, %d]\n", t, slot, q.q1lo,
-                        q.q1hi, q.z2lo, q.z2hi);
             if (q.q1lo > q.q1hi && q.z2lo > q.z2hi) continue;
             need[(size_t)slot * gyb + Y0 / mcs::kBlendTileH].push_back(q);
         }
@@ -499,9 +428,6 @@ int prepare_bands(const Api *A, mcs_plan *p, const Kernels *k, hipStream_t s)
                 }
             }
         }
-    if (getenv("MCS_DEBUG_BANDS"))
-        for (const mcs::MbBand &b : bands)
-            fprintf(stderr, "band slot %d row %d c0 %d\n", b.slot, b.row, b.c0);
     if (bands.empty()) return MCS_OK;
     {
         // streaming tiles under the blend tiles that have mixed pixels: launched first, so the
@@ -520,8 +446,6 @@ int prepare_bands(const Api *A, mcs_plan *p, const Kernels *k, hipStream_t s)
         std::vector<int> first, late;
         for (size_t t = 0; t < early.size(); t++)
             (early[t] ? first : late).push_back((int)t);
-        order_tiles(p, first);
-        order_tiles(p, late);
         std::vector<int> order = launch_list(first);
         p->n_early = (int)order.size();
         const std::vector<int> rest = launch_list(late);
@@ -537,53 +461,11 @@ int prepare_bands(const Api *A, mcs_plan *p, const Kernels *k, hipStream_t s)
         return b.row * mcs::kBlendTileH - mcs::kBlendHalo + mcs::kMbFirst + mcs::kMbUsedY > H ||
                b.c0 + mcs::kMbBandLanes > W;
     };
-    static const bool sort_on = !getenv("MCS_MB_SORT") || strcmp(getenv("MCS_MB_SORT"), "0");
-    if (sort_on)
-        std::stable_sort(bands.begin(), bands.end(),
-                         [](const mcs::MbBand &a, const mcs::MbBand &b) { return a.row < b.row; });
+    std::stable_sort(bands.begin(), bands.end(),
+                     [](const mcs::MbBand &a, const mcs::MbBand &b) { return a.row < b.row; });
     std::stable_partition(bands.begin(), bands.end(), [&](const mcs::MbBand &b) { return !br(b); });
     p->n_bands_in = (int)(std::find_if(bands.begin(), bands.end(), br) - bands.begin());
     const size_t nb = bands.size();
-    {
-        // row chunks with about equal numbers of blend tiles (MCS_MB_ROW_CHUNKS; default 1 = one
-        // band launch, one blend launch.  Measured, same box, two alternations: C2 2 / 3 chunks
-        // 0.954 / 0.950 ms vs 0.956-0.961 unchunked -- noise --, 4 / 6 chunks 1.00-1.03 ms; C4 3
-        // chunks 1.559 vs 1.523 ms: the launch is bound by the passes' contention with the
-        // streaming kernel, not by the band -> blend order)
-        static const int want = getenv("MCS_MB_ROW_CHUNKS") ? atoi(getenv("MCS_MB_ROW_CHUNKS"))
-                                                            : 1;
-        const int K = std::max(1, std::min(want, n));
-        std::vector<int> row_end;   // first tile row past each chunk
-        for (int c = 1; c < K; c++) {
-            const int i = (int)((int64_t)n * c / K);
-            row_end.push_back(list[1 + 2 * i] / p->gxb);
-        }
-        row_end.push_back(gyb);
-        p->mb_chunks.clear();
-        int r0 = 0;
-        for (int r1 : row_end) {
-            if (r1 <= r0) continue;
-            mcs_plan::MbChunk ch{};
-            auto in_rows = [&](int row) { return row >= r0 && row < r1; };
-            ch.i0 = ch.i1 = ch.b0 = ch.b1 = ch.l0 = ch.l1 = -1;
-            for (int i = 0; i < (int)nb; i++) {
-                if (!in_rows(bands[i].row)) continue;
-                int &lo = i < p->n_bands_in ? ch.i0 : ch.b0, &hi = i < p->n_bands_in ? ch.i1 : ch.b1;
-                if (lo < 0) lo = i;
-                hi = i + 1;
-            }
-            for (int i = 0; i < n; i++) {
-                if (!in_rows(list[1 + 2 * i] / p->gxb)) continue;
-                if (ch.l0 < 0) ch.l0 = i;
-                ch.l1 = i + 1;
-            }
-            if (ch.i0 < 0) ch.i0 = ch.i1 = 0;
-            if (ch.b0 < 0) ch.b0 = ch.b1 = p->n_bands_in;
-            if (ch.l0 < 0) ch.l0 = ch.l1 = 0;
-            p->mb_chunks.push_back(ch);
-            r0 = r1;
-        }
-    }
     HIP_TRY(A->hipMalloc((void **)&p->d_bands, nb * sizeof(mcs::MbBand)));
     HIP_TRY(A->hipMalloc((void **)&p->d_tile_bt, tile_bt.size() * sizeof(int)));
     HIP_TRY(A->hipMalloc((void **)&p->d_bdesc,
@@ -617,16 +499,14 @@ int prepare_bands(const Api *A, mcs_plan *p, const Kernels *k, hipStream_t s)
 // source offsets of rows 4g .. 4g + 3 per lane) and the descriptors rewritten to ring offsets.
 // A band takes the ring only when its rows fit the schedule of mb_bands_body: every row's groups
 // issued >= kMbLdsGLead rows before it and still resident (rows advancing with the band's rows, at
-// most kMbLdsRows in flight); the rest keep the global-window form.  MCS_MB_BAND_LDS=0: none.
+// most kMbLdsRows in flight); the rest keep the global-window form.
 int band_lds_tables(const Api *A, mcs_plan *p, std::vector<mcs::MbBand> &bands, hipStream_t s)
 {
-    static const bool off = getenv("MCS_MB_BAND_LDS") && !strcmp(getenv("MCS_MB_BAND_LDS"), "0");
     const size_t nb = bands.size();
     const int C = p->fd.channels, R = mcs::kMbBandRows, DR = mcs::kMbBandDescRows;
     const int L = mcs::kMbBandLanes, NG = mcs::kMbLdsGroups, K = mcs::kMbLdsRows;
     const int SP = mcs::kMbLdsSpan, D4 = mcs::kMbLdsLead / 4;
     p->n_bands_lds = 0;
-    if (off) return MCS_OK;
     std::vector<uint64_t> desc(nb * DR * L);
     HIP_TRY(A->hipMemcpyAsync(desc.data(), p->d_bdesc, desc.size() * sizeof(uint64_t),
                               hipMemcpyDeviceToHost, s));
@@ -716,14 +596,13 @@ int band_lds_tables(const Api *A, mcs_plan *p, std::vector<mcs::MbBand> &bands, 
         bands[i].pad_ |= 1;
         p->n_bands_lds++;
     }
-    if (getenv("MCS_DEBUG_BANDS"))
-        fprintf(stderr, "bands %zu, LDS-ring form %d\n", nb, p->n_bands_lds);
     if (p->n_bands_lds == 0) return MCS_OK;
     HIP_TRY(A->hipMalloc((void **)&p->d_bgrp, grp.size() * sizeof(uint32_t)));
     HIP_TRY(A->hipMemcpyAsync(p->d_bgrp, grp.data(), grp.size() * sizeof(uint32_t),
                               hipMemcpyHostToDevice, s));
-    HIP_TRY(A->hipMemcpyAsync(p->d_bdesc, desc.data(), desc.size() * sizeof(uint64_t),
-                              hipMemcpyHostToDevice, s));
+    // (d_bdesc keeps the frame-offset descriptors: the ring offsets live only in d_bdesc16, so
+    // a launch that takes the unaligned form -- band_form() == 0, decided per launch from the
+    // frame pointers and strides -- reads valid descriptors for every band)
     HIP_TRY(A->hipMalloc((void **)&p->d_bdesc16, d16.size() * sizeof(uint4)));
     HIP_TRY(A->hipMemcpyAsync(p->d_bdesc16, d16.data(), d16.size() * sizeof(uint4),
                               hipMemcpyHostToDevice, s));
@@ -763,8 +642,7 @@ int prepare_multiband(const Api *A, mcs_plan *p, const Kernels *k, hipStream_t s
     const int rc = launch_args(A, k->mb_prep[C][p->fd.interp], (unsigned)n, 1,
                                mcs::kMbPrepThreads, 1, &a, sizeof(a), s);
     if (rc) return rc;
-    static const bool bands_on = !getenv("MCS_MB_BANDS") || strcmp(getenv("MCS_MB_BANDS"), "0");
-    return bands_on ? prepare_bands(A, p, k, s) : MCS_OK;
+    return prepare_bands(A, p, k, s);
 }
 
 // Blended modes: the owner map and the list of 32-px tiles the blend kernels recompute.
@@ -798,10 +676,8 @@ int prepare_blend(const Api *A, mcs_plan *p, const Kernels *k, hipStream_t s)
     HIP_TRY(A->hipStreamSynchronize(s));
     // tail[0]: multi-band tiles with more than kBlendSlots owners (degraded to the feather rule),
     // tail[2]: those of them with pixels to feather (listed in d_dense)
-    static const bool sort_on = !getenv("MCS_MB_SORT") || strcmp(getenv("MCS_MB_SORT"), "0");
-    if (n > 1 && sort_on) {
-        // the list in tile order (classify appends in arrival order): the multi-band passes
-        // walk it in row chunks
+    if (n > 1) {
+        // the list in tile order (classify appends in arrival order)
         std::vector<int> l(1 + 2 * (size_t)n);
         HIP_TRY(A->hipMemcpyAsync(l.data(), p->d_blist, l.size() * sizeof(int),
                                   hipMemcpyDeviceToHost, s));
@@ -829,8 +705,6 @@ void release_tables(const Api *A, mcs_plan *p)
     if (p->stream) (void)A->hipStreamSynchronize(p->stream);
     if (p->side) (void)A->hipStreamSynchronize(p->side);
     if (p->side2) (void)A->hipStreamSynchronize(p->side2);
-    if (p->side3) (void)A->hipStreamSynchronize(p->side3);
-    p->mb_chunks.clear();
     for (void *q : {(void *)p->d_tiles, (void *)p->d_desc, (void *)p->d_desc4,
                     (void *)p->d_fallback,
                     (void *)p->d_owner, (void *)p->d_binfo, (void *)p->d_blist,
@@ -931,7 +805,6 @@ int prepare(const Api *A, mcs_plan *p, hipStream_t s)
         // one launch list of every tile (the multi-band split builds its own, early tiles first)
         std::vector<int> tl(tiles);
         for (size_t t = 0; t < tiles; t++) tl[t] = (int)t;
-        order_tiles(p, tl);
         const std::vector<int> order = launch_list(tl);
         HIP_TRY(A->hipMalloc((void **)&p->d_order, order.size() * sizeof(int)));
         HIP_TRY(A->hipMemcpyAsync(p->d_order, order.data(), order.size() * sizeof(int),
@@ -944,10 +817,9 @@ int prepare(const Api *A, mcs_plan *p, hipStream_t s)
     return MCS_OK;
 }
 
-// One launch pair (stream over all tiles + direct over the fallback tiles) for n_frames captures
-// that share one frame stride.
-// Multi-band level pyramids of captures [f0, f0 + nf) on stream s.
-// (the band pass when the plan has one, else mb_levels)
+// Multi-band level pyramids of captures [f0, f0 + nf) on stream s: the band pass when the plan
+// has one (interior and bottom / right edge bands in ONE launch, blocks below n_in interior, so
+// the edge bands run beside the interior ones), else mb_levels.
 int launch_mb_levels(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KMbArgs &m, int f0,
                      int nf, hipStream_t s)
 {
@@ -959,29 +831,11 @@ int launch_mb_levels(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KMb
         b.f0 = f0;
         b.nf = nf;
         const unsigned gy = (unsigned)((nf + mcs::kMbBandFrames - 1) / mcs::kMbBandFrames);
-        // interior and edge bands in ONE launch (blocks below n_in interior): the edge bands run
-        // beside the interior ones instead of after them.  MCS_MB_BANDS_FUSED=0 (experiments):
-        // two launches.
-        static const bool fused =
-            !getenv("MCS_MB_BANDS_FUSED") || strcmp(getenv("MCS_MB_BANDS_FUSED"), "0") != 0;
-        if (fused && p->n_bands_in > 0 && p->n_bands > p->n_bands_in) {
-            const unsigned gx = band_grid(b, p->n_bands);
-            return launch_args(A, k->mb_bands[p->fd.channels][band_form(p, b.P)][2], gx, gy,
-                               mcs::kMbBandLanes, 1, &b, sizeof(b), s);
-        }
-        int rc = MCS_OK;
-        if (p->n_bands_in > 0) {
-            const unsigned gx = band_grid(b, p->n_bands_in);
-            rc = launch_args(A, k->mb_bands[p->fd.channels][band_form(p, b.P)][0], gx, gy,
-                             mcs::kMbBandLanes, 1, &b, sizeof(b), s);
-        }
-        b.band0 = p->n_bands_in;
-        if (rc == MCS_OK && p->n_bands > p->n_bands_in) {
-            const unsigned gx = band_grid(b, p->n_bands - p->n_bands_in);
-            rc = launch_args(A, k->mb_bands[p->fd.channels][band_form(p, b.P)][1], gx, gy,
-                             mcs::kMbBandLanes, 1, &b, sizeof(b), s);
-        }
-        return rc;
+        const int form = band_form(p, b.P);
+        const int kind = p->n_bands_in == 0 ? 1 : (p->n_bands > p->n_bands_in ? 2 : 0);
+        if (kind == 1) b.band0 = 0;
+        return launch_args(A, k->mb_bands[p->fd.channels][form][kind], (unsigned)p->n_bands, gy,
+                           mcs::kMbBandLanes, 1, &b, sizeof(b), s);
     }
     const unsigned gz = (unsigned)((nf + mcs::kMbLvFrames - 1) / mcs::kMbLvFrames);
     size_t sz = sizeof(m);
@@ -991,26 +845,6 @@ int launch_mb_levels(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KMb
                                      (unsigned)p->mb_slots, gz, mcs::kMbLvThreads, 1, 1, 0, s,
                                      nullptr, cfg));
     return MCS_OK;
-}
-
-// One row chunk of the band pass (captures [f0, f0 + nf)): interior bands [i0, i1) and edge
-// bands [b0, b1) in one fused launch on stream s.
-int launch_band_chunk(const Api *A, const mcs_plan *p, const Kernels *k, const mcs::KParams &P,
-                      const mcs_plan::MbChunk &c, int f0, int nf, hipStream_t s)
-{
-    const int n = (c.i1 - c.i0) + (c.b1 - c.b0);
-    if (n <= 0) return MCS_OK;
-    mcs::KMbBandArgs b;
-    band_args(p, P, b);
-    b.f0 = f0;
-    b.nf = nf;
-    b.band0 = c.i0;
-    b.n_in = c.i1 - c.i0;
-    b.band1 = c.b0;
-    const unsigned gx = band_grid(b, n);
-    const unsigned gy = (unsigned)((nf + mcs::kMbBandFrames - 1) / mcs::kMbBandFrames);
-    return launch_args(A, k->mb_bands[p->fd.channels][band_form(p, b.P)][2], gx, gy,
-                       mcs::kMbBandLanes, 1, &b, sizeof(b), s);
 }
 
 // Multi-band tiles degraded to the feather rule (more than kBlendSlots owners in their
@@ -1029,6 +863,17 @@ int launch_dense(const Api *A, const mcs_plan *p, const Kernels *k, const mcs::K
                        &b, sizeof(b), s);
 }
 
+// The multi-band blend kernel for the plan's owner count (<= 2, <= 4, <= 8 per neighbourhood).
+int launch_mb_blend(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KMbArgs &m, int f0,
+                    int nf, hipStream_t s)
+{
+    m.f0 = f0;
+    m.nf = nf;
+    const int v = p->mb_slots <= 2 ? 0 : (p->mb_slots <= 4 ? 1 : 2);
+    return launch_args(A, k->mb_blend[p->fd.channels][v], (unsigned)p->n_blend, (unsigned)nf,
+                       mcs::kMbBlThreads, 1, &m, sizeof(m), s);
+}
+
 // One launch (stream over all tiles, + direct over the fallback tiles, + the blend passes) for
 // n_frames captures that share one frame stride.  Work that does not read the mosaic -- the
 // direct-gather tiles and the first multi-band chunk's level pyramids -- runs on two side streams,
@@ -1036,15 +881,10 @@ int launch_dense(const Api *A, const mcs_plan *p, const Kernels *k, const mcs::K
 int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams &P, int n_frames,
                 hipStream_t s)
 {
-    const bool mb_all = p->blend == MCS_BLEND_MULTIBAND && p->n_blend > 0;
-    // MCS_MB_CONCURRENT=0 (experiments): the level pyramids on the caller's stream, after the
-    // streaming kernel, instead of beside it
-    static const bool concurrent = !getenv("MCS_MB_CONCURRENT") ||
-                                   strcmp(getenv("MCS_MB_CONCURRENT"), "0") != 0;
-    const bool mb = mb_all && concurrent;
+    const bool mb = p->blend == MCS_BLEND_MULTIBAND && p->n_blend > 0;
     const bool fork = p->n_fallback > 0 || mb;
     mcs::KMbArgs m;
-    if (mb_all) mb_args(p, P, m);
+    if (mb) mb_args(p, P, m);
     if (fork) HIP_TRY(A->hipEventRecord(p->ev_fork, s));
     if (p->n_fallback > 0) {
         HIP_TRY(A->hipStreamWaitEvent(p->side, p->ev_fork, 0));
@@ -1065,21 +905,9 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
     }
     // split (multi-band, one scratch chunk): streaming tiles under mixed pixels first, then the
     // blend on side2 (after the band pass, those tiles and the direct-gather tiles) beside the
-    // remaining streaming tiles.  MCS_MB_SPLIT=0 (experiments): the blend after everything.
-    static const bool split_on = !getenv("MCS_MB_SPLIT") || strcmp(getenv("MCS_MB_SPLIT"), "0");
-    const bool split = mb && split_on && p->d_order && p->n_early > 0 && n_frames <= p->mb_chunk;
-    // row-chunked band pass + blend (split launches with a band pass of 2+ chunks): the blend of
-    // a chunk on side3 as soon as its bands are done, beside the next chunk's bands on side2
-    const bool chunked = split && p->n_bands > 0 && p->mb_chunks.size() > 1 && p->side3 &&
-                         p->ev_band.size() >= p->mb_chunks.size();
-    if (chunked) {
-        HIP_TRY(A->hipStreamWaitEvent(p->side2, p->ev_fork, 0));
-        for (size_t c = 0; c < p->mb_chunks.size(); c++) {
-            const int rc = launch_band_chunk(A, p, k, m.P, p->mb_chunks[c], 0, n_frames, p->side2);
-            if (rc) return rc;
-            HIP_TRY(A->hipEventRecord(p->ev_band[c], p->side2));
-        }
-    } else if (mb) {
+    // remaining streaming tiles (same-box A/B, round 2: C2 1.009 -> 0.985 ms)
+    const bool split = mb && p->d_order && p->n_early > 0 && n_frames <= p->mb_chunk;
+    if (mb) {
         HIP_TRY(A->hipStreamWaitEvent(p->side2, p->ev_fork, 0));
         const int rc = launch_mb_levels(A, p, k, m, 0, std::min(p->mb_chunk, n_frames), p->side2);
         if (rc) return rc;
@@ -1095,7 +923,8 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
     args.pad_ = 0;
     args.pad2_ = 0;
     // 1-D grid dealt over the 8 XCDs; the kernel maps block -> tile (XCD-contiguous bands)
-    auto stream_launch = [&](const int *order, int n_items, unsigned lds) -> int {
+    const unsigned lds = (unsigned)mcs::lds_stream_bytes(p->fd.channels);
+    auto stream_launch = [&](const int *order, int n_items) -> int {
         args.order = order;
         args.n_order = n_items;
         size_t sz = sizeof(args);
@@ -1107,57 +936,17 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
                                          lds, s, nullptr, cfg));
         return MCS_OK;
     };
-    const unsigned lds = (unsigned)mcs::lds_stream_bytes(p->fd.channels);
-    // MCS_STREAM_LDS_LATE (experiments): LDS reserved per block of the late streaming launch, to
-    // leave room on each CU for the multi-band kernels beside it
-    static const unsigned lds_late =
-        getenv("MCS_STREAM_LDS_LATE") ? (unsigned)atoi(getenv("MCS_STREAM_LDS_LATE")) : 0u;
-    const int n_tiles = p->gx * p->gy;
-    if (chunked) {
-        int rc = stream_launch(p->d_order, p->n_early, lds);
-        if (rc) return rc;
-        HIP_TRY(A->hipEventRecord(p->ev_early, s));
-        HIP_TRY(A->hipStreamWaitEvent(p->side3, p->ev_early, 0));
-        if (p->n_fallback > 0) HIP_TRY(A->hipStreamWaitEvent(p->side3, p->ev_join, 0));
-        m.f0 = 0;
-        m.nf = n_frames;
-        const int v = p->mb_slots <= 2 ? 0 : (p->mb_slots <= 4 ? 1 : 2);
-        for (size_t c = 0; c < p->mb_chunks.size(); c++) {
-            const mcs_plan::MbChunk &ch = p->mb_chunks[c];
-            HIP_TRY(A->hipStreamWaitEvent(p->side3, p->ev_band[c], 0));
-            if (ch.l1 <= ch.l0) continue;
-            m.list0 = ch.l0;
-            rc = launch_args(A, k->mb_blend[p->fd.channels][v], (unsigned)(ch.l1 - ch.l0),
-                             (unsigned)n_frames, mcs::kMbBlThreads, 1, &m, sizeof(m), p->side3);
-            if (rc) return rc;
-        }
-        m.list0 = 0;
-        HIP_TRY(A->hipEventRecord(p->ev_join2, p->side3));
-        if (p->n_list > p->n_early) {
-            rc = stream_launch(p->d_order + p->n_early, p->n_list - p->n_early,
-                               std::max(lds, lds_late));
-            if (rc) return rc;
-        }
-        if (p->n_fallback > 0) HIP_TRY(A->hipStreamWaitEvent(s, p->ev_join, 0));
-        HIP_TRY(A->hipStreamWaitEvent(s, p->ev_join2, 0));
-        return launch_dense(A, p, k, P, n_frames, s);
-    }
     if (split) {
-        int rc = stream_launch(p->d_order, p->n_early, lds);
+        int rc = stream_launch(p->d_order, p->n_early);
         if (rc) return rc;
         HIP_TRY(A->hipEventRecord(p->ev_early, s));
         HIP_TRY(A->hipStreamWaitEvent(p->side2, p->ev_early, 0));
         if (p->n_fallback > 0) HIP_TRY(A->hipStreamWaitEvent(p->side2, p->ev_join, 0));
-        m.f0 = 0;
-        m.nf = n_frames;
-        rc = launch_args(A, k->mb_blend[p->fd.channels][p->mb_slots <= 2 ? 0 : (p->mb_slots <= 4 ? 1 : 2)],
-                         (unsigned)p->n_blend, (unsigned)n_frames, mcs::kMbBlThreads, 1, &m,
-                         sizeof(m), p->side2);
+        rc = launch_mb_blend(A, p, k, m, 0, n_frames, p->side2);
         if (rc) return rc;
         HIP_TRY(A->hipEventRecord(p->ev_join2, p->side2));
         if (p->n_list > p->n_early) {
-            rc = stream_launch(p->d_order + p->n_early, p->n_list - p->n_early,
-                               std::max(lds, lds_late));
+            rc = stream_launch(p->d_order + p->n_early, p->n_list - p->n_early);
             if (rc) return rc;
         }
         if (p->n_fallback > 0) HIP_TRY(A->hipStreamWaitEvent(s, p->ev_join, 0));
@@ -1166,8 +955,8 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
     }
     {
         // (d_order: the tile order of prepare / prepare_bands; NULL: row-major grid order)
-        const int rc = p->d_order ? stream_launch(p->d_order, p->n_list, lds)
-                                  : stream_launch(nullptr, n_tiles, lds);
+        const int rc = p->d_order ? stream_launch(p->d_order, p->n_list)
+                                  : stream_launch(nullptr, p->gx * p->gy);
         if (rc) return rc;
     }
     if (p->n_fallback > 0) HIP_TRY(A->hipStreamWaitEvent(s, p->ev_join, 0));
@@ -1189,15 +978,8 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
             // already ran on the side stream) then blend
             for (int f0 = 0; f0 < n_frames && rc == MCS_OK; f0 += p->mb_chunk) {
                 const int nf = std::min(p->mb_chunk, n_frames - f0);
-                if (f0 > 0 || !mb) rc = launch_mb_levels(A, p, k, m, f0, nf, s);
-                m.f0 = f0;
-                m.nf = nf;
-                if (rc == MCS_OK)
-                    rc = launch_args(A,
-                                     k->mb_blend[p->fd.channels]
-                                                [p->mb_slots <= 2 ? 0 : (p->mb_slots <= 4 ? 1 : 2)],
-                                     (unsigned)p->n_blend,
-                                     (unsigned)nf, mcs::kMbBlThreads, 1, &m, sizeof(m), s);
+                if (f0 > 0) rc = launch_mb_levels(A, p, k, m, f0, nf, s);
+                if (rc == MCS_OK) rc = launch_mb_blend(A, p, k, m, f0, nf, s);
             }
         }
         if (rc) return rc;
@@ -1216,26 +998,10 @@ int ensure_side(const Api *A, mcs_plan *p)
         HIP_TRY(A->hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming));
         HIP_TRY(A->hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking));
     }
-    if (mb && p->mb_chunks.size() > 1) {
-        if (!p->side3) HIP_TRY(A->hipStreamCreateWithFlags(&p->side3, hipStreamNonBlocking));
-        while (p->ev_band.size() < p->mb_chunks.size()) {
-            hipEvent_t e = nullptr;
-            HIP_TRY(A->hipEventCreateWithFlags(&e, hipEventDisableTiming));
-            p->ev_band.push_back(e);
-        }
-    }
     if (mb && !p->side2) {
         HIP_TRY(A->hipEventCreateWithFlags(&p->ev_join2, hipEventDisableTiming));
         HIP_TRY(A->hipEventCreateWithFlags(&p->ev_early, hipEventDisableTiming));
-        // MCS_MB_PRIORITY=1 / -1 (experiments): the band pass / blend stream at the greatest /
-        // least priority (measured: greatest 3 % slower, least within noise)
-        static const int prio = getenv("MCS_MB_PRIORITY") ? atoi(getenv("MCS_MB_PRIORITY")) : 0;
-        int lo = 0, hi = 0;
-        if (prio != 0 && A->hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
-            HIP_TRY(A->hipStreamCreateWithPriority(&p->side2, hipStreamNonBlocking,
-                                                   prio > 0 ? hi : lo));
-        else
-            HIP_TRY(A->hipStreamCreateWithFlags(&p->side2, hipStreamNonBlocking));
+        HIP_TRY(A->hipStreamCreateWithFlags(&p->side2, hipStreamNonBlocking));
     }
     return MCS_OK;
 }
@@ -1549,9 +1315,6 @@ int mcs_plan_destroy(mcs_plan *p)
             if (p->stream) (void)A->hipStreamDestroy(p->stream);
             if (p->side) (void)A->hipStreamDestroy(p->side);
             if (p->side2) (void)A->hipStreamDestroy(p->side2);
-            if (p->side3) (void)A->hipStreamSynchronize(p->side3);
-            if (p->side3) (void)A->hipStreamDestroy(p->side3);
-            for (hipEvent_t e : p->ev_band) (void)A->hipEventDestroy(e);
             if (p->ev_fork) (void)A->hipEventDestroy(p->ev_fork);
             if (p->ev_join) (void)A->hipEventDestroy(p->ev_join);
             if (p->ev_join2) (void)A->hipEventDestroy(p->ev_join2);
@@ -1824,6 +1587,7 @@ int mcs_plan_find_seams(mcs_plan *p, const uint8_t *const *cams, int method, int
 {
     mcs::clear_error();
     if (!p) return mcs::fail(MCS_E_INVALID, "NULL plan");
+    for (int64_t &v : p->seam_stats) v = 0;   // (only the device max-flow fills them in)
     if (method != MCS_SEAM_DISTANCE && method != MCS_SEAM_GRAPHCUT)
         return mcs::fail(MCS_E_INVALID, "seam method %d", method);
     if (method == MCS_SEAM_GRAPHCUT && (!cams || scale_log2 < 0 || scale_log2 > 4))

@@ -644,10 +644,9 @@ int orb_detect(const uint8_t *image, bool on_device, int w, int h, int channels,
     }
     // levels 1 .. nlevels-1: one launch (mcs_orb_pyramid) when every level is a < 2x
     // downscale of the one before (its blocks' dependency regions then tile every level), else
-    // (or MCS_ORB_PYRAMID=0) one resize launch per level
+    // one resize launch per level
     mcs::KOrbBuildArgs ba;
-    static const bool fused_on = !getenv("MCS_ORB_PYRAMID") || strcmp(getenv("MCS_ORB_PYRAMID"), "0");
-    const unsigned pyr_blocks = fused_on && e == hipSuccess && rc == MCS_OK && nlevels > 1
+    const unsigned pyr_blocks = e == hipSuccess && rc == MCS_OK && nlevels > 1
                                     ? mcs::feat::pyramid_args(geo, buf + o_lvl, ba)
                                     : 0u;
     if (pyr_blocks > 0) {

@@ -767,15 +767,10 @@ __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *til
     const int per = (n_order + 7) >> 3;
     const int idx = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
     if (idx >= n_order) return;
-    // launch-list item: a tile and a share of the launch's captures (kItem*); -1 = padding
-    const int item = order ? __builtin_amdgcn_readfirstlane(order[idx]) : idx;
-    if (item < 0) return;
-    const int tile = item & kItemTileMask;
-    const int f_beg = (int)(((int64_t)((item >> kItemPartShift) & 15) * n_frames) >>
-                            ((item >> kItemLogShift) & 3));
-    const int f_end = (int)(((int64_t)(((item >> kItemPartShift) & 15) + 1) * n_frames) >>
-                            ((item >> kItemLogShift) & 3));
-    if (f_beg >= f_end) return;
+    // launch-list entry: a tile (-1 = padding); the block streams every capture through it
+    const int tile = order ? __builtin_amdgcn_readfirstlane(order[idx]) : idx;
+    if (tile < 0) return;
+    const int f_beg = 0, f_end = n_frames;
     const int bx = tile % gx, by = tile / gx;
     // the tile header, copied once into LDS (the kernel also stores to global memory, so the
     // compiler cannot serve `tiles` from the scalar cache)

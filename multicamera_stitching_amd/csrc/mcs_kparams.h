@@ -84,13 +84,6 @@ constexpr int kTileH = kWavesPerBlock * kRowsPerWave;
 constexpr int kTileCams = 4;       // cameras one LDS tile may draw from
 constexpr int kTilePx = kTileW * kTileH;
 constexpr int kDescWords = 3;
-// Launch-list items of the streaming kernel: tile index | part << kItemPartShift | log2(parts) <<
-// kItemLogShift -- the tile over captures [part * n / parts, (part + 1) * n / parts) of the
-// launch's n; -1 = padding.  The tiles that start last on each XCD are split into parts so the
-// launch's drain is short (tail items of a quarter of a tile's captures).
-constexpr int kItemTileMask = (1 << 24) - 1;
-constexpr int kItemPartShift = 24;
-constexpr int kItemLogShift = 28;
 
 // Compact per-pixel word the streaming kernel loads (4 B instead of 12): bits 0-15 the row-0
 // window's LDS address, 16-20 fx, 21-25 fy, 26-27 the camera's footprint slot in the tile header;
@@ -321,12 +314,6 @@ struct KMbBandArgs {
                                    // (band band0 + block), the others the _br path (band
                                    // band1 + block - n_in)
     int band1, pad_;
-    // band -> block mapping: 0 = block x is band x (consecutive bands round-robin over the 8
-    // XCDs); n > 0 = XCD-contiguous: the launch's n bands are dealt to the XCDs in contiguous
-    // slices (block b -> band (b % 8) * ceil(n / 8) + b / 8; the grid is padded to a multiple
-    // of 8), so vertically adjacent bands of one owner -- which share 25 of their 89 source
-    // rows -- run on one XCD's L2
-    int xcd;
 };
 struct KBlendArgs {
     KParams P;

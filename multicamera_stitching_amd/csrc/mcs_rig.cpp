@@ -459,7 +459,10 @@ int device_capture(mcs_rig_job *j, bool *overflow)
     int rc = MCS_OK;
     const mcs::rt::Api *A = api_for(j->device, &rc);
     if (rc) return rc;
-    if (!j->dev.ready && (rc = device_setup(j)) != MCS_OK) return rc;
+    if (!j->dev.ready && (rc = device_setup(j)) != MCS_OK) {
+        device_release(j);   // (a partial setup: the next capture starts from clean state)
+        return rc;
+    }
     RigDevice &d = j->dev;
     const mcs::feat::FeatureKernels *k = nullptr;
     mcs::DeviceGuard dg(A, j->device);
@@ -469,11 +472,9 @@ int device_capture(mcs_rig_job *j, bool *overflow)
     const int C = j->n_cams, P = j->n_cams - 1;
     hipStream_t s = d.s;
     if (j->wait_event) HIP_TRY(A->hipStreamWaitEvent(s, (hipEvent_t)j->wait_event, 0));
-    // MCS_RIG_GRAPH=0: plain launches every capture
-    static const bool graphs = !getenv("MCS_RIG_GRAPH") || strcmp(getenv("MCS_RIG_GRAPH"), "0");
     hipError_t e = hipSuccess;
     if ((rc = enqueue_resets(j, A, s)) != MCS_OK) return rc;
-    if (graphs && d.pyr_blocks > 0) {
+    if (d.pyr_blocks > 0) {
         if (!d.exec || d.graph_frames != j->frames) {
             if (d.exec) (void)A->hipGraphExecDestroy(d.exec);
             d.exec = nullptr;
@@ -547,12 +548,6 @@ void start_calls(mcs_rig_job *j)
     j->left.store(j->n_cams - 1);
     for (int k = 0; k < j->n_cams - 1; k++) j->need[k].store(2);
     for (int c = 0; c < j->n_cams; c++) Pool::get().run([j, c] { orb_task(j, c); });
-}
-
-bool calls_path()
-{
-    static const bool calls = getenv("MCS_RIG_PATH") && !strcmp(getenv("MCS_RIG_PATH"), "calls");
-    return calls;
 }
 
 void capture_task(mcs_rig_job *j)
@@ -631,12 +626,7 @@ int mcs_rig_job_submit(mcs_rig_job *j, const uint8_t *const *d_frames, void *wai
     }
     j->frames.assign(d_frames, d_frames + j->n_cams);
     j->wait_event = wait_event;
-    if (calls_path()) {
-        j->captures_calls++;
-        start_calls(j);
-    } else {
-        Pool::get().run([j] { capture_task(j); });
-    }
+    Pool::get().run([j] { capture_task(j); });
     return MCS_OK;
 }
 

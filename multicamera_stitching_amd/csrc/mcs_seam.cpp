@@ -215,19 +215,9 @@ int seam_graphcut_device(int device, hipStream_t s, int n_cams, int gw, int gh, 
     fa.cn = cn;
     // push-relabel rounds between global relabels / relaxation rounds per relabel launch;
     // a round bound far beyond any grid's need (a run-away loop fails loudly instead of hanging)
-    // (MCS_SEAM_PUSH_LAUNCHES / _PUSH_ITERS / _RELABEL_ITERS: tuning experiments)
-    auto knob = [](const char *name, int dflt) {
-        const char *v = getenv(name);
-        return v && atoi(v) > 0 ? atoi(v) : dflt;
-    };
-    static const int kPushLaunches = knob("MCS_SEAM_PUSH_LAUNCHES", 8);
-    static const int kPushIters = knob("MCS_SEAM_PUSH_ITERS", 16);
-    static const int kRelabelIters = knob("MCS_SEAM_RELABEL_ITERS", 64);
-    // global relabels in LDS tiles (default) or with L2 round trips (MCS_SEAM_RELABEL_LDS=0)
-    static const bool relabel_lds =
-        !getenv("MCS_SEAM_RELABEL_LDS") || strcmp(getenv("MCS_SEAM_RELABEL_LDS"), "0");
-    static const int kRelabelLdsIters = knob("MCS_SEAM_RELABEL_LDS_ITERS", 32);
-    static const int kRelabelBatch = knob("MCS_SEAM_RELABEL_BATCH", 8);
+    // (tuned on C4, round 3: tools/experiments/gpu_r03_seamtune*.sh); global relabels run as
+    // Bellman-Ford relaxation rounds in LDS tiles
+    constexpr int kPushLaunches = 8, kPushIters = 16, kRelabelLdsIters = 32, kRelabelBatch = 8;
     constexpr int64_t kMaxRounds = 1 << 20;
     auto launch = [&](hipFunction_t f, unsigned gx, unsigned gy) {
         return feat::launch(A, f, gx, gy, 256, &fa, sizeof(fa), s);
@@ -261,13 +251,12 @@ int seam_graphcut_device(int device, hipStream_t s, int n_cams, int gw, int gh, 
                 rc = launch(k->seam_hinit, gx, gy);
                 // batches of relabel launches, the flag reset before each: the flag read after a
                 // batch is its last launch's, zero only at the fixpoint
-                fa.iters = relabel_lds ? kRelabelLdsIters : kRelabelIters;
+                fa.iters = kRelabelLdsIters;
                 for (;;) {
                     for (int j = 0; j < kRelabelBatch && e == hipSuccess && rc == MCS_OK; j++) {
                         e = A->hipMemsetAsync(fa.flag, 0, 2 * sizeof(int32_t), s);
                         if (e == hipSuccess)
-                            rc = launch(relabel_lds ? k->seam_relabel_lds : k->seam_relabel, gx,
-                                        gy);
+                            rc = launch(k->seam_relabel_lds, gx, gy);
                         st[2]++;
                     }
                     if (e == hipSuccess && rc == MCS_OK) e = read_flags();

@@ -95,6 +95,35 @@ def test_reference_pickle_loads_into_dropin(tmp_path):
         assert a.ABSize == b.ABSize
 
 
+class _Hostile:
+    """Pickles as a call of os.system (what a tampered Stitcher_config.pkl could hold)."""
+
+    def __reduce__(self):
+        return (os.system, ("echo pickle-ran-os.system >&2",))
+
+
+@pytest.mark.parametrize("payload", ["os.system", "builtins.eval"])
+def test_pickle_loader_refuses_foreign_globals(tmp_path, payload):
+    """load_stitcher's unpickler allow-lists the globals a stitcher pickle holds: a pickle naming
+    os.system (or eval) is refused before anything runs, while the reference-written
+    rig4_mild_Stitcher_config.pkl (test above) still loads."""
+    import pickle
+    from multicamera_stitching_amd.StitcherClass import Stitcher
+    meta, frames, _ = goldens.load("rig4_mild")
+    bad = tmp_path / "Stitcher_config.pkl"
+    obj = _Hostile() if payload == "os.system" else _Eval()
+    bad.write_bytes(pickle.dumps({"stitchers": [obj]}, protocol=2))
+    with pytest.raises(pickle.UnpicklingError, match=payload.split(".")[1]):
+        Stitcher(dict(frames)).load_stitcher(str(bad))
+    pkl = os.path.join(goldens.GOLDEN, "rig4_mild_Stitcher_config.pkl")
+    assert isinstance(Stitcher(dict(frames)).load_stitcher(pkl), Stitcher)
+
+
+class _Eval:
+    def __reduce__(self):
+        return (eval, ("1 + 1",))
+
+
 def test_fixture_manifest_is_consistent():
     for name in NAMES:
         meta, frames, out = goldens.load(name)

@@ -77,6 +77,41 @@ def test_multiband_c2_full_size_batch():
     assert 0 < st["mb_bands_lds"] < st["mb_bands"], st
 
 
+@pytest.mark.parametrize("shift, pad", [(1, 0), (3, 2)])
+def test_multiband_c2_unaligned_frames(shift, pad):
+    """Config 2 at full size with camera frames that start off a 4-byte boundary (shift) and,
+    for pad > 0, a frame stride that is not a multiple of 4: the launch takes the band pass's
+    unaligned window form, whose descriptors must stay the frame-offset ones even though the
+    plan's LDS-ring bands rewrote theirs (advisor finding, round 3) -- bit-exact vs the oracle."""
+    import torch
+    plan, cams = _world_plan(4, 1920, 1080, 3, seed=0)
+    plan.set_blend(MODES["multiband"])
+    F = 2
+    shots = [[np.roll(c, 5 * f, axis=1) for c in cams] for f in range(F)]
+    fb = cams[0].size
+    stride = fb + pad
+    dev = []
+    for i in range(len(cams)):
+        buf = torch.zeros(shift + F * stride, dtype=torch.uint8)
+        for f in range(F):
+            buf[shift + f * stride: shift + f * stride + fb] = torch.from_numpy(
+                shots[f][i].reshape(-1))
+        dev.append(buf.cuda())
+    out = torch.zeros((F, plan.out_h, plan.out_w * 3), dtype=torch.uint8, device="cuda")
+    plan.stitch_device([d.data_ptr() + shift for d in dev], [stride] * len(dev),
+                       out.data_ptr(), plan.out_w * 3, out[0].numel(), F, 0)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    for f in range(F):
+        want = oracle.blend_stitch(plan.describe(), shots[f], MODES["multiband"])
+        assert _diff(got[f].reshape(want.shape), want) == 0, f
+    # the aligned launch of the same plan afterwards still uses the ring (descriptors intact)
+    st = plan.stats()
+    assert 0 < st["mb_bands_lds"] < st["mb_bands"], st
+    want = oracle.blend_stitch(plan.describe(), cams, MODES["multiband"])
+    assert _diff(plan.stitch_host(cams).reshape(want.shape), want) == 0
+
+
 @pytest.mark.parametrize("F", [64, 70])
 def test_multiband_batch_split_and_chunked(F):
     """A multi-band device batch of F captures: F <= 64 takes the split launch (streaming tiles

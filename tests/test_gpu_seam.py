@@ -1,6 +1,7 @@
 """GPU graph-cut seams (mcs_plan_find_seams): device sampling of the seam
-grid + host max-flow, then the seam-labelled owner rule inside the stitch kernels, against the
-CPU restatement (oracle/orc_seam.c + orc_blend.c).  Bit-exact labels and panoramas."""
+grid + device push-relabel max-flow (the host Dinic, MCS_SEAM_FLOW=host, is its checker), then
+the seam-labelled owner rule inside the stitch kernels, against the CPU restatement
+(oracle/orc_seam.c + orc_blend.c).  Bit-exact labels and panoramas."""
 import numpy as np
 import pytest
 

@@ -73,6 +73,48 @@ def test_calibrate_without_feature_backend_logs_and_stays_uncalibrated(caplog):
     assert "feature" in caplog.text
 
 
+def test_orb_fallback_is_logged_once(caplog, monkeypatch):
+    """Without OpenCV contrib SIFT the drop-in calibrates with GPU ORB: logged once per process,
+    at the reference's contrib guard (StitcherClass.py:87-93), never silently."""
+    from multicamera_stitching_amd import StitcherClass as sc, features
+    monkeypatch.setattr(features, "backend", lambda: "orb")
+    monkeypatch.setattr(features, "available", lambda: True)
+    monkeypatch.setattr(sc, "_orb_noted", False)
+    monkeypatch.delenv("MCS_FEATURES", raising=False)
+    # (no GPU here: the stages' feature matching is stubbed to "no homography")
+    monkeypatch.setattr(StitcherBase, "calibrate",
+                        lambda self, images, *a, **k: self.reset())
+    imgs = images()
+    with caplog.at_level(logging.WARNING, logger="multicamera_stitching_amd"):
+        Stitcher(imgs).calibrate_stitcher(imgs, save=False)
+        Stitcher(imgs).calibrate_stitcher(imgs, save=False)
+    hits = [r for r in caplog.records if "instead of SIFT" in r.getMessage()]
+    assert len(hits) == 1 and "not a contrib version" in hits[0].getMessage()
+
+
+@pytest.mark.parametrize("code, raises", [(-2, False), (-3, False), (-1, True), (-5, True)])
+def test_gpu_failure_fallback_only_for_runtime_errors(monkeypatch, caplog, code, raises):
+    """A run-time failure of the GPU path (MCS_E_HIP / MCS_E_NOMEM) is logged and the fallback
+    image returned, as the reference returns images on its expected failures; argument and
+    programming errors (MCS_E_INVALID / MCS_E_UNSUPPORTED) raise (advisor finding, round 3)."""
+    from multicamera_stitching_amd import StitcherClass as sc, _capi
+    imgs = images()
+    st = Stitcher(imgs)
+    st.calibrate_stitcher(imgs, save=False, homographies=[[[1, 0, 30], [0, 1, 2], [0, 0, 1]],
+                                                          [[1, 0, 40], [0, 1, 0], [0, 0, 1]]])
+
+    def boom(*a, **k):
+        raise _capi.McsError(code, "injected")
+    monkeypatch.setattr(sc, "_get_plan", boom)
+    if raises:
+        with pytest.raises(_capi.McsError):
+            st.stitch(imgs)
+    else:
+        with caplog.at_level(logging.ERROR, logger="multicamera_stitching_amd"):
+            out = st.stitch(imgs)
+        assert isinstance(out, np.ndarray) and "GPU stitch failed" in caplog.text
+
+
 def test_failed_homography_resets_stage():
     imgs = images()
     st = Stitcher(imgs)
