@@ -48,6 +48,10 @@ def parse():
                          "cylinder: SURVEY.md 8 C4 (8 cameras at 45 degree yaw, f = 1100, "
                          "cylindrical 360 panorama)")
     ap.add_argument("--focal", type=float, default=1100.0, help="cylinder rig focal length (px)")
+    ap.add_argument("--seam", choices=["graphcut", "distance"], default="graphcut",
+                    help="cylinder rig seams: graph-cut (BASELINE configs[3], found once per plan "
+                         "from capture 0 before the timed region, mcs_plan_find_seams on the 1/4 "
+                         "grid) or the distance seam")
     ap.add_argument("--cams", type=int, default=None, help="default 4 (chain) / 8 (cylinder)")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
@@ -147,6 +151,15 @@ def main():
             return _capi.Plan(descs, args.width, args.height, args.channels, interp,
                               device=torch.cuda.current_device())
     plan = make_plan()
+    seam_k = None
+    if cyl and args.seam == "graphcut":
+        # calibration-time step (once per plan, outside the timed region): graph-cut seams on
+        # the 2^2 grid from one capture; every timed capture then follows those seams
+        seam_k = 2
+        t_seam = time.perf_counter()
+        plan.find_seams(cams, _capi.MCS_SEAM_GRAPHCUT, seam_k)
+        seam_ms = (time.perf_counter() - t_seam) * 1e3
+        seam_labels = plan.seam_labels()
     blend = {"none": _capi.MCS_BLEND_NONE, "feather": _capi.MCS_BLEND_FEATHER,
              "multiband": _capi.MCS_BLEND_MULTIBAND, "seam": _capi.MCS_BLEND_SEAM}[args.blend]
     plan.set_blend(blend)
@@ -227,6 +240,8 @@ def main():
     if blend not in (_capi.MCS_BLEND_NONE, _capi.MCS_BLEND_SEAM) and not args.no_paste_ref:
         ref = make_plan()
         if cyl:
+            if seam_k is not None:
+                ref.find_seams(cams, _capi.MCS_SEAM_GRAPHCUT, seam_k)
             ref.set_blend(_capi.MCS_BLEND_SEAM)
         ref.prepare(stream.cuda_stream)
 
@@ -261,7 +276,7 @@ def main():
     workload = (f"{args.cams}x{args.width}x{args.height}x{C}-{args.interp}-"
                 f"super{int(args.super_mode)}-F{F}-{args.blend}")
     if cyl:
-        workload = f"cyl-f{args.focal:g}-" + workload
+        workload = f"cyl-f{args.focal:g}-" + workload + ("-gc2" if seam_k is not None else "")
     traffic_src = None
     try:
         pm = json.load(open(args.pmc_json))
@@ -276,12 +291,21 @@ def main():
     # parity on EVERY rank (outside the timed region): this rank's capture 0 (read back above,
     # before the paste-only launch reuses d_out) against the CPU restatement fed the same camera
     # frames; the line reports the max over ranks
-    runner = oracle_runner(st, args, interp, plan, blend, (rig_cams, geo) if cyl else None)
+    runner = oracle_runner(st, args, interp, plan, blend, (rig_cams, geo) if cyl else None,
+                           seams=(seam_k, seam_labels) if seam_k is not None else None)
     host = host_cpus()
     shift = [(rank * F) % c.shape[0] for c in cams]
     max_abs = check_frame0(runner, [np.roll(c, s, axis=0) for c, s in zip(cams, shift)], frame0,
                            max(1, host["usable"] // world))
     max_abs = shard.max_abs_over_ranks(max_abs, device=dev)
+    seams_equal = None
+    if seam_k is not None and rank == 0:
+        # the plan's cut of capture 0 against the restatement's (orc_seam.c) on the same frames
+        from oracle import oracle
+        _, want_lab = oracle.blend_stitch_cyl(rig_cams, geo["out_w"], geo["out_h"], geo["f_cyl"],
+                                              geo["u0"], geo["v0"], cams, _capi.MCS_BLEND_SEAM,
+                                              interp, seam_k=seam_k, want_seams=True)
+        seams_equal = bool(np.array_equal(want_lab, seam_labels))
 
     result = None
     if rank == 0:
@@ -316,7 +340,11 @@ def main():
                      "lds_tiles": plan_stats["lds_tiles"],
                      "direct_tiles": plan_stats["direct_tiles"],
                      "blend_tiles_32x64": plan_stats["blend_tiles"],
-                     "table_mb": round(plan_stats["table_bytes"] / 1e6, 2)},
+                     "table_mb": round(plan_stats["table_bytes"] / 1e6, 2),
+                     "seams": None if seam_k is None else {
+                         "method": "graph-cut (mcs_plan_find_seams, device push-relabel)",
+                         "grid_log2": seam_k, "ms_once": round(seam_ms, 2),
+                         "labels_equal_restatement": seams_equal}},
             "kernels": {"launch_ms": round(launch_ms, 4),
                         "paste_only_launch_ms": None if paste_ms is None else round(paste_ms, 4)},
             "roofline": {
@@ -342,6 +370,10 @@ def main():
                             "achieved": round(touched_per_launch / (launch_ms * 1e-3) / 1e9, 1),
                             "frac": round(touched_per_launch / (launch_ms * 1e-3) / 1e9 /
                                           HBM_PEAK_GBS, 4)},
+                # which fraction is the honest one: a cylinder's cameras are read only where the
+                # panorama's rows curve through them (B_frame counts every frame byte), a chain
+                # rig's B_frame and touched bytes differ by the few frame pixels no stage reads
+                "honest_frac": "touched" if cyl else "frac",
                 # the HBM-bound streaming kernel alone (the paste-only launch: the same gather
                 # over every tile without the blend passes), same algorithmic bytes
                 "stream_kernel": None if paste_ms is None else {
@@ -492,6 +524,14 @@ def stub_main(args, world, rank):
 
 
 def describe_workload(args, cyl):
+    if cyl and args.seam == "graphcut" and args.blend in ("multiband", "feather", "seam"):
+        what = {"multiband": "graph-cut seams (SURVEY.md 8 NS-6, once per plan) + 3-level "
+                             "multi-band blend (NS-1)",
+                "feather": "graph-cut seams + linear feather blend",
+                "seam": "graph-cut seams, no blend"}[args.blend]
+        return (f"C4 rig: {args.cams} x {args.width}x{args.height} BGR cameras at "
+                f"{360.0 / args.cams:g} degree yaw steps, f = {args.focal:g}, cylindrical warp "
+                f"({args.interp}) + {what}")
     what = {"multiband": "3-level multi-band blend (SURVEY.md 8 NS-1)",
             "feather": "linear feather blend (SURVEY.md 8 NS-2)",
             "seam": "distance seam, no blend",
@@ -533,10 +573,12 @@ def host_cpus() -> dict:
             "model": model}
 
 
-def oracle_runner(st, args, interp, plan, blend, cyl=None):
+def oracle_runner(st, args, interp, plan, blend, cyl=None, seams=None):
     """The workload's CPU restatement (oracle/, test infrastructure) as run(cams) -> mosaic, plus
     the reference-structured cascade (paste only) and the flattened gather, for the baseline.
-    Returns {"workload": (run, what), "cascade": ..., "flat": ...} (None where not defined)."""
+    Returns {"workload": (run, what), "cascade": ..., "flat": ...} (None where not defined).
+    seams = (k, labels): graph-cut seams found once per plan (the labels are checked equal to the
+    restatement's own cut of the same capture by the caller); every capture follows them."""
     from oracle import oracle
     out = {"cascade": None, "flat": None}
     if st is not None:
@@ -555,11 +597,14 @@ def oracle_runner(st, args, interp, plan, blend, cyl=None):
                            "flattened single-pass gather (mcs_oracle.c orc_flat_stitch)")
     elif cyl is not None:
         rig_cams, g = cyl
+        sk, lab = seams if seams is not None else (None, None)
         out["workload"] = (
             lambda cams: oracle.blend_stitch_cyl(rig_cams, g["out_w"], g["out_h"], g["f_cyl"],
-                                                 g["u0"], g["v0"], cams, blend, interp),
+                                                 g["u0"], g["v0"], cams, blend, interp,
+                                                 seam_k=sk, seam_labels=lab),
             {1: "feather", 2: "3-level multi-band", 3: "seam"}[blend] +
-            " cylindrical panorama (orc_blend.c)")
+            " cylindrical panorama (orc_blend.c" +
+            (", graph-cut seams of the plan, orc_seam.c)" if sk is not None else ")"))
     else:
         flat = plan.describe()
         out["workload"] = (lambda cams: oracle.blend_stitch(flat, cams, blend, interp),

@@ -153,12 +153,13 @@ int mcs_plan_describe(const mcs_plan *plan, mcs_flat_desc *out);
  * call it on first use.  stream: hipStream_t or NULL for the plan's own stream. */
 int mcs_plan_prepare(mcs_plan *plan, void *stream);
 
-/* stats[0..10] = prepared, tiles, tiles on the LDS path, tiles on the direct path, table bytes,
+/* stats[0..11] = prepared, tiles, tiles on the LDS path, tiles on the direct path, table bytes,
  * blend mode, 32 x 64 tiles the blend kernels recompute per frame, the most owners any
  * multi-band tile blends (<= 8), multi-band tiles degraded to the feather rule (their
  * neighbourhood -- the tile grown by 16 px -- holds more than 8 owners), multi-band bands of the
  * level pass, of those the bands whose source rows are staged in the LDS ring (the rest read
- * their windows from global memory).  Entries past 10 read 0. */
+ * their windows from global memory), and of the LDS-path tiles those whose footprints need the
+ * large-footprint streaming launch (16 rows per wave, 120 KiB ring).  Entries past 11 read 0. */
 int mcs_plan_stats(const mcs_plan *plan, int64_t *stats, int n);
 
 /* Blend mode of the plan (MCS_BLEND_*; default NONE = the reference's paste).  Changing it drops

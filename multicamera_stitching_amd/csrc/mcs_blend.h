@@ -13,6 +13,11 @@
 //                -> mask-weighted blend per level (double) -> collapse -> bytes.
 // Both are a few percent of the mosaic's tiles for a linear rig.
 #pragma once
+// Band-pass timing decomposition (variant builds only, never the product): bit 0 = no bilinear
+// arithmetic, bit 1 = no horizontal level-1 reduce, bit 2 = no level-2 arithmetic (wrong values).
+#ifndef MCS_EXP_BAND_PART
+#define MCS_EXP_BAND_PART 0
+#endif
 
 namespace mcs {
 
@@ -335,6 +340,10 @@ __device__ __forceinline__ void exp_taps(int x, int n, int *idx, int *wt)
     idx[2] = idx[1], wt[2] = 0;   // padding tap: adds an exact 0, keeps the trip count fixed
 }
 
+// Parity class of a fine position's expand taps: bit 0 = odd column (2 taps), bit 1 = odd row.
+// (Reflection at the level's borders keeps parity: refl(-i) = i, refl(n - 1 + i) = n - 1 - i.)
+__device__ __forceinline__ int mb_cls(int x, int y) { return (x & 1) | ((y & 1) << 1); }
+
 // Geometry of one multi-band tile: level sizes and the origins of the arrays held per level.
 struct MbGeo {
     int W, H, w1, h1, w2, h2;
@@ -593,12 +602,19 @@ __device__ __forceinline__ void mb_prep(const KMbArgs &a)
     // the other ("mixed") pixels and the R1 entries they read.
     __shared__ int need_r1[kMbNRX * kMbNRY];
     __shared__ int n_px, n_r1;
+    // Both lists are stored grouped by the parity class of their expand taps (mb_cls: row
+    // parity, column parity -> 3 or 2 taps per axis), so the blend kernel's waves run one
+    // fixed-count tap body each (4, 6 or 9 taps instead of 9 with zero-weight padding)
+    __shared__ uint8_t px_cls[kMbTilePx];
+    __shared__ int cls_n[2][4], cls_at[2][4];
     // per owner slot: mosaic level-1 / level-2 columns the blend reads from it (band pass)
     __shared__ int nq1lo[kBlendSlots], nq1hi[kBlendSlots], nz2lo[kBlendSlots], nz2hi[kBlendSlots];
     int32_t *t_cnt = t_d2 + kMbN2X * kMbN2Y;
     uint16_t *t_px = reinterpret_cast<uint16_t *>(t_cnt + kMbTabCounts);
     uint16_t *t_r1 = t_px + kMbTilePx;
     for (int e = tid; e < kMbNRX * kMbNRY; e += nt) need_r1[e] = 0;
+    for (int i = tid; i < kMbTilePx; i += nt) px_cls[i] = 255;
+    if (tid < 8) cls_n[tid >> 2][tid & 3] = 0;
     if (tid == 0) n_px = n_r1 = 0;
     if (tid < kBlendSlots) {
         nq1lo[tid] = nz2lo[tid] = 1 << 30;
@@ -629,7 +645,9 @@ __device__ __forceinline__ void mb_prep(const KMbArgs &a)
                     }
             }
         if (!mixed) continue;
-        t_px[atomicAdd(&n_px, 1)] = (uint16_t)i;
+        atomicAdd(&n_px, 1);
+        px_cls[i] = (uint8_t)mb_cls(x, y);
+        atomicAdd(&cls_n[0][px_cls[i]], 1);
         for (int u = 0; u < 3; u++)
             for (int v = 0; v < 3; v++)
                 need_r1[ix2<false>(iy[u], G.YR, kMbNRY) * kMbNRX + ix2<false>(ix[v], G.XR, kMbNRX)] =
@@ -640,7 +658,22 @@ __device__ __forceinline__ void mb_prep(const KMbArgs &a)
     }
     __syncthreads();
     for (int e = tid; e < kMbNRX * kMbNRY; e += nt)
-        if (need_r1[e]) t_r1[atomicAdd(&n_r1, 1)] = (uint16_t)e;
+        if (need_r1[e]) {
+            atomicAdd(&n_r1, 1);
+            atomicAdd(&cls_n[1][mb_cls(G.XR + e % kMbNRX, G.YR + e / kMbNRX)], 1);
+        }
+    __syncthreads();
+    if (tid < 2) {
+        int at = 0;
+        for (int c = 0; c < 4; c++) cls_at[tid][c] = at, at += cls_n[tid][c];
+    }
+    __syncthreads();
+    for (int i = tid; i < kMbTilePx; i += nt)
+        if (px_cls[i] != 255) t_px[atomicAdd(&cls_at[0][px_cls[i]], 1)] = (uint16_t)i;
+    for (int e = tid; e < kMbNRX * kMbNRY; e += nt)
+        if (need_r1[e])
+            t_r1[atomicAdd(&cls_at[1][mb_cls(G.XR + e % kMbNRX, G.YR + e / kMbNRX)], 1)] =
+                (uint16_t)e;
     // R1 at a listed entry reads owner j's g1 there and g2 at its level-2 taps where m1_j > 0,
     // and B2 at those taps reads g2_j where m2_j > 0 (positions in the mosaic: reflected, as the
     // blend kernel addresses them)
@@ -1173,9 +1206,22 @@ __device__ __forceinline__ void mb_target(const KMbBandArgs &a, int s, int row, 
 // the reduces computed there are the reflected entries (reflect-101 about 0 commutes with the
 // 2x decimation).  At the bottom / right edges it does not (for even level sizes), so BR units
 // give level 2 the reflected level-1 rows (a history of four) and columns (source lanes).
-// This block's band of the launch (block x = band x: consecutive bands round-robin over the 8
-// XCDs; an XCD-contiguous mapping measured within noise, round 3).
-__device__ __forceinline__ int mb_band_of_block(const KMbBandArgs &a) { return (int)blockIdx.x; }
+// XCD-grouped 1-D launch of nx * ny units (x: a band or blend tile, y: its captures): block b
+// runs on XCD b % 8 (the dispatcher deals blocks round-robin), and XCD k takes the contiguous
+// unit range [k * per, (k + 1) * per), x-major -- so all captures of one band / tile run on one
+// XCD one after another, and the band's descriptors (101 KB, the same for every capture) or the
+// tile's tables come from that XCD's L2 after the first wave instead of being fetched again by
+// every capture (round 3: 0.58 GB of descriptor reads per C2 launch, every band's 32 waves spread
+// over the whole launch and over the XCDs).  False past the launch's units.
+__device__ __forceinline__ bool xcd_unit(int nx, int ny, int &x, int &y)
+{
+    const int n = nx * ny, per = (n + 7) >> 3;
+    const int u = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+    if (u >= n) return false;
+    x = u / ny;
+    y = u - x * ny;
+    return true;
+}
 
 // CN consecutive ints by one buffer store (offset past the range: nothing written).
 template <int CN>
@@ -1240,7 +1286,7 @@ constexpr int mb_lds_wait(int ph, bool first)
 // the loop holds no ordinary global load: the compiler's own vmcnt waits for ordinary loads
 // would otherwise drain the LDS-DMAs every row.
 template <int CN, int FR, bool BR, int WM>
-__device__ __forceinline__ void mb_bands_body(const KMbBandArgs &a, int bi, lds_u8 *ring)
+__device__ __forceinline__ void mb_bands_body(const KMbBandArgs &a, int bi, lds_u8 *ring, int pr)
 {
     constexpr bool AL = WM >= 1, LD = WM == 2;
     typedef __attribute__((address_space(1))) const uint8_t gu8;
@@ -1257,7 +1303,7 @@ __device__ __forceinline__ void mb_bands_body(const KMbBandArgs &a, int bi, lds_
     const KParams &P = a.P;
     const int l = threadIdx.x;
     const MbBand B = a.bands[bi];
-    const int fl0 = blockIdx.y * FR;
+    const int fl0 = pr * FR;
     if (fl0 >= a.nf) return;
     int cam, w, h;
     slot_info(P, B.slot, cam, w, h);
@@ -1429,12 +1475,16 @@ __device__ __forceinline__ void mb_bands_body(const KMbBandArgs &a, int bi, lds_
     auto level1_done = [&](int i, auto P2c, auto M3c, int f, uint32_t vl, uint32_t vh) {
         constexpr int P2 = decltype(P2c)::value, M3 = decltype(M3c)::value;
         // horizontal: level-1 entry at lane x = 2 qx reads lanes x - 2 .. x + 2
+#if MCS_EXP_BAND_PART & 2   // (timing experiment: no horizontal level-1 reduce -- wrong values)
+        uint32_t gl = vl, gh = vh;
+#else
         const uint32_t l1 = lane_prev(vl), l2 = lane_prev(l1), r1 = lane_next(vl),
                        r2 = lane_next(r1);
         const uint32_t h1_ = lane_prev(vh), h2_ = lane_prev(h1_), s1 = lane_next(vh),
                        s2 = lane_next(s1);
         uint32_t gl = (l2 + r2) + 4u * (l1 + r1) + 6u * vl;
         uint32_t gh = (h2_ + s2) + 4u * (h1_ + s1) + 6u * vh;
+#endif
         const int qy = Y1 + i;
         if constexpr (LD) {
             pend1 = i;
@@ -1462,8 +1512,24 @@ __device__ __forceinline__ void mb_bands_body(const KMbBandArgs &a, int bi, lds_
 #pragma unroll
         for (int k = 0; k < CN; k++)
             g[k] = (int)((((k & 1) ? gh : gl) >> ((k & 2) ? 16 : 0)) & 0xffffu);
+#if MCS_EXP_BAND_PART & 4   // (timing experiment: no level-2 arithmetic, zero entries stored)
+        if (P2 == 0) {
+            const int e = (i >> 1) - 2, zy = Y2 + e;
+            if (LD) {
+                pend2 = e;
+                ok2 = e >= 0 && e < kMbN2Y && zy < h2;
+            }
+            if (LD || (e >= 0 && e < kMbN2Y && zy < h2)) {
+                pend2 = e;
+#pragma unroll
+                for (int k = 0; k < CN; k++) p2[f][k] = g[k];
+            }
+        }
+        if (false) {
+#else
         // vertical: level-2 array row e reads level-1 rows 2e .. 2e + 4
         if (P2 == 0) {
+#endif
 #pragma unroll
             for (int k = 0; k < CN; k++) V2[f][(M3 + 1) % 3][k] += g[k];   // row m - 2 done
             const int e = (i >> 1) - 2, zy = Y2 + e;
@@ -1585,8 +1651,12 @@ __device__ __forceinline__ void mb_bands_body(const KMbBandArgs &a, int bi, lds_
                     r1 = wq1[b0][f];
                 }
                 v[f] = 0;
+#if MCS_EXP_BAND_PART & 1   // (timing experiment: no bilinear arithmetic -- wrong values)
+                v[f] = (r0.x ^ r1.y) & 0x00ffffffu;
+#else
 #pragma unroll
                 for (int c = 0; c < CN; c++) v[f] |= mb_tap<CN>(r0, r1, wa, wb, c, dd) << (8 * c);
+#endif
             }
             // the previous row's finished entries (after this row's window wait), then the loads:
             // windows of row r + A (its descriptor arrived a row ago), descriptor of row r + A + 1
@@ -1635,17 +1705,17 @@ __device__ __forceinline__ void mb_bands_body(const KMbBandArgs &a, int bi, lds_
 // The band pass of band bi: the aligned launch (AL) runs bands flagged for the LDS ring (MbBand
 // pad_ bit 0, band_lds_tables) in mode 2, the others in mode 1.
 template <int CN, int FR, bool BR, bool AL>
-__device__ __forceinline__ void mb_bands(const KMbBandArgs &a, int bi, lds_u8 *ring)
+__device__ __forceinline__ void mb_bands(const KMbBandArgs &a, int bi, lds_u8 *ring, int pr)
 {
     if constexpr (AL) {
         const int lds = __builtin_amdgcn_readfirstlane(a.bands[bi].pad_) & 1;
 #ifdef MCS_EXP_BAND_SKIP   // (timing experiments only: 1 = skip the global-window bands, 2 = the LDS ones)
         if (MCS_EXP_BAND_SKIP == (lds ? 2 : 1)) return;
 #endif
-        if (lds) mb_bands_body<CN, FR, BR, 2>(a, bi, ring);
-        else mb_bands_body<CN, FR, BR, 1>(a, bi, ring);
+        if (lds) mb_bands_body<CN, FR, BR, 2>(a, bi, ring, pr);
+        else mb_bands_body<CN, FR, BR, 1>(a, bi, ring, pr);
     } else {
-        mb_bands_body<CN, FR, BR, 0>(a, bi, ring);
+        mb_bands_body<CN, FR, BR, 0>(a, bi, ring, pr);
     }
 }
 
@@ -1668,11 +1738,12 @@ struct MbPix {
 
 template <int CN, int S, bool IN>
 __device__ __forceinline__ void mb_blend_tile(const KMbArgs &a, const MbGeo &G, MbBlLds<CN, S> &L,
-                                              const MbPix<CN> &px, uint32_t mask, int ns, int f)
+                                              const MbPix<CN> &px, uint32_t mask, int ns, int f,
+                                              int bt)
 {
     const KParams &P = a.P;
     const int tid = threadIdx.x, nt = blockDim.x;
-    const int32_t *tab = a.tab + (int64_t)(a.list0 + (int)blockIdx.x) * mb_tab_words(a.slots);
+    const int32_t *tab = a.tab + (int64_t)bt * mb_tab_words(a.slots);
     const int32_t *t_m1 = tab, *t_m2 = tab + a.slots * kMbNRX * kMbNRY;
     const int32_t *t_d1 = t_m2 + a.slots * kMbN2X * kMbN2Y, *t_d2 = t_d1 + kMbNRX * kMbNRY;
     // (24-bit multiplies: full-rate v_mul_u32_u24 instead of quarter-rate v_mul_lo_u32)
@@ -1709,6 +1780,8 @@ __device__ __forceinline__ void mb_blend_tile(const KMbArgs &a, const MbGeo &G, 
     const int n_r1 = t_d2[kMbN2X * kMbN2Y + 1];
     const uint16_t *t_r1 =
         reinterpret_cast<const uint16_t *>(t_d2 + kMbN2X * kMbN2Y + kMbTabCounts) + kMbTilePx;
+    // (the list is grouped by parity class, mb_prep: the zero-weight third taps of odd
+    // coordinates are skipped by whole waves)
     for (int l = tid; l < n_r1; l += nt) {
         const int e = t_r1[l];
         const int ey = div_small<kMbNRX>(e), ex = e - (int)__umul24((unsigned)ey, kMbNRX);
@@ -1716,6 +1789,7 @@ __device__ __forceinline__ void mb_blend_tile(const KMbArgs &a, const MbGeo &G, 
         int iy[3], wy[3], ix[3], wx[3];
         exp_taps<IN>(qy, G.h2, iy, wy);
         exp_taps<IN>(qx, G.w2, ix, wx);
+        const bool y3 = wy[2] != 0, x3 = wx[2] != 0;
         int tp[9], tw[9];
 #pragma unroll
         for (int u = 0; u < 3; u++)
@@ -1734,10 +1808,12 @@ __device__ __forceinline__ void mb_blend_tile(const KMbArgs &a, const MbGeo &G, 
 #pragma unroll
             for (int k = 0; k < CN; k++) e2[k] = 0;
 #pragma unroll
-            for (int t = 0; t < 9; t++)
+            for (int t = 0; t < 9; t++) {
+                if ((t >= 6 && !y3) || (t % 3 == 2 && !x3)) continue;   // zero-weight taps
 #pragma unroll
                 for (int k = 0; k < CN; k++)   // (tw <= 36, g2 < 2^24: a 24-bit multiply)
                     e2[k] += (int)__umul24((unsigned)tw[t], (unsigned)L.g2[j][k][tp[t]]);
+            }
             const uint2 g1 = L.g1[j][p1];
             const double m = (double)t_m1[__umul24((unsigned)j, kMbNRX * kMbNRY) + p1];
 #pragma unroll
@@ -1749,6 +1825,7 @@ __device__ __forceinline__ void mb_blend_tile(const KMbArgs &a, const MbGeo &G, 
         for (int k = 0; k < CN; k++) acc[k] = 0.0;
 #pragma unroll
         for (int t = 0; t < 9; t++) {
+            if ((t >= 6 && !y3) || (t % 3 == 2 && !x3)) continue;   // (adds of an exact 0)
             const double wt = (double)tw[t];
 #pragma unroll
             for (int k = 0; k < CN; k++) acc[k] += wt * L.b2[k][tp[t]];
@@ -1787,10 +1864,15 @@ __device__ __forceinline__ void mb_blend_tile(const KMbArgs &a, const MbGeo &G, 
         double acc[CN];
 #pragma unroll
         for (int k = 0; k < CN; k++) e1[k] = 0, acc[k] = 0.0;
+        // the taps in the restatement's order (rows outer); an odd coordinate's third tap has
+        // weight 0 and is skipped (it would add an exact 0) -- the list is grouped by parity
+        // class (mb_prep), so a wave skips it together
 #pragma unroll
-        for (int u = 0; u < 3; u++)
+        for (int u = 0; u < 3; u++) {
+            if (u == 2 && wy[2] == 0) break;
 #pragma unroll
             for (int v = 0; v < 3; v++) {
+                if (v == 2 && wx[2] == 0) break;
                 const int p = ir(ix[v], iy[u]), wt = wy[u] * wx[v];
                 const uint2 g1 = L.g1[s][p];
                 const double wd = (double)wt;
@@ -1800,6 +1882,7 @@ __device__ __forceinline__ void mb_blend_tile(const KMbArgs &a, const MbGeo &G, 
                     acc[k] += wd * L.r1[k][p];
                 }
             }
+        }
 #pragma unroll
         for (int k = 0; k < CN; k++) {
             const int l0 = 16384 * (int)((px.v[q] >> (8 * k)) & 0xffu) - e1[k];
@@ -1817,7 +1900,10 @@ __device__ __forceinline__ void mb_blend(const KMbArgs &a, MbBlLds<CN, S> &L)
     typedef __attribute__((address_space(1))) const uint2 cgu2;
     typedef __attribute__((address_space(1))) const int32_t cgi32;
     const KParams &P = a.P;
-    const int bt = a.list0 + (int)blockIdx.x, fl = blockIdx.y, tid = threadIdx.x;
+    // (tile, capture) units dealt XCD-grouped: a tile's captures share its tables in one L2
+    int ux, fl;
+    if (!xcd_unit(a.n_list, a.nf, ux, fl)) return;   // (block-uniform, before any barrier)
+    const int bt = a.list0 + ux, tid = threadIdx.x;
     const uint32_t mask = (uint32_t)a.list[2 + 2 * bt];
     const int ns = __popc(mask), f = a.f0 + fl;
     const MbGeo G = mb_geo(P, a.list[1 + 2 * bt]);
@@ -1884,8 +1970,8 @@ __device__ __forceinline__ void mb_blend(const KMbArgs &a, MbBlLds<CN, S> &L)
         }
     }
     __syncthreads();
-    if (G.interior) mb_blend_tile<CN, S, true>(a, G, L, px, mask, ns, f);
-    else mb_blend_tile<CN, S, false>(a, G, L, px, mask, ns, f);
+    if (G.interior) mb_blend_tile<CN, S, true>(a, G, L, px, mask, ns, f, bt);
+    else mb_blend_tile<CN, S, false>(a, G, L, px, mask, ns, f, bt);
 }
 
 }  // namespace mcs

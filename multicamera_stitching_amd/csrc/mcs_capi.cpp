@@ -26,6 +26,8 @@ struct mcs_plan {
     // prepared tables (mcs_plan_prepare): tile headers, per-pixel LDS descriptors, fallback list
     bool prepared = false;
     int gx = 0, gy = 0, n_fallback = 0;
+    int n_big = 0;                    // large-footprint tiles (mcs_stream_big, listed in d_big)
+    int *d_big = nullptr;             // (the second half of d_fallback's allocation)
     mcs::TileHdr *d_tiles = nullptr;
     uint32_t *d_desc = nullptr;
     uint32_t *d_desc4 = nullptr;      // compact per-pixel words (the streaming kernel reads these)
@@ -101,6 +103,7 @@ struct Kernels {
     bool loaded = false;
     hipFunction_t prepare[5][2] = {};     // [channels][interp]
     hipFunction_t stream[5][2] = {};      // [channels][buffer-resource DMA]
+    hipFunction_t stream_big[5][2] = {};  // large-footprint tiles, as stream
     hipFunction_t direct[5][2][2] = {};   // [channels][interp][32-bit offsets]
     hipFunction_t footprint[2] = {};
     hipFunction_t resize[5] = {};         // [channels]
@@ -135,6 +138,10 @@ int kernels(const Api *A, int device, const Kernels **out)
             rc = fn(name, &k.stream[c][0]);
             snprintf(name, sizeof(name), "mcs_stream_c%d_b32", c);
             if (rc == MCS_OK) rc = fn(name, &k.stream[c][1]);
+            snprintf(name, sizeof(name), "mcs_stream_big_c%d", c);
+            if (rc == MCS_OK) rc = fn(name, &k.stream_big[c][0]);
+            snprintf(name, sizeof(name), "mcs_stream_big_c%d_b32", c);
+            if (rc == MCS_OK) rc = fn(name, &k.stream_big[c][1]);
             snprintf(name, sizeof(name), "mcs_resize_c%d", c);
             if (rc == MCS_OK) rc = fn(name, &k.resize[c]);
             snprintf(name, sizeof(name), "mcs_mb_levels_c%d", c);
@@ -278,7 +285,7 @@ void mb_args(const mcs_plan *p, const mcs::KParams &P, mcs::KMbArgs &a)
     a.f0 = 0;
     a.nf = 0;
     a.list0 = 0;
-    a.pad_ = 0;
+    a.n_list = p->n_blend;
 }
 
 void band_args(const mcs_plan *p, const mcs::KParams &P, mcs::KMbBandArgs &a)
@@ -300,8 +307,11 @@ void band_args(const mcs_plan *p, const mcs::KParams &P, mcs::KMbBandArgs &a)
     a.band0 = 0;
     a.n_in = p->n_bands_in;
     a.band1 = p->n_bands_in;
-    a.pad_ = 0;
+    a.nb = p->n_bands;
 }
+
+// 1-D grid of an XCD-grouped launch of n units (mcs_blend.h xcd_unit): 8 * ceil(n / 8) blocks.
+unsigned xcd_grid(int64_t n) { return 8u * (unsigned)((n + 7) / 8); }
 
 // The band pass's dword-aligned window form (mb_bands AL, mb_desc's sh) applies when every used
 // camera's rows and frames are multiples of 4 bytes, its frames start at 4-byte boundaries and hold
@@ -732,6 +742,8 @@ void release_tables(const Api *A, mcs_plan *p)
     p->d_desc = nullptr;
     p->d_desc4 = nullptr;
     p->d_fallback = nullptr;
+    p->d_big = nullptr;
+    p->n_big = 0;
     p->d_owner = nullptr;
     p->d_binfo = nullptr;
     p->d_blist = nullptr;
@@ -784,23 +796,28 @@ int prepare(const Api *A, mcs_plan *p, hipStream_t s)
     HIP_TRY(A->hipMalloc((void **)&p->d_tiles, tiles * sizeof(mcs::TileHdr)));
     HIP_TRY(A->hipMalloc((void **)&p->d_desc, tiles * mcs::kTilePx * mcs::kDescWords * 4));
     HIP_TRY(A->hipMalloc((void **)&p->d_desc4, tiles * mcs::kTilePx * 4));
-    HIP_TRY(A->hipMalloc((void **)&p->d_fallback, (tiles + 1) * sizeof(int)));
+    HIP_TRY(A->hipMalloc((void **)&p->d_fallback, 2 * (tiles + 1) * sizeof(int)));
+    p->d_big = p->d_fallback + tiles + 1;
     HIP_TRY(A->hipMemsetAsync(p->d_fallback, 0, sizeof(int), s));
+    HIP_TRY(A->hipMemsetAsync(p->d_big, 0, sizeof(int), s));
     mcs::KPrepareArgs args;
     args.P = p->kp;
     args.tiles = p->d_tiles;
     args.desc = p->d_desc;
     args.desc4 = p->d_desc4;
     args.fallback = p->d_fallback;
+    args.big = p->d_big;
     size_t sz = sizeof(args);
     void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, (void *)&args, HIP_LAUNCH_PARAM_BUFFER_SIZE,
                    &sz, HIP_LAUNCH_PARAM_END};
     HIP_TRY(A->hipModuleLaunchKernel(k->prepare[p->fd.channels][p->fd.interp], p->gx, p->gy, 1,
                                      mcs::kWave, mcs::kWavesPerBlock, 1, 0, s, nullptr, cfg));
-    int nf = 0;
+    int nf = 0, nb = 0;
     HIP_TRY(A->hipMemcpyAsync(&nf, p->d_fallback, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(A->hipMemcpyAsync(&nb, p->d_big, sizeof(int), hipMemcpyDeviceToHost, s));
     HIP_TRY(A->hipStreamSynchronize(s));
     p->n_fallback = nf;
+    p->n_big = nb;
     if (!p->d_order) {
         // one launch list of every tile (the multi-band split builds its own, early tiles first)
         std::vector<int> tl(tiles);
@@ -834,8 +851,9 @@ int launch_mb_levels(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KMb
         const int form = band_form(p, b.P);
         const int kind = p->n_bands_in == 0 ? 1 : (p->n_bands > p->n_bands_in ? 2 : 0);
         if (kind == 1) b.band0 = 0;
-        return launch_args(A, k->mb_bands[p->fd.channels][form][kind], (unsigned)p->n_bands, gy,
-                           mcs::kMbBandLanes, 1, &b, sizeof(b), s);
+        return launch_args(A, k->mb_bands[p->fd.channels][form][kind],
+                           xcd_grid((int64_t)p->n_bands * gy), 1, mcs::kMbBandLanes, 1, &b,
+                           sizeof(b), s);
     }
     const unsigned gz = (unsigned)((nf + mcs::kMbLvFrames - 1) / mcs::kMbLvFrames);
     size_t sz = sizeof(m);
@@ -870,7 +888,9 @@ int launch_mb_blend(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KMbA
     m.f0 = f0;
     m.nf = nf;
     const int v = p->mb_slots <= 2 ? 0 : (p->mb_slots <= 4 ? 1 : 2);
-    return launch_args(A, k->mb_blend[p->fd.channels][v], (unsigned)p->n_blend, (unsigned)nf,
+    m.list0 = 0;
+    m.n_list = p->n_blend;
+    return launch_args(A, k->mb_blend[p->fd.channels][v], xcd_grid((int64_t)p->n_blend * nf), 1,
                        mcs::kMbBlThreads, 1, &m, sizeof(m), s);
 }
 
@@ -878,41 +898,55 @@ int launch_mb_blend(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KMbA
 // n_frames captures that share one frame stride.  Work that does not read the mosaic -- the
 // direct-gather tiles and the first multi-band chunk's level pyramids -- runs on two side streams,
 // concurrently with the HBM-bound streaming kernel.
+// Timing decomposition of the multi-band launch (variant builds only, tools/build_variant.py;
+// never the product): 1 = band pass and blend serially after the streaming kernel on the
+// caller's stream (standalone kernel times in a trace), 2 = no blend, 3 = no band pass, 4 = neither
+// (2-4 write wrong pixels).
+#ifndef MCS_EXP_MB
+#define MCS_EXP_MB 0
+#endif
+
 int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams &P, int n_frames,
                 hipStream_t s)
 {
-    const bool mb = p->blend == MCS_BLEND_MULTIBAND && p->n_blend > 0;
-    const bool fork = p->n_fallback > 0 || mb;
-    mcs::KMbArgs m;
-    if (mb) mb_args(p, P, m);
-    if (fork) HIP_TRY(A->hipEventRecord(p->ev_fork, s));
-    if (p->n_fallback > 0) {
-        HIP_TRY(A->hipStreamWaitEvent(p->side, p->ev_fork, 0));
-        mcs::KDirectArgs args;
+#if MCS_EXP_MB
+    if (p->blend == MCS_BLEND_MULTIBAND && p->n_blend > 0) {
+        mcs::KMbArgs m;
+        mb_args(p, P, m);
+        mcs::KStreamArgs args;
         args.P = P;
-        const bool off32 = offset_base(p, args.P, &args.P.base);
-        args.fallback = p->d_fallback;
+        const bool b32 = stream_base(p, P, n_frames, &args.P.base);
+        args.tiles = p->d_tiles;
+        args.desc = p->d_desc;
+        args.desc4 = p->d_desc4;
         args.n_frames = n_frames;
         args.pad_ = 0;
+        args.pad2_ = 0;
+        args.order = p->d_order;
+        args.n_order = p->n_list;
         size_t sz = sizeof(args);
         void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, (void *)&args, HIP_LAUNCH_PARAM_BUFFER_SIZE,
                        &sz, HIP_LAUNCH_PARAM_END};
-        const unsigned gy = (unsigned)((n_frames + mcs::kDirectFrames - 1) / mcs::kDirectFrames);
-        HIP_TRY(A->hipModuleLaunchKernel(k->direct[p->fd.channels][p->fd.interp][off32 ? 1 : 0],
-                                         p->n_fallback, gy, 1, mcs::kWave, mcs::kWavesPerBlock, 1,
-                                         0, p->side, nullptr, cfg));
-        HIP_TRY(A->hipEventRecord(p->ev_join, p->side));
+        HIP_TRY(A->hipModuleLaunchKernel(k->stream[p->fd.channels][b32 ? 1 : 0],
+                                         8u * (((unsigned)p->n_list + 7u) / 8u), 1, 1, mcs::kWave,
+                                         mcs::kWavesPerBlock, 1,
+                                         (unsigned)mcs::lds_stream_bytes(p->fd.channels), s,
+                                         nullptr, cfg));
+        const int nf = std::min(p->mb_chunk, n_frames);
+        int rc = MCS_OK;
+        if (MCS_EXP_MB == 1 || MCS_EXP_MB == 2) rc = launch_mb_levels(A, p, k, m, 0, nf, s);
+        if (rc == MCS_OK && (MCS_EXP_MB == 1 || MCS_EXP_MB == 3))
+            rc = launch_mb_blend(A, p, k, m, 0, nf, s);
+        return rc;
     }
-    // split (multi-band, one scratch chunk): streaming tiles under mixed pixels first, then the
-    // blend on side2 (after the band pass, those tiles and the direct-gather tiles) beside the
-    // remaining streaming tiles (same-box A/B, round 2: C2 1.009 -> 0.985 ms)
-    const bool split = mb && p->d_order && p->n_early > 0 && n_frames <= p->mb_chunk;
-    if (mb) {
-        HIP_TRY(A->hipStreamWaitEvent(p->side2, p->ev_fork, 0));
-        const int rc = launch_mb_levels(A, p, k, m, 0, std::min(p->mb_chunk, n_frames), p->side2);
-        if (rc) return rc;
-        if (!split) HIP_TRY(A->hipEventRecord(p->ev_join2, p->side2));
-    }
+#endif
+    const bool mb = p->blend == MCS_BLEND_MULTIBAND && p->n_blend > 0;
+    // side work beside the main streaming launch: the large-footprint tiles and the
+    // direct-gather tiles (tiles the main launch skips), on p->side
+    const bool aside = p->n_fallback > 0 || p->n_big > 0;
+    const bool fork = aside || mb;
+    mcs::KMbArgs m;
+    if (mb) mb_args(p, P, m);
     mcs::KStreamArgs args;
     args.P = P;
     const bool b32 = stream_base(p, P, n_frames, &args.P.base);
@@ -922,6 +956,46 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
     args.n_frames = n_frames;
     args.pad_ = 0;
     args.pad2_ = 0;
+    if (fork) HIP_TRY(A->hipEventRecord(p->ev_fork, s));
+    if (aside) HIP_TRY(A->hipStreamWaitEvent(p->side, p->ev_fork, 0));
+    if (p->n_big > 0) {
+        mcs::KStreamArgs bg = args;
+        bg.order = p->d_big + 1;
+        bg.n_order = p->n_big;
+        size_t sz = sizeof(bg);
+        void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, (void *)&bg, HIP_LAUNCH_PARAM_BUFFER_SIZE,
+                       &sz, HIP_LAUNCH_PARAM_END};
+        HIP_TRY(A->hipModuleLaunchKernel(k->stream_big[p->fd.channels][b32 ? 1 : 0],
+                                         8u * (((unsigned)p->n_big + 7u) / 8u), 1, 1, mcs::kWave,
+                                         mcs::kWavesPerBlock, 1, (unsigned)mcs::kBigStreamLds,
+                                         p->side, nullptr, cfg));
+    }
+    if (p->n_fallback > 0) {
+        mcs::KDirectArgs da;
+        da.P = P;
+        const bool off32 = offset_base(p, da.P, &da.P.base);
+        da.fallback = p->d_fallback;
+        da.n_frames = n_frames;
+        da.pad_ = 0;
+        size_t sz = sizeof(da);
+        void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, (void *)&da, HIP_LAUNCH_PARAM_BUFFER_SIZE,
+                       &sz, HIP_LAUNCH_PARAM_END};
+        const unsigned gy = (unsigned)((n_frames + mcs::kDirectFrames - 1) / mcs::kDirectFrames);
+        HIP_TRY(A->hipModuleLaunchKernel(k->direct[p->fd.channels][p->fd.interp][off32 ? 1 : 0],
+                                         p->n_fallback, gy, 1, mcs::kWave, mcs::kWavesPerBlock, 1,
+                                         0, p->side, nullptr, cfg));
+    }
+    if (aside) HIP_TRY(A->hipEventRecord(p->ev_join, p->side));
+    // split (multi-band, one scratch chunk): streaming tiles under mixed pixels first, then the
+    // blend on side2 (after the band pass, those tiles and the side tiles) beside the remaining
+    // streaming tiles (same-box A/B, round 2: C2 1.009 -> 0.985 ms)
+    const bool split = mb && p->d_order && p->n_early > 0 && n_frames <= p->mb_chunk;
+    if (mb) {
+        HIP_TRY(A->hipStreamWaitEvent(p->side2, p->ev_fork, 0));
+        const int rc = launch_mb_levels(A, p, k, m, 0, std::min(p->mb_chunk, n_frames), p->side2);
+        if (rc) return rc;
+        if (!split) HIP_TRY(A->hipEventRecord(p->ev_join2, p->side2));
+    }
     // 1-D grid dealt over the 8 XCDs; the kernel maps block -> tile (XCD-contiguous bands)
     const unsigned lds = (unsigned)mcs::lds_stream_bytes(p->fd.channels);
     auto stream_launch = [&](const int *order, int n_items) -> int {
@@ -941,7 +1015,7 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
         if (rc) return rc;
         HIP_TRY(A->hipEventRecord(p->ev_early, s));
         HIP_TRY(A->hipStreamWaitEvent(p->side2, p->ev_early, 0));
-        if (p->n_fallback > 0) HIP_TRY(A->hipStreamWaitEvent(p->side2, p->ev_join, 0));
+        if (aside) HIP_TRY(A->hipStreamWaitEvent(p->side2, p->ev_join, 0));
         rc = launch_mb_blend(A, p, k, m, 0, n_frames, p->side2);
         if (rc) return rc;
         HIP_TRY(A->hipEventRecord(p->ev_join2, p->side2));
@@ -949,7 +1023,7 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
             rc = stream_launch(p->d_order + p->n_early, p->n_list - p->n_early);
             if (rc) return rc;
         }
-        if (p->n_fallback > 0) HIP_TRY(A->hipStreamWaitEvent(s, p->ev_join, 0));
+        if (aside) HIP_TRY(A->hipStreamWaitEvent(s, p->ev_join, 0));
         HIP_TRY(A->hipStreamWaitEvent(s, p->ev_join2, 0));
         return launch_dense(A, p, k, P, n_frames, s);
     }
@@ -959,7 +1033,7 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
                                   : stream_launch(nullptr, p->gx * p->gy);
         if (rc) return rc;
     }
-    if (p->n_fallback > 0) HIP_TRY(A->hipStreamWaitEvent(s, p->ev_join, 0));
+    if (aside) HIP_TRY(A->hipStreamWaitEvent(s, p->ev_join, 0));
     if (mb) HIP_TRY(A->hipStreamWaitEvent(s, p->ev_join2, 0));
     if (p->n_blend > 0) {
         // recompute the blended tiles over the owner-sampled mosaic (same stream: ordered)
@@ -992,9 +1066,10 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
 int ensure_side(const Api *A, mcs_plan *p)
 {
     const bool mb = p->blend == MCS_BLEND_MULTIBAND && p->n_blend > 0;
-    if ((p->n_fallback > 0 || mb) && !p->ev_fork)
+    const bool aside = p->n_fallback > 0 || p->n_big > 0;
+    if ((aside || mb) && !p->ev_fork)
         HIP_TRY(A->hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming));
-    if (p->n_fallback > 0 && !p->side) {
+    if (aside && !p->side) {
         HIP_TRY(A->hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming));
         HIP_TRY(A->hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking));
     }
@@ -1758,12 +1833,12 @@ int mcs_plan_stats(const mcs_plan *p, int64_t *stats, int n)
 {
     if (!p || !stats) return mcs::fail(MCS_E_INVALID, "NULL plan/stats");
     const int64_t tiles = (int64_t)p->gx * p->gy;
-    const int64_t v[11] = {p->prepared ? 1 : 0, tiles, tiles - p->n_fallback, p->n_fallback,
+    const int64_t v[12] = {p->prepared ? 1 : 0, tiles, tiles - p->n_fallback, p->n_fallback,
                            tiles * (int64_t)(sizeof(mcs::TileHdr) +
                                              mcs::kTilePx * (mcs::kDescWords + 1) * 4),
                            p->blend, p->n_blend, p->mb_slots, p->n_degraded, p->n_bands,
-                           p->n_bands_lds};
-    for (int i = 0; i < n; i++) stats[i] = i < 11 ? v[i] : 0;
+                           p->n_bands_lds, p->n_big};
+    for (int i = 0; i < n; i++) stats[i] = i < 12 ? v[i] : 0;
     return MCS_OK;
 }
 

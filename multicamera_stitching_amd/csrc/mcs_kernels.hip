@@ -501,7 +501,7 @@ struct FootprintLds {
 
 template <int CN, int INTERP>
 __device__ __forceinline__ void prepare_tile(const KParams &P, TileHdr *tiles, uint32_t *desc,
-                                             uint32_t *desc4, int *fallback)
+                                             uint32_t *desc4, int *fallback, int *big)
 {
     __shared__ FootprintLds fl;
     __shared__ TileHdr th;
@@ -577,12 +577,18 @@ __device__ __forceinline__ void prepare_tile(const KParams &P, TileHdr *tiles, u
         const int buf = (total + kLdsSlack + 15) & ~15;
         th.buf_bytes = buf;
         th.ring = min(kMaxRing, lds_ring_bytes(CN) / buf);
-        th.fits = fits && th.ring >= 2 && total < 65536 - kLdsSlack &&
-                  jobs <= kJobsPerWave * kWavesPerBlock;
+        const bool ok = fits && total < 65536 - kLdsSlack;
+        th.fits = ok && th.ring >= 2 && jobs <= kJobsPerWave * kWavesPerBlock;
+        if (!th.fits && ok && min(kMaxRing, big_ring_bytes() / buf) >= 2 &&
+            jobs <= kBigJobsPerWave * kWavesPerBlock) {
+            th.fits = 2;
+            th.ring = min(kMaxRing, big_ring_bytes() / buf);
+        }
         th.last_shift = shifts;
         th.pad_ = 0;
         tiles[tile] = th;
-        if (!th.fits) fallback[1 + atomicAdd(&fallback[0], 1)] = tile;
+        if (th.fits == 0) fallback[1 + atomicAdd(&fallback[0], 1)] = tile;
+        if (th.fits == 2) big[1 + atomicAdd(&big[0], 1)] = tile;
     }
     __syncthreads();
     uint32_t d[kPx * kDescWords], cw[kPx];
@@ -658,22 +664,22 @@ __device__ __forceinline__ int uni(const int &v) { return __builtin_amdgcn_readf
 //   P.base, read through one buffer resource (buffer_load_dwordx4 ... offen lds), the capture's
 //   offset f * fstride in the instruction's scalar offset -- no per-row 64-bit address math;
 //   otherwise 64-bit frame-0 addresses for global_load_lds_dwordx4.
-template <bool BUF>
+template <bool BUF, int NJ>
 struct WaveJobs {
     typedef typename std::conditional<BUF, uint32_t, const uint8_t *>::type src_t;
-    src_t src[kJobsPerWave];
-    uint32_t w[kJobsPerWave];
+    src_t src[NJ];
+    uint32_t w[NJ];
     int n;
 };
 
-template <int CN, bool BUF>
-__device__ __forceinline__ WaveJobs<BUF> wave_jobs(const KParams &P, const TileHdr &h, int wave)
+template <int CN, bool BUF, int NJ>
+__device__ __forceinline__ WaveJobs<BUF, NJ> wave_jobs(const KParams &P, const TileHdr &h, int wave)
 {
-    WaveJobs<BUF> J;
+    WaveJobs<BUF, NJ> J;
     const int njobs = uni(h.njobs);
     J.n = 0;
 #pragma unroll
-    for (int jj = 0; jj < kJobsPerWave; jj++) {
+    for (int jj = 0; jj < NJ; jj++) {
         const int j = wave + jj * kWavesPerBlock;
         J.src[jj] = 0;
         J.w[jj] = 0;
@@ -702,12 +708,13 @@ __device__ __forceinline__ WaveJobs<BUF> wave_jobs(const KParams &P, const TileH
 
 // Issues capture f's footprint rows into `slot`: one LDS-DMA wave instruction per row (lane =
 // 16-byte chunk).  foff = f * fstride (fits 32 bits in BUF mode).
-template <bool BUF>
-__device__ __forceinline__ void stage_capture(const WaveJobs<BUF> &J, __amdgpu_buffer_rsrc_t rs,
-                                              uint8_t *slot, int64_t foff, int lane)
+template <bool BUF, int NJ>
+__device__ __forceinline__ void stage_capture(const WaveJobs<BUF, NJ> &J,
+                                              __amdgpu_buffer_rsrc_t rs, uint8_t *slot,
+                                              int64_t foff, int lane)
 {
 #pragma unroll
-    for (int jj = 0; jj < kJobsPerWave; jj++) {
+    for (int jj = 0; jj < NJ; jj++) {
         if (jj < J.n) {
             const uint32_t w = J.w[jj];
             // LDS destination: wave-uniform row base (M0); the hardware adds 16 * lane
@@ -755,12 +762,15 @@ __device__ __forceinline__ void wait_vmcnt_le(int n)
 // walked in list (row-major) order; vertically adjacent tiles, whose footprints overlap
 // by a few source rows, then run at about the same time on the same L2.  (Placement affects
 // speed only.)
-template <int CN, bool BUF>
+template <int CN, bool BUF, int FITS = 1>
 __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *tiles,
                                             const uint32_t *desc, const uint32_t *desc4,
                                             int n_frames, const int *order, int n_order,
                                             uint8_t *smem)
 {
+    // FITS 1: the tiles of the main launch; 2: the large-footprint tiles (kBigJobsPerWave rows per
+    // wave, kBigStreamLds bytes of LDS)
+    constexpr int NJ = FITS == 2 ? kBigJobsPerWave : kJobsPerWave;
     const int lane = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(threadIdx.y);
     const int tid = wave * kWave + lane;
     const int gx = (P.out_w + kTileW - 1) / kTileW;
@@ -779,7 +789,7 @@ __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *til
     if (tid < (int)(sizeof(TileHdr) / 4))
         reinterpret_cast<int *>(&h)[tid] = reinterpret_cast<const int *>(&tiles[tile])[tid];
     __syncthreads();
-    if (!uni(h.fits)) return;                  // handled by the direct-gather launch
+    if (uni(h.fits) != FITS) return;           // handled by another launch of the plan
     int xg, y;
     tile_pixel(bx, by, lane, wave, xg, y);
     const bool live = xg < P.out_w && y < P.out_h;
@@ -818,7 +828,7 @@ __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *til
             d[p * kDescWords + 2] = d2;
         }
     }
-    const WaveJobs<BUF> J = wave_jobs<CN, BUF>(P, h, wave);
+    const WaveJobs<BUF, NJ> J = wave_jobs<CN, BUF, NJ>(P, h, wave);
     // (BUF: raw buffer over [P.base, P.base + 4 GiB); no range clamping needed, every chunk is
     // inside a frame)
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
@@ -830,7 +840,8 @@ __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *til
     const bool wide = npx == kPx && (((uintptr_t)dst | (uintptr_t)P.out_fstride) & 3) == 0;
     const int64_t fstride = P.cam_fstride[0];
     for (int q = 0; q < ring - 1 && f_beg + q < f_end; q++)
-        stage_capture<BUF>(J, rs, ring0 + q * buf_bytes, (int64_t)(f_beg + q) * fstride, lane);
+        stage_capture<BUF, NJ>(J, rs, ring0 + q * buf_bytes, (int64_t)(f_beg + q) * fstride,
+                               lane);
     wait_vmcnt_le(0);
     __builtin_amdgcn_s_barrier();
     // Steady state: waitn = DMA instructions this wave has certainly issued after those of
@@ -844,7 +855,8 @@ __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *til
         const int ahead = f + ring - 1;
         const bool full = ahead < f_end && !MCS_EXP_NODMA;
         if (full)
-            stage_capture<BUF>(J, rs, ring0 + slot_a * buf_bytes, (int64_t)ahead * fstride, lane);
+            stage_capture<BUF, NJ>(J, rs, ring0 + slot_a * buf_bytes, (int64_t)ahead * fstride,
+                                   lane);
         const uint8_t *b = ring0 + slot_f * buf_bytes;
         if (live && !MCS_EXP_NOSTORE) {
 #if MCS_EXP_NOCOMPUTE
@@ -1013,9 +1025,9 @@ __device__ __forceinline__ void resize_px(const KResizeArgs &a)
 #define MCS_PREPARE_ENTRY(CN, IN)                                                              \
     extern "C" __global__ __launch_bounds__(512) void mcs_prepare_c##CN##_i##IN(               \
         const mcs::KParams P, mcs::TileHdr *tiles, uint32_t *desc, uint32_t *desc4,            \
-        int *fallback)                                                                         \
+        int *fallback, int *big)                                                               \
     {                                                                                          \
-        mcs::prepare_tile<CN, IN>(P, tiles, desc, desc4, fallback);                            \
+        mcs::prepare_tile<CN, IN>(P, tiles, desc, desc4, fallback, big);                       \
     }
 #ifdef MCS_STREAM_WAVES_PER_EU   // experiment knob: occupancy target of the streaming kernel
 #define MCS_STREAM_ATTR __attribute__((amdgpu_waves_per_eu(MCS_STREAM_WAVES_PER_EU)))
@@ -1034,6 +1046,13 @@ __device__ __forceinline__ void resize_px(const KResizeArgs &a)
     {                                                                                          \
         extern __shared__ __attribute__((aligned(16))) uint8_t smem[];                         \
         mcs::stream_tile<CN, BUF>(P, tiles, desc, desc4, n_frames, order, n_order, smem);      \
+    }                                                                                          \
+    extern "C" __global__ __launch_bounds__(512) void mcs_stream_big_c##CN##SUF(               \
+        const mcs::KParams P, const mcs::TileHdr *tiles, const uint32_t *desc,                \
+        const uint32_t *desc4, int n_frames, const int *order, int n_order)                    \
+    {                                                                                          \
+        extern __shared__ __attribute__((aligned(16))) uint8_t smem[];                         \
+        mcs::stream_tile<CN, BUF, 2>(P, tiles, desc, desc4, n_frames, order, n_order, smem);   \
     }
 #define MCS_DIRECT_ENTRY(CN, IN, O32)                                                          \
     extern "C" __global__ __launch_bounds__(512) void mcs_direct_c##CN##_i##IN##_o##O32(       \
@@ -1115,26 +1134,32 @@ extern "C" __global__ __launch_bounds__(256) void mcs_blend_classify(const mcs::
         const mcs::KMbBandArgs a)                                                              \
     {                                                                                          \
         MCS_MB_BAND_RING(AL);                                                                  \
-        const int bl = mcs::mb_band_of_block(a);                                               \
-        if (bl >= 0) mcs::mb_bands<CN, mcs::kMbBandFrames, false, AL>(a, a.band0 + bl, ring);  \
+        int bl, pr;                                                                            \
+        if (!mcs::xcd_unit(a.nb, (a.nf + mcs::kMbBandFrames - 1) / mcs::kMbBandFrames, bl, pr)) \
+            return;                                                                            \
+        mcs::mb_bands<CN, mcs::kMbBandFrames, false, AL>(a, a.band0 + bl, ring, pr);          \
     }                                                                                          \
     extern "C" __global__ __launch_bounds__(64) MCS_MB_BAND_ATTR(CN) void                     \
         mcs_mb_bands_br##SFX##_c##CN(                                                          \
         const mcs::KMbBandArgs a)                                                              \
     {                                                                                          \
         MCS_MB_BAND_RING(AL);                                                                  \
-        const int bl = mcs::mb_band_of_block(a);                                               \
-        if (bl >= 0) mcs::mb_bands<CN, mcs::kMbBandFrames, true, AL>(a, a.band0 + bl, ring);   \
+        int bl, pr;                                                                            \
+        if (!mcs::xcd_unit(a.nb, (a.nf + mcs::kMbBandFrames - 1) / mcs::kMbBandFrames, bl, pr)) \
+            return;                                                                            \
+        mcs::mb_bands<CN, mcs::kMbBandFrames, true, AL>(a, a.band0 + bl, ring, pr);           \
     }                                                                                          \
     extern "C" __global__ __launch_bounds__(64) MCS_MB_BAND_ATTR(CN) void                     \
         mcs_mb_bands_all##SFX##_c##CN(                                                         \
         const mcs::KMbBandArgs a)                                                              \
     {                                                                                          \
         MCS_MB_BAND_RING(AL);                                                                  \
-        const int bl = mcs::mb_band_of_block(a);                                               \
-        if (bl < 0) return;                                                                    \
-        if (bl < a.n_in) mcs::mb_bands<CN, mcs::kMbBandFrames, false, AL>(a, a.band0 + bl, ring); \
-        else mcs::mb_bands<CN, mcs::kMbBandFrames, true, AL>(a, a.band1 + bl - a.n_in, ring);  \
+        int bl, pr;                                                                            \
+        if (!mcs::xcd_unit(a.nb, (a.nf + mcs::kMbBandFrames - 1) / mcs::kMbBandFrames, bl, pr)) \
+            return;                                                                            \
+        if (bl < a.n_in)                                                                       \
+            mcs::mb_bands<CN, mcs::kMbBandFrames, false, AL>(a, a.band0 + bl, ring, pr);      \
+        else mcs::mb_bands<CN, mcs::kMbBandFrames, true, AL>(a, a.band1 + bl - a.n_in, ring, pr); \
     }
 #define MCS_MB_ENTRY(CN)                                                                       \
     extern "C" __global__ __launch_bounds__(MCS_MB_LV_THREADS) __attribute__((amdgpu_waves_per_eu(MCS_MB_WAVES))) \

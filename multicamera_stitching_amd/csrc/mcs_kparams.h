@@ -94,7 +94,8 @@ constexpr uint32_t kCwZero = 1u << 29;       // no live tap (no camera): output 
 constexpr uint32_t kCwFull = 1u << 30;       // read the full form
 constexpr uint32_t kCwOneRow = 1u << 31;     // fy = 0: row 1 unused (= row 0)
 struct TileHdr {
-    int fits;                      // 1: LDS path, 0: listed for the direct-gather launch
+    int fits;                      // 1: LDS path, 2: the large-footprint LDS path (mcs_stream_big),
+                                   // 0: listed for the direct-gather launch
     int ncam, njobs, ring, buf_bytes;
     // stride[k]: LDS row pitch (bits 0-15) | 16-byte DMA chunks per row (bits 16-23)
     int cam[kTileCams], rmin[kTileCams], cal[kTileCams], stride[kTileCams], base[kTileCams];
@@ -113,7 +114,8 @@ struct KPrepareArgs {
     TileHdr *tiles;
     uint32_t *desc;
     uint32_t *desc4;               // compact words (kCw*), 4 per lane
-    int *fallback;                 // [0] = count, then tile indices
+    int *fallback;                 // [0] = count, then tile indices (direct-gather tiles)
+    int *big;                      // [0] = count, then tile indices (large-footprint tiles)
 };
 struct KStreamArgs {
     KParams P;
@@ -220,7 +222,8 @@ struct KMbArgs {
     int slots;                     // owners per tile (the tables' slot dimension)
     int chunk;                     // scratch capture stride
     int f0, nf;                    // captures [f0, f0 + nf) of this launch
-    int list0, pad_;               // blend: first list entry of this launch (block x: list0 + x)
+    int list0;                     // blend: first list entry of this launch
+    int n_list;                    // blend: list entries in this launch (xcd_unit's nx)
 };
 
 // Band pass of the multi-band levels (mcs_mb_bands_c*): one wave per (band, kMbBandFrames
@@ -313,7 +316,8 @@ struct KMbBandArgs {
     int n_in;                      // mcs_mb_bands_all: blocks below n_in take the interior path
                                    // (band band0 + block), the others the _br path (band
                                    // band1 + block - n_in)
-    int band1, pad_;
+    int band1;
+    int nb;                        // bands in this launch (xcd_unit's nx)
 };
 struct KBlendArgs {
     KParams P;
@@ -342,6 +346,14 @@ constexpr int kMaxRing = 6;
 #endif
 constexpr int lds_stream_bytes(int cn) { return cn >= 3 ? MCS_STREAM_LDS : 40960; }
 constexpr int lds_ring_bytes(int cn) { return lds_stream_bytes(cn) - (int)sizeof(TileHdr); }
+// Large-footprint tiles (TileHdr::fits == 2): the tiles whose footprints exceed the streaming
+// block's budget -- the C4 cylinder's top and bottom tiles, whose rows curve over ~45 source rows
+// per camera, two cameras at a seam -- run the same streaming code with 16 footprint rows per
+// wave and a 120 KiB ring (one block per CU) over their own list, on the side stream beside the
+// main launch (round 3 sent these 39 C4 tiles to the direct-gather kernel).
+constexpr int kBigJobsPerWave = 16;
+constexpr int kBigStreamLds = 120 * 1024;
+constexpr int big_ring_bytes() { return kBigStreamLds - (int)sizeof(TileHdr); }
 // LDS row pitch of a footprint row of `bytes` DMA bytes.  The 32 lanes of an output row read
 // dwords ~3 apart (C = 3, 4 pixels per lane: a permutation of the 32 ds_read_b32 banks); where
 // the source row changes inside the lane group (a rotated map), the lanes past the change read

@@ -3,13 +3,128 @@
 // per slot into a hipGraph) on the compute stream, D2H on a second copy stream, so that the
 // upload of capture i+1, the stitch of capture i and the download of capture i-1 overlap.  Uses
 // only the public plan API (mcs_stitch_device) plus the bound HIP runtime.
+#include <sched.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cstring>
+#include <deque>
+#include <functional>
+#include <mutex>
 #include <new>
+#include <thread>
+#include <vector>
 
 #include "mcs_common.h"
 
 namespace {
 constexpr int kMaxDepth = 8;
+
+// Host staging copies (caller frames -> pinned slot, pinned slot -> caller mosaic) split over a
+// few worker threads: one thread's memcpy into pinned memory runs at ~30 GB/s, under the PCIe
+// link it feeds (round 3: the non-zero-copy C5 path reached 0.27 of the link), so the
+// double-buffered H2D pipeline needs several.  Chunks of >= kCopyChunk bytes.
+constexpr size_t kCopyChunk = 2u << 20;
+
+class CopyPool {
+public:
+    static CopyPool &get()
+    {
+        static CopyPool *p = new CopyPool(workers());
+        return *p;
+    }
+    int size() const { return n_; }
+    // Runs every copy job -- `rows` rows of `row` bytes, dense at dst, src_pitch apart at src --
+    // the calling thread taking a share, and returns when all are done.
+    struct Job {
+        uint8_t *dst;
+        const uint8_t *src;
+        size_t row, rows, src_pitch;
+    };
+    void copy(const std::vector<Job> &jobs)
+    {
+        std::vector<Job> chunks;   // pieces of about kCopyChunk bytes
+        for (const Job &j : jobs) {
+            if (j.src_pitch == j.row) {
+                const size_t bytes = j.row * j.rows;
+                for (size_t o = 0; o < bytes; o += kCopyChunk)
+                    chunks.push_back({j.dst + o, j.src + o, std::min(kCopyChunk, bytes - o), 1,
+                                      0});
+                continue;
+            }
+            const size_t per = std::max<size_t>(1, kCopyChunk / std::max<size_t>(j.row, 1));
+            for (size_t r = 0; r < j.rows; r += per)
+                chunks.push_back({j.dst + r * j.row, j.src + r * j.src_pitch, j.row,
+                                  std::min(per, j.rows - r), j.src_pitch});
+        }
+        auto one = [](const Job &c) {
+            for (size_t r = 0; r < c.rows; r++)
+                memcpy(c.dst + r * c.row, c.src + r * c.src_pitch, c.row);
+        };
+        if (chunks.size() <= 1 || n_ == 0) {
+            for (const Job &c : chunks) one(c);
+            return;
+        }
+        std::atomic<size_t> next{0};
+        int left = 0;
+        std::mutex m;
+        std::condition_variable done;
+        auto work = [&] {
+            for (size_t i; (i = next.fetch_add(1)) < chunks.size();) one(chunks[i]);
+        };
+        const int helpers = (int)std::min<size_t>((size_t)n_, chunks.size() - 1);
+        left = helpers;
+        for (int h = 0; h < helpers; h++)
+            run([&] {
+                work();
+                std::lock_guard<std::mutex> lk(m);
+                if (--left == 0) done.notify_one();
+            });
+        work();
+        std::unique_lock<std::mutex> lk(m);
+        done.wait(lk, [&] { return left == 0; });
+    }
+
+private:
+    static int workers()
+    {
+        // the CPUs this process may run on (the GPU box's cgroup leaves 16 of nproc), capped:
+        // a handful of memcpy threads saturate the host memory the link reads
+        cpu_set_t set;
+        const int cpus = sched_getaffinity(0, sizeof(set), &set) == 0 ? CPU_COUNT(&set) : 1;
+        return std::max(0, std::min(7, cpus / 2 - 1));
+    }
+    explicit CopyPool(int n) : n_(n)
+    {
+        for (int i = 0; i < n; i++) std::thread([this] { loop(); }).detach();
+    }
+    void run(std::function<void()> f)
+    {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            q_.push_back(std::move(f));
+        }
+        cv_.notify_one();
+    }
+    void loop()
+    {
+        for (;;) {
+            std::function<void()> f;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [this] { return !q_.empty(); });
+                f = std::move(q_.front());
+                q_.pop_front();
+            }
+            f();
+        }
+    }
+    int n_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<std::function<void()>> q_;
+};
 }
 
 struct mcs_stream {
@@ -196,19 +311,18 @@ int mcs_stream_submit_strided(mcs_stream *s, const uint8_t *const *cams,
     if (sl.busy)
         return mcs::fail(MCS_E_INVALID, "slot %d not yet collected (call mcs_stream_wait)", i);
     mcs::DeviceGuard g(A, s->device);
-    if (cams)   // else: the caller filled mcs_stream_input() buffers in place
+    if (cams) {   // else: the caller filled mcs_stream_input() buffers in place
+        // (a camera inside a wider frame, e.g. the main_stream layout with cameras side by side
+        // on axis 1, is gathered row by row into its dense staging slot)
+        std::vector<CopyPool::Job> jobs;
         for (int c = 0; c < s->n_cams; c++) {
             if (!cams[c]) continue;
             const size_t row = (size_t)s->cam_w[c] * s->channels;
-            if (!row_pitch || row_pitch[c] == (int64_t)row) {
-                memcpy(sl.h_in + s->cam_off[c], cams[c], row * s->cam_h[c]);
-                continue;
-            }
-            // a camera inside a wider frame (e.g. the main_stream layout, cameras side by side
-            // on axis 1): gathered row by row into its dense staging slot
-            for (int y = 0; y < s->cam_h[c]; y++)
-                memcpy(sl.h_in + s->cam_off[c] + y * row, cams[c] + y * row_pitch[c], row);
+            jobs.push_back({sl.h_in + s->cam_off[c], cams[c], row, (size_t)s->cam_h[c],
+                            row_pitch ? (size_t)row_pitch[c] : row});
         }
+        CopyPool::get().copy(jobs);
+    }
     HIP_TRY(A->hipMemcpyAsync(sl.d_in, sl.h_in, s->in_bytes, hipMemcpyHostToDevice, s->up));
     HIP_TRY(A->hipEventRecord(sl.ev_in, s->up));
     HIP_TRY(A->hipStreamWaitEvent(s->compute, sl.ev_in, 0));
@@ -238,7 +352,7 @@ int mcs_stream_wait(mcs_stream *s, int slot, uint8_t *out)
     if (!A) return MCS_E_HIP;
     mcs::DeviceGuard g(A, s->device);
     HIP_TRY(A->hipEventSynchronize(sl.ev_out));
-    if (out) memcpy(out, sl.h_out, s->out_bytes);
+    if (out) CopyPool::get().copy({{out, sl.h_out, s->out_bytes, 1, s->out_bytes}});
     sl.busy = false;
     return MCS_OK;
 }

@@ -304,15 +304,23 @@ BLEND_MULTIBAND = 2
 BLEND_SEAM = 3
 
 
-def _seam_buf(ow, oh, seam_k):
+def _seam_buf(ow, oh, seam_k, seam_labels=None):
+    """(k argument, label buffer): seam_labels (the 2^seam_k grid, e.g. a plan's graph-cut seams
+    found once from another capture) are passed in as k + 256 (orc_blend.c)."""
     if seam_k is None or seam_k < 0:
         return -1, np.zeros(1, np.uint8)
     k = int(seam_k)
-    return k, np.zeros((((oh + (1 << k) - 1) >> k), ((ow + (1 << k) - 1) >> k)), np.uint8)
+    shape = (((oh + (1 << k) - 1) >> k), ((ow + (1 << k) - 1) >> k))
+    if seam_labels is not None:
+        lab = np.ascontiguousarray(seam_labels, np.uint8).copy()
+        if lab.shape != shape:
+            raise ValueError(f"seam labels {lab.shape}, grid {shape}")
+        return k + 256, lab
+    return k, np.zeros(shape, np.uint8)
 
 
 def blend_stitch(flat: dict, cams, mode: int, interp: int = INTER_LINEAR, want_owner=False,
-                 seam_k=None, want_seams=False):
+                 seam_k=None, want_seams=False, seam_labels=None):
     """Blended mosaic of the plan's geometry (orc_blend.c: FEATHER = 1, MULTIBAND = 2,
     SEAM = 3).  flat: mcs_plan_describe dict; cams: all cameras in sorted-label order,
     calibrated sizes.  seam_k: graph-cut seams on the 2^k grid (orc_seam.c), None = distance."""
@@ -330,7 +338,7 @@ def blend_stitch(flat: dict, cams, mode: int, interp: int = INTER_LINEAR, want_o
     ptrs = (ctypes.c_void_p * len(cams))(*[c.ctypes.data for c in cams])
     cw = np.array([c.shape[1] for c in cams], np.int32)
     ch = np.array([c.shape[0] for c in cams], np.int32)
-    k, lab = _seam_buf(ow, oh, seam_k)
+    k, lab = _seam_buf(ow, oh, seam_k, seam_labels)
     rc = lib().orc_blend_stitch(n, _p(offx), _p(offy), _p(minv), _p(bw0), _p(scam), ptrs, _p(cw),
                                 _p(ch), cn, interp, mode, _p(out), ow, oh, _p(owner), k, _p(lab))
     if rc != 0:
@@ -345,7 +353,7 @@ def _ret(out, owner, lab, want_owner, want_seams):
 
 def blend_stitch_cyl(rig: list, out_w: int, out_h: int, f_cyl: float, u0: float, v0: float,
                      cams, mode: int, interp: int = INTER_LINEAR, want_owner=False, seam_k=None,
-                     want_seams=False):
+                     want_seams=False, seam_labels=None):
     """Cylindrical panorama (orc_blend.c orc_blend_stitch_cyl): rig = [dict(R, f, cx, cy)] per
     camera (as mcs_plan_create_cylindrical), cams = the frames; owner values = camera index."""
     n = len(rig)
@@ -361,7 +369,7 @@ def blend_stitch_cyl(rig: list, out_w: int, out_h: int, f_cyl: float, u0: float,
     ptrs = (ctypes.c_void_p * n)(*[c.ctypes.data for c in cams])
     cw = np.array([c.shape[1] for c in cams], np.int32)
     ch = np.array([c.shape[0] for c in cams], np.int32)
-    k, lab = _seam_buf(out_w, out_h, seam_k)
+    k, lab = _seam_buf(out_w, out_h, seam_k, seam_labels)
     rc = lib().orc_blend_stitch_cyl(n, _p(R), _p(f), _p(cx), _p(cy), float(f_cyl), float(u0),
                                     float(v0), ptrs, _p(cw), _p(ch), cn, interp, mode, _p(out),
                                     int(out_w), int(out_h), _p(owner), k, _p(lab))

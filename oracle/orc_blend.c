@@ -39,7 +39,8 @@
  *   on the samples and the owner map only).
  * SEAM: out = I_owner (the seam without blending), 0 where no slot covers p.
  * Graph-cut seams (seam_k >= 0, orc_seam.c): the owner is the seam label's camera when it
- *   covers p (d >= 0), else the distance owner above.
+ *   covers p (d >= 0), else the distance owner above.  seam_k >= 256: the labels of the
+ *   2^(seam_k - 256) grid are the caller's (found once per plan, from one capture).
  * Cylindrical rigs (orc_blend_stitch_cyl, NS-6): slot s = camera s, positions from
  *   orc__cyl_xy over the panorama's per-column (sin t, cos t) and per-row h, t = (u - u0) / fc,
  *   h = (v - v0) / fc (libm sin/cos, once per column); the rest as above.
@@ -254,8 +255,12 @@ static int blend_core(const geo_t *geo, int S, const int *scam, const uint8_t *c
                       int ow, int oh, uint8_t *owner_out, int seam_k, uint8_t *seam_lab)
 {
     const long npx = (long)ow * oh;
+    /* seam_k >= 256: the labels of the 2^(seam_k - 256) grid are given in seam_lab (a plan's
+     * seams are found once, from one capture, and then serve every capture) */
+    const int given = seam_k >= 256;
+    if (given) seam_k -= 256;
     const int gw = seam_k >= 0 ? (ow + (1 << seam_k) - 1) >> seam_k : 0;
-    if (seam_k >= 0 &&
+    if (seam_k >= 0 && !given &&
         seam_labels(geo, S, scam, cams, cw, ch, cn, interp, ow, oh, seam_k, seam_lab) != 0)
         return -1;
     uint8_t *owner = (uint8_t *)malloc((size_t)npx);

@@ -48,6 +48,27 @@ def test_warp_plan_vs_oracle(case, interp):
     assert _diff(got, want) == 0
 
 
+@pytest.mark.parametrize("M, src, dst, path", [
+    # vertical zoom-out x5: a 16-row tile reads ~80 source rows (> 64 rows of the main streaming
+    # block): the large-footprint streaming launch (mcs_stream_big, 16 rows per wave)
+    ([[1.0, 0.0, 0.0], [0.0, 0.2, 0.0], [0.0, 0.0, 1.0]], (400, 1000), (400, 200), "big_tiles"),
+    # and x0.1 horizontally too: 1280 source columns per tile row (> 1 KiB per DMA row): the
+    # direct-gather kernel
+    ([[0.1, 0.0, 0.0], [0.0, 0.2, 0.0], [0.0, 0.0, 1.0]], (3000, 1000), (300, 200), "direct_tiles"),
+])
+def test_warp_plan_side_paths_vs_oracle(M, src, dst, path):
+    """Tiles whose source footprints exceed the main streaming block take the side launches --
+    the large-footprint streaming kernel or the direct gather -- and stay bit-exact."""
+    from multicamera_stitching_amd import _capi, rig
+    img = rig.texture(src[1], src[0], 3, seed=5)
+    plan = _capi.Plan.warp(np.array(M), src[0], src[1], dst[0], dst[1], 3)
+    got = plan.stitch_host([img]).reshape(dst[1], dst[0], 3)
+    st = plan.stats()
+    assert st[path] > 0, st
+    want = oracle.warp_perspective(img, M, dst, 1)
+    assert _diff(got, want) == 0
+
+
 def test_undistort_device_batch():
     """A batch of captures through one undistortion plan (device-resident)."""
     import torch
