@@ -340,6 +340,9 @@ def main():
                      "lds_tiles": plan_stats["lds_tiles"],
                      "direct_tiles": plan_stats["direct_tiles"],
                      "blend_tiles_32x64": plan_stats["blend_tiles"],
+                     "mb_bands": plan_stats["mb_bands"],
+                     "mb_mixed_px_per_capture": plan_stats["mb_mixed_px"],
+                     "mb_r1_entries_per_capture": plan_stats["mb_r1_entries"],
                      "table_mb": round(plan_stats["table_bytes"] / 1e6, 2),
                      "seams": None if seam_k is None else {
                          "method": "graph-cut (mcs_plan_find_seams, device push-relabel)",

@@ -159,7 +159,8 @@ int mcs_plan_prepare(mcs_plan *plan, void *stream);
  * neighbourhood -- the tile grown by 16 px -- holds more than 8 owners), multi-band bands of the
  * level pass, of those the bands whose source rows are staged in the LDS ring (the rest read
  * their windows from global memory), and of the LDS-path tiles those whose footprints need the
- * large-footprint streaming launch (16 rows per wave, 120 KiB ring).  Entries past 11 read 0. */
+ * large-footprint streaming launch (16 rows per wave, 120 KiB ring), then per capture the
+ * multi-band blend's computed ("mixed") pixels and R1 entries.  Entries past 13 read 0. */
 int mcs_plan_stats(const mcs_plan *plan, int64_t *stats, int n);
 
 /* Blend mode of the plan (MCS_BLEND_*; default NONE = the reference's paste).  Changing it drops

@@ -14,7 +14,8 @@
 // Both are a few percent of the mosaic's tiles for a linear rig.
 #pragma once
 // Band-pass timing decomposition (variant builds only, never the product): bit 0 = no bilinear
-// arithmetic, bit 1 = no horizontal level-1 reduce, bit 2 = no level-2 arithmetic (wrong values).
+// arithmetic, bit 1 = no horizontal level-1 reduce, bit 2 = no level-2 arithmetic, bit 3 = no
+// level stores, bit 4 = no descriptor refresh (wrong values).
 #ifndef MCS_EXP_BAND_PART
 #define MCS_EXP_BAND_PART 0
 #endif
@@ -430,6 +431,24 @@ __device__ __forceinline__ uint2 mb_desc(const MbSrc &q, int w, int h)
 
 // The 8 bytes starting sh (<= 10) bytes into a 12-byte window, zero past its end (v_alignbyte
 // funnel shifts).
+// 6 a + b for packed u16 pairs whose product does not fit 24 bits, as two full-rate shift-adds
+// (the compiler otherwise emits the multiply as a v_mad_u64_u32)
+__device__ __forceinline__ uint32_t mad6_u32(uint32_t a, uint32_t b)
+{
+    uint32_t t, r;
+    asm("v_lshl_add_u32 %0, %1, 1, %2" : "=v"(t) : "v"(a), "v"(b));
+    asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(r) : "v"(a), "v"(t));
+    return r;
+}
+
+// The LDS-ring window (mb_bands_body mode 2): 4-byte aligned in the ring, byte shift sh < 4, so
+// the 8 bytes are two alignbytes (no third dword's select as in mb_win_shift).
+__device__ __forceinline__ uint2 mb_win_shift4(uint3 v, uint32_t sh)
+{
+    return make_uint2(__builtin_amdgcn_alignbyte(v.y, v.x, sh & 3u),
+                      __builtin_amdgcn_alignbyte(v.z, v.y, sh & 3u));
+}
+
 template <int CN>
 __device__ __forceinline__ uint2 mb_win_shift(uint3 v, uint32_t sh)
 {
@@ -466,6 +485,19 @@ __device__ __forceinline__ void mb_weights(uint32_t meta, uint32_t &wa, uint32_t
     wb = wx * (fy << 5);
 }
 
+// mb_weights with every weight doubled, min(2 w, 65535) (the stitch kernels' w2x): a channel's
+// mb_tap2 sum then carries mb_tap's (sum p w + 2^14) >> 15 in its byte 2 -- s = 2 sum p w + 2^15
+// < 2^24; the one weight 2 w = 65536 (fx' = 0 or 32 with fy = 0: all on one pixel) clamps to
+// 65535, and 65535 p + 2^15 still has p in byte 2 -- so the band pass packs channels with one
+// v_perm instead of shifting, masking and or-ing each.
+__device__ __forceinline__ void mb_weights2(uint32_t meta, uint32_t &wa, uint32_t &wb)
+{
+    const uint32_t fx = meta & 63u, fy = (meta >> 6) & 31u;
+    const uint32_t ya = (32u - fy) << 6, yb = fy << 6;
+    wa = min((32u - fx) * ya, 65535u) | (min(fx * ya, 65535u) << 16);
+    wb = min((32u - fx) * yb, 65535u) | (min(fx * yb, 65535u) << 16);
+}
+
 // Channel k of a descriptor's sample from its two (shifted) row windows.
 template <int CN>
 __device__ __forceinline__ uint32_t mb_tap(uint2 r0, uint2 r1, uint32_t wa, uint32_t wb, int k,
@@ -480,6 +512,22 @@ __device__ __forceinline__ uint32_t mb_tap(uint2 r0, uint2 r1, uint32_t wa, uint
                                         16384u, false);
     v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, a1), __builtin_bit_cast(us2, wb), v, false);
     return v >> 15;
+}
+
+// Channel k of a sample with mb_weights2's doubled weights: the value is byte 2 of the result.
+template <int CN>
+__device__ __forceinline__ uint32_t mb_tap2(uint2 r0, uint2 r1, uint32_t wa, uint32_t wb, int k,
+                                            uint32_t d)
+{
+    typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+    const uint32_t sel = ((uint32_t)k | (0x0cu << 8) | ((uint32_t)(CN + k) << 16) | (0x0cu << 24)) +
+                         d * 0x00010001u;
+    const uint32_t a0 = __builtin_amdgcn_perm(r0.y, r0.x, sel);
+    const uint32_t a1 = __builtin_amdgcn_perm(r1.y, r1.x, sel);
+    const uint32_t v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, a0),
+                                              __builtin_bit_cast(us2, wa), 32768u, false);
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(us2, a1), __builtin_bit_cast(us2, wb), v,
+                                  false);
 }
 
 // Makes a register array opaque to the optimiser (one asm per capture): values derived from it
@@ -1122,13 +1170,15 @@ __device__ __forceinline__ void mb_bdesc(const KMbBandArgs &a)
 }
 
 // Value of lane l + 1 / l - 1 of the wave (DPP wave_shl:1 / wave_shr:1; the end lanes get 0).
+// (bound_ctrl: a lane without a source reads 0 -- the edge lanes' value -- so no `old` register
+// has to be zeroed before every DPP move)
 __device__ __forceinline__ uint32_t lane_next(uint32_t v)
 {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, false);
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, true);
 }
 __device__ __forceinline__ uint32_t lane_prev(uint32_t v)
 {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false);
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, true);
 }
 // Value of lane `src` (byte address src * 4: ds_bpermute).
 __device__ __forceinline__ int lane_at(int v, int src4)
@@ -1359,7 +1409,7 @@ __device__ __forceinline__ void mb_bands_body(const KMbBandArgs &a, int bi, lds_
     g8 *const g1b = (g8 *)a.g1, *const g2b = (g8 *)a.g2;
     const uint64_t *dsc = a.bdesc + (int64_t)bi * kMbBandDescRows * kMbBandLanes + l;
     const int nst = min(FR, a.nf - fl0);
-    const uint32_t M = 0x00ff00ffu;
+    [[maybe_unused]] const uint32_t M = 0x00ff00ffu;   // (timing experiments only)
     // Rolling vertical sums, indexed by row % 3 (compile-time inside the 12-row body): level-1
     // rows (packed u16: lo = channels 0, 2; hi = 1, 3), level-2 rows (one int per channel).  A
     // row's sum starts with '=' at its first input row, so the rows before the array (and the
@@ -1418,6 +1468,9 @@ __device__ __forceinline__ void mb_bands_body(const KMbBandArgs &a, int bi, lds_
     const __amdgpu_buffer_rsrc_t rs2 = __builtin_amdgcn_make_buffer_rsrc((void *)a.g2, 0, 0x7fffffff, 0x00020000);
     auto flush_ld = [&](auto PHc) {
         constexpr int ph = decltype(PHc)::value;
+#if MCS_EXP_BAND_PART & 8   // (timing experiment: no level stores)
+        return;
+#endif
         constexpr uint32_t none = 0xfffffff0u;
         if constexpr (ph & 1) {
 #pragma unroll
@@ -1482,8 +1535,8 @@ __device__ __forceinline__ void mb_bands_body(const KMbBandArgs &a, int bi, lds_
                        r2 = lane_next(r1);
         const uint32_t h1_ = lane_prev(vh), h2_ = lane_prev(h1_), s1 = lane_next(vh),
                        s2 = lane_next(s1);
-        uint32_t gl = (l2 + r2) + 4u * (l1 + r1) + 6u * vl;
-        uint32_t gh = (h2_ + s2) + 4u * (h1_ + s1) + 6u * vh;
+        uint32_t gl = mad6_u32(vl, (l2 + r2) + 4u * (l1 + r1));
+        uint32_t gh = mad6_u32(vh, (h2_ + s2) + 4u * (h1_ + s1));
 #endif
         const int qy = Y1 + i;
         if constexpr (LD) {
@@ -1579,6 +1632,9 @@ __device__ __forceinline__ void mb_bands_body(const KMbBandArgs &a, int bi, lds_
     constexpr int NL = kMbLdsDescRing;
     const uint4 *d16 = a.bdesc16 + (int64_t)bi * kMbLdsDescRows * kMbBandLanes + l;
     auto issue_desc = [&](int row) {   // descriptor row `row` into ring slot row % NL
+#if MCS_EXP_BAND_PART & 16   // (timing experiment: descriptors staged once, never refreshed)
+        if (row >= NL) return;
+#endif
         __builtin_amdgcn_global_load_lds(d16 + row * kMbBandLanes,
                                          dring + (row % NL) * kMbBandLanes * 16, 16, 0, 0);
         asm volatile("" ::: "memory");
@@ -1623,25 +1679,31 @@ __device__ __forceinline__ void mb_bands_body(const KMbBandArgs &a, int bi, lds_
                     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(mb_lds_wait<FR, NL>(ph, true)) : "memory");
                 else
                     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(mb_lds_wait<FR, NL>(ph, false)) : "memory");
+                // (ring descriptor: windows + shift, and the doubled weights precomputed on the
+                // host, band_lds_tables)
                 const lu32 *dd = (const lu32 *)(dring + (ph % NL) * kMbBandLanes * 16 + l * 16);
                 dxr = dd[0];
-                meta = dd[1];
+                wa = dd[1];
+                wb = dd[3];
+                meta = 0u;
             } else {
                 dxr = (uint32_t)dq[d0];
                 meta = (uint32_t)(dq[d0] >> 32);
+                mb_weights2(meta, wa, wb);
             }
             const uint32_t dd = AL ? 0u : (meta >> 12) & 7u;
-            mb_weights(meta, wa, wb);
-            uint32_t v[FR];
+            // per capture the sample's channels as packed u16 pairs: pl = (ch 0, ch 2), ph = (ch
+            // 1, ch 3), each channel from byte 2 of its mb_tap2 sum
+            uint32_t pls[FR], phs[FR];
 #pragma unroll
             for (int f = 0; f < FR; f++) {
                 uint2 r0, r1;
                 if constexpr (LD) {
-                    const uint32_t dx = dxr, sh = (meta >> 15) & 15u;
-                    const lu32 *pa = (const lu32 *)(ring + f * kMbLdsRingBytes + (dx & 0xffffu));
+                    const uint32_t dx = dxr, sh = (dx >> 14) & 3u;
+                    const lu32 *pa = (const lu32 *)(ring + f * kMbLdsRingBytes + (dx & 0x3fffu));
                     const lu32 *pb = (const lu32 *)(ring + f * kMbLdsRingBytes + (dx >> 16));
-                    r0 = mb_win_shift<CN>(make_uint3(pa[0], pa[1], pa[2]), sh);
-                    r1 = mb_win_shift<CN>(make_uint3(pb[0], pb[1], pb[2]), sh);
+                    r0 = mb_win_shift4(make_uint3(pa[0], pa[1], pa[2]), sh);
+                    r1 = mb_win_shift4(make_uint3(pb[0], pb[1], pb[2]), sh);
                 } else if constexpr (AL) {
                     const uint32_t sh = (meta >> 15) & 15u;
                     r0 = mb_win_shift<CN>(wq0[b0][f], sh);
@@ -1650,12 +1712,18 @@ __device__ __forceinline__ void mb_bands_body(const KMbBandArgs &a, int bi, lds_
                     r0 = wq0[b0][f];
                     r1 = wq1[b0][f];
                 }
-                v[f] = 0;
 #if MCS_EXP_BAND_PART & 1   // (timing experiment: no bilinear arithmetic -- wrong values)
-                v[f] = (r0.x ^ r1.y) & 0x00ffffffu;
+                pls[f] = (r0.x ^ r1.y) & M;
+                phs[f] = (r0.y ^ r1.x) & M;
 #else
+                uint32_t t[4];
 #pragma unroll
-                for (int c = 0; c < CN; c++) v[f] |= mb_tap<CN>(r0, r1, wa, wb, c, dd) << (8 * c);
+                for (int c = 0; c < 4; c++) t[c] = c < CN ? mb_tap2<CN>(r0, r1, wa, wb, c, dd) : 0u;
+                if constexpr (CN >= 3) pls[f] = __builtin_amdgcn_perm(t[2], t[0], 0x0c060c02u);
+                else pls[f] = (t[0] >> 16) & 0xffu;
+                if constexpr (CN >= 4) phs[f] = __builtin_amdgcn_perm(t[3], t[1], 0x0c060c02u);
+                else if constexpr (CN == 2 || CN == 3) phs[f] = (t[1] >> 16) & 0xffu;
+                else phs[f] = 0u;
 #endif
             }
             // the previous row's finished entries (after this row's window wait), then the loads:
@@ -1664,6 +1732,10 @@ __device__ __forceinline__ void mb_bands_body(const KMbBandArgs &a, int bi, lds_
             else flush();
             load_win(dq[dA], wq0[bA], wq1[bA]);
             if constexpr (LD) {
+                // this row's descriptor slot is refilled below (issue_desc(r + NL)): its LDS reads
+                // must have completed -- in the schedule and in hardware -- before that DMA is
+                // issued (without this the compiler sank the weight reads past it: a race)
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 if constexpr (ph % 4 == 0) {
                     const lu32 *dd = (const lu32 *)(dring + (ph % NL) * kMbBandLanes * 16 + l * 16);
                     issue_group(r / 4 + kMbLdsLead / 4 + 1, dd[2]);
@@ -1678,7 +1750,7 @@ __device__ __forceinline__ void mb_bands_body(const KMbBandArgs &a, int bi, lds_
             const int k = r >> 1;
 #pragma unroll
             for (int f = 0; f < FR; f++) {
-                const uint32_t pl = v[f] & M, ph_ = (v[f] >> 8) & M;
+                const uint32_t pl = pls[f], ph_ = phs[f];
                 // vertical: level-1 array row i reads level-0 rows 2i .. 2i + 4
                 if ((ph & 1) == 0) {
                     Vl[f][(K3 + 1) % 3] += pl;   // row k - 2 done
@@ -1686,8 +1758,9 @@ __device__ __forceinline__ void mb_bands_body(const KMbBandArgs &a, int bi, lds_
                     level1_done(k - 2, std::integral_constant<int, P2>(),
                                 std::integral_constant<int, M3>(), f, Vl[f][(K3 + 1) % 3],
                                 Vh[f][(K3 + 1) % 3]);
-                    Vl[f][(K3 + 2) % 3] += 6u * pl;
-                    Vh[f][(K3 + 2) % 3] += 6u * ph_;
+                    // (pl, ph_ <= 0x00ff00ff < 2^24: a full-rate 24-bit multiply)
+                    Vl[f][(K3 + 2) % 3] += __umul24(pl, 6u);
+                    Vh[f][(K3 + 2) % 3] += __umul24(ph_, 6u);
                     Vl[f][K3] = pl;
                     Vh[f][K3] = ph_;
                 } else {
@@ -1756,6 +1829,9 @@ __device__ __forceinline__ void mb_blend_tile(const KMbArgs &a, const MbGeo &G, 
 #if defined(MCS_MB_BL_SKIP) && MCS_MB_BL_SKIP >= 3
     return;
 #endif
+    const int n_r1 = t_d2[kMbN2X * kMbN2Y + 1];
+    const uint16_t *t_r1 =
+        reinterpret_cast<const uint16_t *>(t_d2 + kMbN2X * kMbN2Y + kMbTabCounts) + kMbTilePx;
     // B2 = sum m2 g2 / (sum m2 * 65536)
     for (int e = tid; e < kMbN2X * kMbN2Y; e += nt) {
         // (integer sums in double: every product < 2^41, every sum < 2^43 -- exact)
@@ -1777,9 +1853,6 @@ __device__ __forceinline__ void mb_blend_tile(const KMbArgs &a, const MbGeo &G, 
     return;
 #endif
     // R1 = B1 + up(B2), B1 = sum m1 (16384 g1 - E(g2)) / (sum m1 * 4194304)
-    const int n_r1 = t_d2[kMbN2X * kMbN2Y + 1];
-    const uint16_t *t_r1 =
-        reinterpret_cast<const uint16_t *>(t_d2 + kMbN2X * kMbN2Y + kMbTabCounts) + kMbTilePx;
     // (the list is grouped by parity class, mb_prep: the zero-weight third taps of odd
     // coordinates are skipped by whole waves)
     for (int l = tid; l < n_r1; l += nt) {

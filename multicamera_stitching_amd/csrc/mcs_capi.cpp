@@ -73,6 +73,7 @@ struct mcs_plan {
     uint32_t *d_bgrp = nullptr;    // LDS-ring band pass: group source offsets (band_lds_tables)
     uint4 *d_bdesc16 = nullptr;    // LDS-ring band pass: descriptors + group offsets per row
     int n_bands_lds = 0;
+    int64_t mb_mixed_px = 0, mb_r1 = 0;   // per capture: blend pixels computed, R1 entries
     // cylindrical plans: per-column (sin, cos) and per-row h, host copy and device table
     bool cyl = false;
     std::vector<double> cyl_tab;
@@ -92,6 +93,7 @@ struct mcs_plan {
 int mcs::plan_device(const mcs_plan *plan) { return plan ? plan->device : 0; }
 
 #define MCS_VERSION_STRING "mcs 0.1.0 (gfx950 code object, HIP module launch)"
+
 
 namespace {
 
@@ -485,6 +487,11 @@ int prepare_bands(const Api *A, mcs_plan *p, const Kernels *k, hipStream_t s)
     HIP_TRY(A->hipMemcpyAsync(p->d_tile_bt, tile_bt.data(), tile_bt.size() * sizeof(int),
                               hipMemcpyHostToDevice, s));
     p->n_bands = (int)nb;
+    p->mb_mixed_px = p->mb_r1 = 0;
+    for (int i = 0; i < n; i++) {
+        p->mb_mixed_px += cnt[(size_t)i * mcs::kMbTabCounts];
+        p->mb_r1 += cnt[(size_t)i * mcs::kMbTabCounts + 1];
+    }
     mcs::KMbBandArgs a;
     band_args(p, p->kp, a);
     int rc = launch_args(A, k->mb_bdesc[C][p->fd.interp], (unsigned)nb, 1, 256, 1, &a, sizeof(a),
@@ -594,14 +601,24 @@ int band_lds_tables(const Api *A, mcs_plan *p, std::vector<mcs::MbBand> &bands, 
                 const uint32_t ny = (dy & ~(15u << 15)) | ((uint32_t)(cb & 3) << 15);
                 d[r * L + l] = (uint64_t)(wa | (wb << 16)) | ((uint64_t)ny << 32);
             }
-        // the 16-byte descriptors the kernel stages by LDS-DMA: windows, meta, and on rows
-        // r % 4 == 0 the lane's source offset of the group issued after row r
+        // the 16-byte descriptors the kernel stages by LDS-DMA: .x = the windows' ring offsets
+        // (12 bits each) with the byte shift in bits 14-15, .y / .w = the doubled bilinear
+        // weights of rows a / b as u16 pairs (mb_weights2, precomputed here once per plan
+        // instead of per row and wave), .z on rows r % 4 == 0 the lane's source offset of the
+        // group issued after row r
         for (int r = 0; r < DL; r++)
             for (int l = 0; l < L; l++) {
                 const uint64_t v = d[std::min(r, R - 1) * L + l];
+                const uint32_t x = (uint32_t)v, meta = (uint32_t)(v >> 32);
+                const uint32_t sh = (meta >> 15) & 3u, fx = meta & 63u, fy = (meta >> 6) & 31u;
+                const uint32_t ya = (32u - fy) << 6, yb = fy << 6;
+                const uint32_t wa = std::min((32u - fx) * ya, 65535u) |
+                                    (std::min(fx * ya, 65535u) << 16);
+                const uint32_t wb = std::min((32u - fx) * yb, 65535u) |
+                                    (std::min(fx * yb, 65535u) << 16);
                 const int g = r / 4 + D4 + 1;
                 const uint32_t z = (r < R && r % 4 == 0 && g < NG) ? gt[g * L + l] : 0u;
-                d16[(i * DL + r) * L + l] = make_uint4((uint32_t)v, (uint32_t)(v >> 32), z, 0u);
+                d16[(i * DL + r) * L + l] = make_uint4(x | (sh << 14), wa, z, wb);
             }
         bands[i].pad_ |= 1;
         p->n_bands_lds++;
@@ -732,6 +749,7 @@ void release_tables(const Api *A, mcs_plan *p)
     p->d_tile_bt = nullptr;
     p->d_bdesc = nullptr;
     p->n_bands = p->n_bands_in = p->gxb = 0;
+    p->mb_mixed_px = p->mb_r1 = 0;
     p->d_mbdesc = nullptr;
     p->d_mbtab = nullptr;
     p->d_mbfoot = nullptr;
@@ -1833,12 +1851,12 @@ int mcs_plan_stats(const mcs_plan *p, int64_t *stats, int n)
 {
     if (!p || !stats) return mcs::fail(MCS_E_INVALID, "NULL plan/stats");
     const int64_t tiles = (int64_t)p->gx * p->gy;
-    const int64_t v[12] = {p->prepared ? 1 : 0, tiles, tiles - p->n_fallback, p->n_fallback,
+    const int64_t v[14] = {p->prepared ? 1 : 0, tiles, tiles - p->n_fallback, p->n_fallback,
                            tiles * (int64_t)(sizeof(mcs::TileHdr) +
                                              mcs::kTilePx * (mcs::kDescWords + 1) * 4),
                            p->blend, p->n_blend, p->mb_slots, p->n_degraded, p->n_bands,
-                           p->n_bands_lds, p->n_big};
-    for (int i = 0; i < n; i++) stats[i] = i < 12 ? v[i] : 0;
+                           p->n_bands_lds, p->n_big, p->mb_mixed_px, p->mb_r1};
+    for (int i = 0; i < n; i++) stats[i] = i < 14 ? v[i] : 0;
     return MCS_OK;
 }
 
