@@ -75,7 +75,9 @@ def parse():
                          "C4 seams) that a 1-GPU run appends under 'also'")
     ap.add_argument("--no-paste-ref", action="store_true",
                     help="skip the paste-only reference launch (PMC passes: one plan's dispatches)")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
+    ap.add_argument("--pmc-json", default=None,
+                    help="counter summary for roofline.traffic (default profiles/pmc_latest.json, "
+                         "profiles/pmc_latest_cyl.json with --rig cylinder)")
     return ap.parse_args()
 
 
@@ -279,6 +281,9 @@ def main():
         workload = f"cyl-f{args.focal:g}-" + workload + ("-gc2" if seam_k is not None else "")
     traffic_src = None
     try:
+        if args.pmc_json is None:
+            args.pmc_json = os.path.join(ROOT, "profiles",
+                                         "pmc_latest_cyl.json" if cyl else "pmc_latest.json")
         pm = json.load(open(args.pmc_json))
         # counters count only for the kernels they were taken on: same workload AND same build
         # of the embedded code objects (mcs_build_id), else traffic stays null
@@ -362,6 +367,7 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "traffic_source": traffic_src,
+                "traffic_workload": workload,
                 "build_id": _capi.build_id(),
                 "bytes": "SURVEY.md 8d B_frame: every camera frame read once + the mosaic "
                          "written once, x frames per launch",

@@ -459,8 +459,8 @@ extern "C" __global__ __launch_bounds__(256) void mcs_orb_level(const mcs::KOrbP
     __shared__ uint16_t hb[(kOrbTY + 6) * kOrbTX];
     __shared__ uint8_t sc[kOrbSY * kOrbSX];
     __shared__ int sx[kOrbTX * kOrbTY];
-    __shared__ uint16_t fl[kOrbSY * kOrbSX];
-    __shared__ int ns, nf;
+    __shared__ uint16_t fl[kOrbSY * kOrbSX], fc[kOrbSY * kOrbSX];
+    __shared__ int ns, nf, nc;
     const int b = blockIdx.x, tid = threadIdx.x, cam = blockIdx.y;
     int l = 0;
     for (int k = 1; k < p.nlevels; k++) l += b >= p.bstart[k] ? 1 : 0;
@@ -468,11 +468,18 @@ extern "C" __global__ __launch_bounds__(256) void mcs_orb_level(const mcs::KOrbP
     const int bx = (w + kOrbTX - 1) / kOrbTX, loc = b - p.bstart[l];
     const int y0 = (loc / bx) * kOrbTY, x0 = (loc % bx) * kOrbTX;
     const uint8_t *im = p.img + cam * p.stride + p.off[l];
-    if (tid == 0) ns = 0, nf = 0;
-    for (int i = tid; i < kOrbLY * kOrbLX; i += 256) {
-        const int yy = orb_refl(min(max(y0 - kOrbHalo + i / kOrbLX, -(h - 1)), 2 * h - 2), h);
-        const int xx = orb_refl(min(max(x0 - kOrbHalo + i % kOrbLX, -(w - 1)), 2 * w - 2), w);
-        img[i] = im[(int64_t)yy * w + xx];
+    if (tid == 0) ns = 0, nf = 0, nc = 0;
+    if (x0 >= kOrbHalo && y0 >= kOrbHalo && x0 + kOrbTX + kOrbHalo <= w &&
+        y0 + kOrbTY + kOrbHalo <= h) {   // interior tile: no reflection
+        const uint8_t *src = im + (int64_t)(y0 - kOrbHalo) * w + (x0 - kOrbHalo);
+        for (int i = tid; i < kOrbLY * kOrbLX; i += 256)
+            img[i] = src[(i / kOrbLX) * w + i % kOrbLX];
+    } else {
+        for (int i = tid; i < kOrbLY * kOrbLX; i += 256) {
+            const int yy = orb_refl(min(max(y0 - kOrbHalo + i / kOrbLX, -(h - 1)), 2 * h - 2), h);
+            const int xx = orb_refl(min(max(x0 - kOrbHalo + i % kOrbLX, -(w - 1)), 2 * w - 2), w);
+            img[i] = im[(int64_t)yy * w + xx];
+        }
     }
     __syncthreads();
     // blur: horizontal over rows y0 - 3 .. y0 + 18, then vertical
@@ -483,30 +490,34 @@ extern "C" __global__ __launch_bounds__(256) void mcs_orb_level(const mcs::KOrbP
         for (int t = 0; t < 7; t++) s += mcs::kOrbBlur[t] * r[t];
         hb[i] = (uint16_t)s;
     }
-    // FAST on the tile and a one-pixel ring (positions x0 - 1 .., y0 - 1 ..): the segment test
-    // (= score > threshold) everywhere, the survivors compacted in LDS and scored on full waves
+    // FAST on the tile and a one-pixel ring (positions x0 - 1 .., y0 - 1 ..), in three compacted
+    // stages so that every stage runs on full waves: the cardinal pre-test everywhere, the
+    // segment test (= score > threshold) on its survivors, the score on the corners
     const int lo = mcs::kOrbEdge - 1;
+    auto append = [&](int *count, uint16_t *list, int i) {   // (called by the active lanes)
+        const unsigned long long act = __ballot(1);
+        const int lane = __lane_id(), leader = __ffsll((long long)act) - 1;
+        int base = 0;
+        if (lane == leader) base = atomicAdd(count, __popcll(act));
+        list[__shfl(base, leader) + __popcll(act & ((1ull << lane) - 1ull))] = (uint16_t)i;
+    };
+    auto at = [&](int i) { return img + (i / kOrbSX + kOrbHalo - 1) * kOrbLX + i % kOrbSX + kOrbHalo - 1; };
     for (int i = tid; i < kOrbSY * kOrbSX; i += 256) {
         const int yy = y0 - 1 + i / kOrbSX, xx = x0 - 1 + i % kOrbSX;
-        bool corner = false;
-        if (xx >= lo && yy >= lo && xx < w - lo && yy < h - lo)
-            corner = mcs::orb_fast_test(
-                img + (i / kOrbSX + kOrbHalo - 1) * kOrbLX + i % kOrbSX + kOrbHalo - 1, kOrbLX,
-                p.threshold);
         sc[i] = 0;
-        if (corner) {
-            const unsigned long long act = __ballot(1);
-            const int lane = __lane_id(), leader = __ffsll((long long)act) - 1;
-            int base = 0;
-            if (lane == leader) base = atomicAdd(&nf, __popcll(act));
-            fl[__shfl(base, leader) + __popcll(act & ((1ull << lane) - 1ull))] = (uint16_t)i;
-        }
+        if (xx >= lo && yy >= lo && xx < w - lo && yy < h - lo &&
+            mcs::orb_fast_pretest(at(i), kOrbLX, p.threshold))
+            append(&nc, fc, i);
+    }
+    __syncthreads();
+    for (int j = tid; j < nc; j += 256) {
+        const int i = fc[j];
+        if (mcs::orb_fast_test(at(i), kOrbLX, p.threshold)) append(&nf, fl, i);
     }
     __syncthreads();
     for (int j = tid; j < nf; j += 256) {
         const int i = fl[j];
-        sc[i] = (uint8_t)mcs::orb_fast_score(
-            img + (i / kOrbSX + kOrbHalo - 1) * kOrbLX + i % kOrbSX + kOrbHalo - 1, kOrbLX);
+        sc[i] = (uint8_t)mcs::orb_fast_score(at(i), kOrbLX);
     }
     uint8_t *blur = p.blur + cam * p.stride + p.off[l];
     for (int i = tid; i < kOrbTY * kOrbTX; i += 256) {

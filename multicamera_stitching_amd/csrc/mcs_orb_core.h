@@ -102,6 +102,22 @@ MCS_ORB_HD bool orb_fast_test(const uint8_t *p, int step, int t)
     return ((a | b) & 0xffffu) != 0;
 }
 
+// Necessary condition for orb_fast_test: any 9 contiguous circle positions hold two cyclically
+// adjacent cardinal positions (0, 4, 8, 12 -- spacing 4), so a corner has such a pair both
+// brighter than I_c + t or both darker than I_c - t.  A cheap filter ahead of the full test.
+MCS_ORB_HD bool orb_fast_pretest(const uint8_t *p, int step, int t)
+{
+    const int c = p[0];
+    const int v0 = p[3 * step], v4 = p[3], v8 = p[-3 * step], v12 = p[-3];
+    const uint32_t br = (uint32_t)(v0 > c + t) | (uint32_t)(v4 > c + t) << 1 |
+                        (uint32_t)(v8 > c + t) << 2 | (uint32_t)(v12 > c + t) << 3;
+    const uint32_t dk = (uint32_t)(v0 < c - t) | (uint32_t)(v4 < c - t) << 1 |
+                        (uint32_t)(v8 < c - t) << 2 | (uint32_t)(v12 < c - t) << 3;
+    // adjacent pairs (0,4) (4,8) (8,12) (12,0): bit k and bit (k + 1) mod 4
+    const uint32_t rb = br & ((br >> 1) | (br << 3)), rd = dk & ((dk >> 1) | (dk << 3));
+    return ((rb | rd) & 15u) != 0;
+}
+
 // 3x3 Sobel gradients at p.
 MCS_ORB_HD void orb_sobel(const uint8_t *p, int step, int &ix, int &iy)
 {

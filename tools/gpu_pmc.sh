@@ -1,10 +1,12 @@
 # rocprofv3 counter passes (one counter group per pass, no tracing domains) over the default bench
-# workload; stops at the first failing pass.  Summarise with: python tools/pmc_summary.py
+# workload (extra bench flags as arguments; output dir $MCS_PMC_DIR, default gpurun_out/pmc);
+# stops at the first failing pass.  Summarise with: python tools/pmc_summary.py
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 R="$GRAFT_REPO_ROOT"
-mkdir -p "$R/gpurun_out/pmc"
+P="${MCS_PMC_DIR:-$R/gpurun_out/pmc}"
+mkdir -p "$P"
 cd /tmp
 i=0
 for c in "FETCH_SIZE" "WRITE_SIZE" \
@@ -13,7 +15,7 @@ for c in "FETCH_SIZE" "WRITE_SIZE" \
          "SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM GRBM_GUI_ACTIVE GRBM_COUNT" \
          "TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
-  echo "$c" > "$R/gpurun_out/pmc/pass$i.txt"
-  timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d "$R/gpurun_out/pmc/pass$i" -o run -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-paste-ref --no-also "$@" > "$R/gpurun_out/pmc/pass$i.log" 2>&1 || exit $?
+  echo "$c" > "$P/pass$i.txt"
+  timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d "$P/pass$i" -o run -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-paste-ref --no-also "$@" > "$P/pass$i.log" 2>&1 || exit $?
 done
 echo done
