@@ -1,4 +1,5 @@
-# Round-4 final record on one build: full -m gpu suite, smoke, PMC counter passes over the default bench
+# Round-4 final record on one build (argument a: tests, smoke, counters, bench lines; b: traces,
+# C3, matcher, seams, C5, probe; none: both): full -m gpu suite, smoke, PMC counter passes over the default bench
 # workload (-> profiles/pmc_latest.json on the box, copied to gpurun_out/), the default bench line
 # (roofline.traffic from those counters, the full CPU-baseline protocol), paste-only and cylinder
 # lines, marker-bracketed kernel traces of the timed launches (tools/trace_stats.py), C3 lines and
@@ -8,6 +9,7 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 R="$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
+if [ "${1:-all}" != b ]; then
 timeout -k 10 900 python -u -m pytest tests/ -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }
 tail -1 gpurun_out/pytest_gpu.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit $?
@@ -25,6 +27,8 @@ timeout -k 10 300 python bench.py --blend none --no-also > gpurun_out/bench_past
 grep '^{"metric"' gpurun_out/bench_paste.log > gpurun_out/bench_line_paste.json
 timeout -k 10 300 python bench.py --rig cylinder --no-also > gpurun_out/bench_cyl.log 2>&1 || exit $?
 grep '^{"metric"' gpurun_out/bench_cyl.log > gpurun_out/bench_line_cyl.json
+[ "${1:-all}" = a ] && { echo done a; exit 0; }
+fi
 for w in "mb:" "paste:--blend none" "cyl:--rig cylinder"; do
   n=${w%%:*}; a=${w#*:}
   rm -rf "$R/gpurun_out/trace_$n"

@@ -1,4 +1,4 @@
-"""Copies one tools/gpu_r03_final.sh run's outputs from gpurun_out/ into profiles/<prefix>_*
+"""Copies one tools/gpu_r04_final.sh (or r03) run's outputs from gpurun_out/ into profiles/<prefix>_*
 (the committed record; gpurun_out/ is scratch).  Usage: python tools/save_record.py r03b_final"""
 import glob
 import os
@@ -35,10 +35,14 @@ for n in ("mb", "paste", "cyl"):
     cp(f"trace_{n}_line.json", f"trace_line_{n}.json")
     for f in glob.glob(os.path.join(G, f"trace_{n}", "**", "*kernel_stats.csv"), recursive=True):
         shutil.copy(f, os.path.join(P, f"{pre}_kernel_stats_{n}.csv"))
+    cp(f"trace_{n}_trimmed.csv", f"kernel_trace_{n}.csv")   # (tools/trace_stats.py --trim)
 cp("pmc_summary.txt", "pmc_summary.txt")
 cp("pmc_latest.json", "pmc_latest.json")
-if os.path.exists(os.path.join(G, "pmc_latest.json")):
-    shutil.copy(os.path.join(G, "pmc_latest.json"), os.path.join(P, "pmc_latest.json"))
+cp("pmc_summary_cyl.txt", "pmc_summary_cyl.txt")
+cp("pmc_latest_cyl.json", "pmc_latest_cyl.json")
+for f in ("pmc_latest.json", "pmc_latest_cyl.json"):
+    if os.path.exists(os.path.join(G, f)):
+        shutil.copy(os.path.join(G, f), os.path.join(P, f))
 last_json("c3_serial.log", "c3_serial.json")
 last_json("c3_overlap.log", "c3_overlap_depth4.json")
 last_json("c3_resident.log", "c3_resident_depth4.json")

@@ -1,7 +1,7 @@
 """Per-dispatch statistics of the bench's TIMED launches from a rocprofv3 kernel trace.
 
     python tools/trace_stats.py <rocprofv3 output dir | kernel_trace.csv> [--bench-line line.json]
-                                [--out x.json]
+                                [--out x.json] [--trim trimmed.csv]
 
 The bench run must set MCS_BENCH_MARKERS=1: bench.py then launches a tiny spin kernel on its
 stream right before the first and right after the last timed launch of the main plan, and the
@@ -12,7 +12,9 @@ Per window: every mcs_* kernel's dispatch count, mean / median / min / max durat
 launch the span from its first dispatch's start to its last dispatch's end (the same quantity
 the bench's HIP events bracket, minus event overhead).  With --bench-line (the JSON line of the
 same run) the roofline fractions are recomputed from those spans and the line's algorithmic
-bytes (SURVEY.md 8d B_frame and the touched-pixel figure).
+bytes (SURVEY.md 8d B_frame and the touched-pixel figure).  --trim writes the raw trace rows
+(every column) of the dispatches inside the marker windows, markers included: the committed
+record of the timed launches.
 """
 import argparse
 import csv
@@ -72,11 +74,32 @@ def summarize(disp):
             for n, v in sorted(per.items(), key=lambda kv: -sum(kv[1]))}
 
 
+def trim(d, wins, out):
+    """The raw kernel_trace.csv rows whose dispatch lies inside one of the windows (or is one of
+    their markers), in start-time order."""
+    files = [d] if os.path.isfile(d) else glob.glob(os.path.join(d, "**", "*kernel_trace.csv"),
+                                                     recursive=True)
+    keep, fields = [], None
+    for f in files:
+        rd = csv.DictReader(open(f))
+        fields = fields or rd.fieldnames
+        for r in rd:
+            s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+            if any(t0 - 10**6 <= s and e <= t1 + 10**6 for t0, t1 in wins):
+                keep.append(r)
+    keep.sort(key=lambda r: int(r["Start_Timestamp"]))
+    with open(out, "w", newline="") as fo:
+        w = csv.DictWriter(fo, fieldnames=fields)
+        w.writeheader()
+        w.writerows(keep)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace_dir")
     ap.add_argument("--bench-line")
     ap.add_argument("--out")
+    ap.add_argument("--trim")
     a = ap.parse_args()
     rows = load(a.trace_dir)
     line = json.load(open(a.bench_line)) if a.bench_line else None
@@ -103,6 +126,8 @@ def main():
         res["bench_line"] = {"kernel_ms_per_launch": rf["kernel_ms_per_launch"], "frac": rf["frac"],
                              "stream_kernel": rf.get("stream_kernel"),
                              "build_id": rf.get("build_id")}
+    if a.trim:
+        trim(a.trace_dir, windows(rows), a.trim)
     txt = json.dumps(res, indent=1)
     if a.out:
         open(a.out, "w").write(txt + "\n")
