@@ -867,11 +867,24 @@ __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *til
             w.w3 = d[3];
 #else
             uint32_t rr[kPx * CN];
+            // every LDS read of the 4 pixels issued before the first use (one latency per capture,
+            // not one per pixel)
+            uint32_t raw[kPx][6];
 #pragma unroll
             for (int p = 0; p < kPx; p++) {
                 const uint32_t win = d[p * kDescWords];
-                const uint2 r0 = lds_window(b, win & 0xffffu);
-                const uint2 r1 = lds_window(b, win >> 16);
+                const lds_u32 *w0 = (const lds_u32 *)(((const lds_u8 *)b) + ((win & 0xffffu) & ~3u));
+                const lds_u32 *w1 = (const lds_u32 *)(((const lds_u8 *)b) + ((win >> 16) & ~3u));
+                raw[p][0] = w0[0], raw[p][1] = w0[1], raw[p][2] = w0[2];
+                raw[p][3] = w1[0], raw[p][4] = w1[1], raw[p][5] = w1[2];
+            }
+#pragma unroll
+            for (int p = 0; p < kPx; p++) {
+                const uint32_t win = d[p * kDescWords], s0 = win & 3u, s1 = (win >> 16) & 3u;
+                const uint2 r0 = make_uint2(__builtin_amdgcn_alignbyte(raw[p][1], raw[p][0], s0),
+                                            __builtin_amdgcn_alignbyte(raw[p][2], raw[p][1], s0));
+                const uint2 r1 = make_uint2(__builtin_amdgcn_alignbyte(raw[p][4], raw[p][3], s1),
+                                            __builtin_amdgcn_alignbyte(raw[p][5], raw[p][4], s1));
 #pragma unroll
                 for (int k = 0; k < CN; k++)
                     rr[p * CN + k] = blend<CN>(r0, r1, d[p * kDescWords + 1],
