@@ -1136,7 +1136,10 @@ extern "C" __global__ __launch_bounds__(256) void mcs_blend_classify(const mcs::
 #endif
 // band pass entry points: interior, bottom / right edge, both in one grid; SFX _a = the
 // dword-aligned window form (mb_bands AL).  Up to 3 channels at most 128 VGPRs: 4 waves per SIMD.
-#define MCS_MB_BAND_ATTR(CN) __attribute__((amdgpu_waves_per_eu((CN) <= 3 ? 4 : 3)))
+// (3 waves per SIMD: 129 VGPRs and no scratch; at 4 the register cap spilled 3 dwords whose
+// reloads in the global-form store path drained every load in flight, s_waitcnt vmcnt(0) --
+// C4 launch -1 %, C2 unchanged, profiles/r04_band_wpe_ab.txt)
+#define MCS_MB_BAND_ATTR(CN) __attribute__((amdgpu_waves_per_eu(3)))
 // (the aligned entries hold the LDS ring of mode 2; the others none)
 #define MCS_MB_BAND_RING(AL)                                                                   \
     __shared__ __attribute__((aligned(16))) uint8_t ring_[(AL) ? mcs::kMbLdsBytes : 16];       \
