@@ -1,5 +1,7 @@
 # rocprofv3 counter passes over the C3 estimation bench (ORB + kNN-2 + RANSAC per capture), one
-# counter group per pass; summarise with: python tools/pmc_c3_summary.py
+# counter group per pass (bench flags in $C3_ARGS: the resident rig-job path with
+# C3_ARGS='--stitch --pipelined --overlap --resident --depth 1 --steps 20 --warmup 2');
+# summarise with: python tools/pmc_c3_summary.py
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
@@ -13,6 +15,6 @@ for c in "FETCH_SIZE" "WRITE_SIZE" \
          "TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
   echo "$c" > "$R/gpurun_out/pmc_c3/pass$i.txt"
-  timeout -s KILL 150 rocprofv3 --pmc $c --output-format csv -d "$R/gpurun_out/pmc_c3/pass$i" -o run -- python3 "$R/tools/estimate_bench.py" --steps 10 --warmup 2 --threads 1 --no-cpu-baseline > "$R/gpurun_out/pmc_c3/pass$i.log" 2>&1 || exit $?
+  timeout -s KILL 150 rocprofv3 --pmc $c --output-format csv -d "$R/gpurun_out/pmc_c3/pass$i" -o run -- python3 "$R/tools/estimate_bench.py" ${C3_ARGS:---steps 10 --warmup 2 --threads 1} --no-cpu-baseline > "$R/gpurun_out/pmc_c3/pass$i.log" 2>&1 || exit $?
 done
 echo done

@@ -10,15 +10,18 @@ os.environ.setdefault("MCS_PMC_DIR", os.path.join(ROOT, "gpurun_out", "pmc_c3"))
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import pmc_summary as ps  # noqa: E402
 
-FAMILIES = ["mcs_orb_gray", "mcs_resize", "mcs_orb_level", "mcs_orb_select", "mcs_orb_describe",
-            "mcs_hamming_knn2", "mcs_ransac"]
+FAMILIES = ["mcs_orb_gray", "mcs_resize", "mcs_orb_pyramid", "mcs_orb_level", "mcs_orb_select",
+            "mcs_orb_describe", "mcs_hamming_knn2", "mcs_ransac", "mcs_rig_knn2", "mcs_rig_match",
+            "mcs_rig_ransac", "mcs_rig_best", "mcs_direct"]
 
 
 def main(out):
     sys.path.insert(0, ROOT)
     from multicamera_stitching_amd import _capi
-    res = {"workload": "C3: tools/estimate_bench.py --steps 10 --warmup 2 --threads 1 "
-                       "(4 x 1080p ORB 2000 features, 3 pairs kNN-2 + RANSAC per capture)",
+    args = os.environ.get("C3_ARGS", "--steps 10 --warmup 2 --threads 1")
+    res = {"workload": "C3: tools/estimate_bench.py " + args +
+                       " (4 x 1080p ORB 2000 features, 3 pairs kNN-2 + RANSAC per capture"
+                       + (", stitched" if "--stitch" in args else "") + ")",
            "build_id": _capi.build_id(), "per_kernel": {}}
     for fam in FAMILIES:
         avg = ps.family_counters(fam)
