@@ -292,10 +292,12 @@ def pipelined_main(args, frames, truth, W, Hh, N):
 
     def start(i, t_start):
         slot = i % D
-        upload(slot)
+        # (resident: the frames never change, so there is no upload to order after -- no event)
+        if not args.resident:
+            upload(slot)
         t_start[slot] = time.perf_counter()
         if args.overlap:
-            est.submit(ptrs[slot], ev_up[slot].cuda_event, slot)
+            est.submit(ptrs[slot], 0 if args.resident else ev_up[slot].cuda_event, slot)
 
     def run(n):
         mpix = 0.0
@@ -310,7 +312,8 @@ def pipelined_main(args, frames, truth, W, Hh, N):
             if args.overlap:
                 pair_H = est.collect(slot)
             else:
-                ev_up[slot].synchronize()             # this capture's frames are on the device
+                if not args.resident:
+                    ev_up[slot].synchronize()         # this capture's frames are on the device
                 pair_H = est.estimate(ptrs[slot])
             lat.append(time.perf_counter() - t_start[slot])
             if pending[slot] is not None:         # the set's previous plan: its stitch is done
