@@ -153,7 +153,7 @@ int mcs_plan_describe(const mcs_plan *plan, mcs_flat_desc *out);
  * call it on first use.  stream: hipStream_t or NULL for the plan's own stream. */
 int mcs_plan_prepare(mcs_plan *plan, void *stream);
 
-/* stats[0..11] = prepared, tiles, tiles on the LDS path, tiles on the direct path, table bytes,
+/* stats[0..13] = prepared, tiles, tiles on the LDS path, tiles on the direct path, table bytes,
  * blend mode, 32 x 64 tiles the blend kernels recompute per frame, the most owners any
  * multi-band tile blends (<= 8), multi-band tiles degraded to the feather rule (their
  * neighbourhood -- the tile grown by 16 px -- holds more than 8 owners), multi-band bands of the
