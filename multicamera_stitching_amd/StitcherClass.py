@@ -456,19 +456,21 @@ def _note_orb_fallback(owner):
                    "reference's".format(why), log_type="warn")
 
 
-# C-ABI statuses of run-time failures (include/mcs.h), the only ones _run_chain turns into a
-# logged fallback image
-_RUNTIME_FAILURES = (-2, -3)   # MCS_E_HIP, MCS_E_NOMEM
+# C-ABI statuses (include/mcs.h) _run_chain turns into a logged fallback image: run-time failures
+# and inputs the reference handles but the kernels do not (more cameras than MCS_MAX_CAMS, a
+# channel count outside 1-4, more than 8 cameras meeting in one multi-band tile neighbourhood)
+_RUNTIME_FAILURES = (-2, -3, -5)   # MCS_E_HIP, MCS_E_NOMEM, MCS_E_UNSUPPORTED
 
 
 def _run_chain(owner, chain, cams, fallback):
     """One GPU stitch of the chain.  The reference never raises on an expected failure: it logs
     and returns a fallback image (:126-128 the last camera's image, :255-256 B).  A failure of
-    the GPU path at run time (MCS_E_HIP, MCS_E_NOMEM: a device allocation or launch that fails) is
-    logged the same way and `fallback` is returned -- the caller's thread (Qt GUI / worker) gets
-    an image, never an exception, and the log says why.  Argument and programming errors
-    (MCS_E_INVALID, MCS_E_SHAPE, MCS_E_UNSUPPORTED) are raised: the reference has no catch for
-    them either.  (There is no CPU stitch behind it: a missing libmcs.so fails at import.)"""
+    the GPU path at run time (MCS_E_HIP, MCS_E_NOMEM: a device allocation or launch that fails) or
+    an input the reference handles but these kernels do not (MCS_E_UNSUPPORTED: more cameras than
+    MCS_MAX_CAMS, a channel count outside 1-4) is logged the same way and `fallback` is returned --
+    the caller's thread (Qt GUI / worker) gets an image, never an exception, and the log says why.
+    Argument and programming errors (MCS_E_INVALID, MCS_E_SHAPE) are raised: the reference has no
+    catch for them either.  (There is no CPU stitch behind it: a missing libmcs.so fails at import.)"""
     cams, cam0_hw, sizes = _conform_cameras(owner, chain, cams)
     cache = owner._cache()
     with cache.lock:

@@ -397,6 +397,13 @@ int prepare_bands(const Api *A, mcs_plan *p, const Kernels *k, hipStream_t s)
             need[(size_t)slot * gyb + Y0 / mcs::kBlendTileH].push_back(q);
         }
     }
+    // per capture: the blend pixels and R1 entries the blend kernel computes (counted before the
+    // band list: a plan whose tiles need no band still blends its mixed pixels)
+    p->mb_mixed_px = p->mb_r1 = 0;
+    for (int i = 0; i < n; i++) {
+        p->mb_mixed_px += cnt[(size_t)i * mcs::kMbTabCounts];
+        p->mb_r1 += cnt[(size_t)i * mcs::kMbTabCounts + 1];
+    }
     std::vector<mcs::MbBand> bands;
     const int big = 1 << 30;
     for (int slot = 0; slot < kSlots; slot++)
@@ -487,11 +494,6 @@ int prepare_bands(const Api *A, mcs_plan *p, const Kernels *k, hipStream_t s)
     HIP_TRY(A->hipMemcpyAsync(p->d_tile_bt, tile_bt.data(), tile_bt.size() * sizeof(int),
                               hipMemcpyHostToDevice, s));
     p->n_bands = (int)nb;
-    p->mb_mixed_px = p->mb_r1 = 0;
-    for (int i = 0; i < n; i++) {
-        p->mb_mixed_px += cnt[(size_t)i * mcs::kMbTabCounts];
-        p->mb_r1 += cnt[(size_t)i * mcs::kMbTabCounts + 1];
-    }
     mcs::KMbBandArgs a;
     band_args(p, p->kp, a);
     int rc = launch_args(A, k->mb_bdesc[C][p->fd.interp], (unsigned)nb, 1, 256, 1, &a, sizeof(a),

@@ -288,6 +288,9 @@ constexpr int kMbLdsRows = MCS_MB_LDS_ROWS;
 constexpr int kMbLdsLead = MCS_MB_LDS_LEAD;
 constexpr int kMbLdsGLead = MCS_MB_LDS_GLEAD;   // rows between a group's DMA and its first reader
 constexpr int kMbLdsRingBytes = kMbLdsRows * kMbLdsSpan;
+// (the ring descriptor keeps window a's ring offset in 14 bits, its byte shift in bits 14-15:
+// mcs_capi.cpp band_lds_tables, decoded with & 0x3fff in mb_bands_body)
+static_assert(kMbLdsRingBytes <= (1 << 14), "LDS band ring: offsets must fit the 14-bit field");
 // per wave: the captures' rings, then the descriptor ring (kMbLdsDescRing rows of 16 B per
 // lane: the descriptor of row r + kMbLdsDescRing is staged after row r, so the kMbLdsDescRing - 1
 // descriptor DMAs after it bound the wait)

@@ -215,7 +215,8 @@ int seam_graphcut_device(int device, hipStream_t s, int n_cams, int gw, int gh, 
     fa.cn = cn;
     // push-relabel rounds between global relabels / relaxation rounds per relabel launch;
     // a round bound far beyond any grid's need (a run-away loop fails loudly instead of hanging)
-    // (tuned on C4, round 3: tools/experiments/gpu_r03_seamtune*.sh); global relabels run as
+    // (tuned on C4 in round 3; the tuning scripts were pruned in round 4, the tuned form's record is
+    // profiles/r04_final_seam_c4.json); global relabels run as
     // Bellman-Ford relaxation rounds in LDS tiles
     constexpr int kPushLaunches = 8, kPushIters = 16, kRelabelLdsIters = 32, kRelabelBatch = 8;
     constexpr int64_t kMaxRounds = 1 << 20;

@@ -5,6 +5,9 @@
 // only the public plan API (mcs_stitch_device) plus the bound HIP runtime.
 #include <sched.h>
 
+#include <cstdio>
+#include <cstdlib>
+
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
@@ -31,8 +34,9 @@ class CopyPool {
 public:
     static CopyPool &get()
     {
-        static CopyPool *p = new CopyPool(workers());
-        return *p;
+        static CopyPool *p = new (std::nothrow) CopyPool(workers());
+        static CopyPool serial(0);   // (the pool itself could not be allocated)
+        return p ? *p : serial;
     }
     int size() const { return n_; }
     // Runs every copy job -- `rows` rows of `row` bytes, dense at dst, src_pitch apart at src --
@@ -42,26 +46,30 @@ public:
         const uint8_t *src;
         size_t row, rows, src_pitch;
     };
-    void copy(const std::vector<Job> &jobs)
+    // Never throws (it runs inside extern "C" entry points): when the chunk list or a helper
+    // cannot be allocated, the jobs the helpers did not take are copied on the calling thread.
+    void copy(const Job *jobs, int n_jobs) noexcept
     {
         std::vector<Job> chunks;   // pieces of about kCopyChunk bytes
-        for (const Job &j : jobs) {
-            if (j.src_pitch == j.row) {
-                const size_t bytes = j.row * j.rows;
-                for (size_t o = 0; o < bytes; o += kCopyChunk)
-                    chunks.push_back({j.dst + o, j.src + o, std::min(kCopyChunk, bytes - o), 1,
-                                      0});
-                continue;
+        try {
+            for (int k = 0; k < n_jobs; k++) {
+                const Job &j = jobs[k];
+                if (j.src_pitch == j.row) {
+                    const size_t bytes = j.row * j.rows;
+                    for (size_t o = 0; o < bytes; o += kCopyChunk)
+                        chunks.push_back({j.dst + o, j.src + o, std::min(kCopyChunk, bytes - o),
+                                          1, 0});
+                    continue;
+                }
+                const size_t per = std::max<size_t>(1, kCopyChunk / std::max<size_t>(j.row, 1));
+                for (size_t r = 0; r < j.rows; r += per)
+                    chunks.push_back({j.dst + r * j.row, j.src + r * j.src_pitch, j.row,
+                                      std::min(per, j.rows - r), j.src_pitch});
             }
-            const size_t per = std::max<size_t>(1, kCopyChunk / std::max<size_t>(j.row, 1));
-            for (size_t r = 0; r < j.rows; r += per)
-                chunks.push_back({j.dst + r * j.row, j.src + r * j.src_pitch, j.row,
-                                  std::min(per, j.rows - r), j.src_pitch});
+        } catch (...) {
+            for (int k = 0; k < n_jobs; k++) one(jobs[k]);
+            return;
         }
-        auto one = [](const Job &c) {
-            for (size_t r = 0; r < c.rows; r++)
-                memcpy(c.dst + r * c.row, c.src + r * c.src_pitch, c.row);
-        };
         if (chunks.size() <= 1 || n_ == 0) {
             for (const Job &c : chunks) one(c);
             return;
@@ -74,38 +82,74 @@ public:
             for (size_t i; (i = next.fetch_add(1)) < chunks.size();) one(chunks[i]);
         };
         const int helpers = (int)std::min<size_t>((size_t)n_, chunks.size() - 1);
-        left = helpers;
-        for (int h = 0; h < helpers; h++)
-            run([&] {
-                work();
+        for (int h = 0; h < helpers; h++) {
+            {
                 std::lock_guard<std::mutex> lk(m);
-                if (--left == 0) done.notify_one();
-            });
-        work();
+                left++;
+            }
+            if (!run([&] {
+                    work();
+                    std::lock_guard<std::mutex> lk(m);
+                    if (--left == 0) done.notify_one();
+                })) {
+                std::lock_guard<std::mutex> lk(m);
+                left--;
+                break;
+            }
+        }
+        work();   // (takes whatever the helpers have not)
         std::unique_lock<std::mutex> lk(m);
         done.wait(lk, [&] { return left == 0; });
     }
 
 private:
+    static void one(const Job &c)
+    {
+        for (size_t r = 0; r < c.rows; r++)
+            memcpy(c.dst + r * c.row, c.src + r * c.src_pitch, c.row);
+    }
     static int workers()
     {
-        // the CPUs this process may run on (the GPU box's cgroup leaves 16 of nproc), capped:
-        // a handful of memcpy threads saturate the host memory the link reads
+        // the CPUs this process may run on: the affinity set, bounded by the cgroup's CPU quota
+        // (the GPU box reports an affinity of every CPU of the machine but a quota of 16), capped
+        // at 7 helpers -- a handful of memcpy threads saturate the host memory the link reads
         cpu_set_t set;
-        const int cpus = sched_getaffinity(0, sizeof(set), &set) == 0 ? CPU_COUNT(&set) : 1;
+        int cpus = sched_getaffinity(0, sizeof(set), &set) == 0 ? CPU_COUNT(&set) : 1;
+        if (FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+            char q[32] = {};
+            long period = 0;
+            if (fscanf(f, "%31s %ld", q, &period) == 2 && strcmp(q, "max") != 0 && period > 0) {
+                const long quota = (atol(q) + period / 2) / period;
+                if (quota >= 1 && quota < cpus) cpus = (int)quota;
+            }
+            fclose(f);
+        }
         return std::max(0, std::min(7, cpus / 2 - 1));
     }
-    explicit CopyPool(int n) : n_(n)
+    // helper threads that could be started (a failed std::thread leaves the pool smaller)
+    explicit CopyPool(int n) : n_(0)
     {
-        for (int i = 0; i < n; i++) std::thread([this] { loop(); }).detach();
-    }
-    void run(std::function<void()> f)
-    {
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            q_.push_back(std::move(f));
+        for (int i = 0; i < n; i++) {
+            try {
+                std::thread([this] { loop(); }).detach();
+                n_++;
+            } catch (...) {
+                break;
+            }
         }
-        cv_.notify_one();
+    }
+    bool run(std::function<void()> f) noexcept
+    {
+        try {
+            {
+                std::lock_guard<std::mutex> lk(mu_);
+                q_.push_back(std::move(f));
+            }
+            cv_.notify_one();
+            return true;
+        } catch (...) {
+            return false;
+        }
     }
     void loop()
     {
@@ -314,14 +358,15 @@ int mcs_stream_submit_strided(mcs_stream *s, const uint8_t *const *cams,
     if (cams) {   // else: the caller filled mcs_stream_input() buffers in place
         // (a camera inside a wider frame, e.g. the main_stream layout with cameras side by side
         // on axis 1, is gathered row by row into its dense staging slot)
-        std::vector<CopyPool::Job> jobs;
+        CopyPool::Job jobs[MCS_MAX_CAMS];
+        int n_jobs = 0;
         for (int c = 0; c < s->n_cams; c++) {
             if (!cams[c]) continue;
             const size_t row = (size_t)s->cam_w[c] * s->channels;
-            jobs.push_back({sl.h_in + s->cam_off[c], cams[c], row, (size_t)s->cam_h[c],
-                            row_pitch ? (size_t)row_pitch[c] : row});
+            jobs[n_jobs++] = {sl.h_in + s->cam_off[c], cams[c], row, (size_t)s->cam_h[c],
+                              row_pitch ? (size_t)row_pitch[c] : row};
         }
-        CopyPool::get().copy(jobs);
+        CopyPool::get().copy(jobs, n_jobs);
     }
     HIP_TRY(A->hipMemcpyAsync(sl.d_in, sl.h_in, s->in_bytes, hipMemcpyHostToDevice, s->up));
     HIP_TRY(A->hipEventRecord(sl.ev_in, s->up));
@@ -352,7 +397,10 @@ int mcs_stream_wait(mcs_stream *s, int slot, uint8_t *out)
     if (!A) return MCS_E_HIP;
     mcs::DeviceGuard g(A, s->device);
     HIP_TRY(A->hipEventSynchronize(sl.ev_out));
-    if (out) CopyPool::get().copy({{out, sl.h_out, s->out_bytes, 1, s->out_bytes}});
+    if (out) {
+        const CopyPool::Job job = {out, sl.h_out, s->out_bytes, 1, s->out_bytes};
+        CopyPool::get().copy(&job, 1);
+    }
     sl.busy = false;
     return MCS_OK;
 }

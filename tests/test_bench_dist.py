@@ -35,9 +35,23 @@ def test_bench_gpus2_spawns_two_ranks():
     want = 2 * res["mpix_per_step_per_rank"] * 4 / res["max_seconds"]
     assert abs(res["value"] - want) <= 1e-5 * want + 1e-6
     assert res["max_seconds"] >= res["rank0_seconds"]
-    assert res["gather"] == {"verified": True, "ranks": 2, "bytes_into_rank0": 4 * 32 * 48 * 3}
-    # every rank checked its own output; the line carries the max over ranks, a number
+    g = res["gather"]
+    assert (g["verified"], g["ranks"], g["bytes_into_rank0"]) == (True, 2, 4 * 32 * 48 * 3)
+    # the second timed loop: steps of stitch + gather to rank 0, max over ranks
+    assert g["stitch_and_gather"]["value"] > 0
+    # every rank checked captures 0, F/2, F-1 of its own output; the line carries the max over
+    # ranks and captures, a number
     assert res["max_abs_diff"] == 0
+    assert res["checked_captures"] == {"per_rank": [0, 2, 3], "ranks": 2}
+    # the C4 and C5 lines every N emits, measured by the same two ranks
+    c4, c5 = res["also"]["c4_cylinder_multiband"], res["also"]["c5_stream_4k"]
+    assert c4["n_gpus"] == 2 and c4["max_abs_diff"] == 0 and c4["gather"]["verified"]
+    assert c4["max_seconds"] >= c4["rank0_seconds"]
+    assert abs(c4["value"] - 2 * c4["mpix_per_step_per_rank"] * 4 / c4["max_seconds"]) <= \
+        1e-5 * c4["value"] + 1e-6
+    assert c5["n_gpus"] == 2 and c5["max_abs_diff"] == 0
+    assert c5["gather"] == {"verified": True, "ranks": 2}
+    assert c5["value"] > 0
 
 
 def test_bench_gpus1_stub_single_process():
@@ -45,6 +59,8 @@ def test_bench_gpus1_stub_single_process():
     assert r.returncode == 0, r.stderr[-2000:]
     res = _line(r.stdout)
     assert res["n_gpus"] == 1 and res["gather"] is None
+    assert res["also"]["c4_cylinder_multiband"]["gather"] is None
+    assert res["also"]["c5_stream_4k"]["gather"] is None
 
 
 def test_bench_refuses_world_mismatch():

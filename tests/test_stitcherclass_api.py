@@ -92,11 +92,13 @@ def test_orb_fallback_is_logged_once(caplog, monkeypatch):
     assert len(hits) == 1 and "not a contrib version" in hits[0].getMessage()
 
 
-@pytest.mark.parametrize("code, raises", [(-2, False), (-3, False), (-1, True), (-5, True)])
+@pytest.mark.parametrize("code, raises", [(-2, False), (-3, False), (-5, False), (-1, True),
+                                         (-4, True)])
 def test_gpu_failure_fallback_only_for_runtime_errors(monkeypatch, caplog, code, raises):
     """A run-time failure of the GPU path (MCS_E_HIP / MCS_E_NOMEM) is logged and the fallback
-    image returned, as the reference returns images on its expected failures; argument and
-    programming errors (MCS_E_INVALID / MCS_E_UNSUPPORTED) raise (advisor finding, round 3)."""
+    image returned, as the reference returns images on its expected failures, and so is an input
+    the reference handles but the kernels do not (MCS_E_UNSUPPORTED, advisor finding, round 4);
+    argument and programming errors (MCS_E_INVALID / MCS_E_SHAPE) raise (round 3)."""
     from multicamera_stitching_amd import StitcherClass as sc, _capi
     imgs = images()
     st = Stitcher(imgs)

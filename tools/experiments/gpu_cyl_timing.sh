@@ -1,3 +1,7 @@
+# RETIRED (round 4): libmcs no longer reads MCS_DEBUG_BANDS, MCS_MB_CONCURRENT -- the knob was stripped
+# from the product path, so this script now times the same build on both sides of its A/B.
+# Kept as the record of how the numbers DESIGN.md cites were taken; to repeat such an A/B,
+# build the variants as compile-time defines with tools/build_variant.py (MCS_LIBRARY=...).
 # serial kernel stats of the C4 cylinder bench (multi-band levels on the caller's stream)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"

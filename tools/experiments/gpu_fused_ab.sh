@@ -1,3 +1,7 @@
+# RETIRED (round 4): libmcs no longer reads MCS_MB_BANDS_FUSED -- the knob was stripped
+# from the product path, so this script now times the same build on both sides of its A/B.
+# Kept as the record of how the numbers DESIGN.md cites were taken; to repeat such an A/B,
+# build the variants as compile-time defines with tools/build_variant.py (MCS_LIBRARY=...).
 # interior + edge bands in one launch (MCS_MB_BANDS_FUSED=1) vs two: parity of the blend / stream
 # paths, then C2 and C4 bench lines alternating
 set -o pipefail

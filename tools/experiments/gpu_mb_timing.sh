@@ -1,3 +1,7 @@
+# RETIRED (round 4): libmcs no longer reads MCS_MB_CONCURRENT -- the knob was stripped
+# from the product path, so this script now times the same build on both sides of its A/B.
+# Kept as the record of how the numbers DESIGN.md cites were taken; to repeat such an A/B,
+# build the variants as compile-time defines with tools/build_variant.py (MCS_LIBRARY=...).
 # serial multi-band kernel stats per library variant (no parity tests: timing experiments)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"

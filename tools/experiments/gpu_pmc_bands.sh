@@ -1,3 +1,7 @@
+# RETIRED (round 4): libmcs no longer reads MCS_MB_CONCURRENT -- the knob was stripped
+# from the product path, so this script now times the same build on both sides of its A/B.
+# Kept as the record of how the numbers DESIGN.md cites were taken; to repeat such an A/B,
+# build the variants as compile-time defines with tools/build_variant.py (MCS_LIBRARY=...).
 # PMC passes over the serial multi-band launch (band kernel alone); per-kernel averages with
 #   MCS_PMC_DIR=gpurun_out/pmc_bands python tools/pmc_kernel.py mcs_mb_bands_all_a_c3
 set -o pipefail

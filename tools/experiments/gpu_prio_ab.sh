@@ -1,3 +1,7 @@
+# RETIRED (round 4): libmcs no longer reads MCS_MB_PRIORITY -- the knob was stripped
+# from the product path, so this script now times the same build on both sides of its A/B.
+# Kept as the record of how the numbers DESIGN.md cites were taken; to repeat such an A/B,
+# build the variants as compile-time defines with tools/build_variant.py (MCS_LIBRARY=...).
 # multi-band side stream at the greatest priority (MCS_MB_PRIORITY=1) vs default: C2 and C4 bench lines
 # alternating (timing only)
 set -o pipefail

@@ -1,3 +1,7 @@
+# RETIRED (round 4): libmcs no longer reads MCS_MB_BAND_ALIGNED, MCS_MB_BAND_LDS, MCS_MB_CONCURRENT -- the knob was stripped
+# from the product path, so this script now times the same build on both sides of its A/B.
+# Kept as the record of how the numbers DESIGN.md cites were taken; to repeat such an A/B,
+# build the variants as compile-time defines with tools/build_variant.py (MCS_LIBRARY=...).
 # band pass window alignment: serial kernel times and concurrent multi-band lines per variant
 # (main; unaligned = main with MCS_MB_BAND_ALIGNED=0; noring = MCS_MB_BAND_LDS=0; else
 # variants/<name>.so; timing only:

@@ -1,3 +1,7 @@
+# RETIRED (round 4): libmcs no longer reads MCS_MB_SPLIT -- the knob was stripped
+# from the product path, so this script now times the same build on both sides of its A/B.
+# Kept as the record of how the numbers DESIGN.md cites were taken; to repeat such an A/B,
+# build the variants as compile-time defines with tools/build_variant.py (MCS_LIBRARY=...).
 # multi-band launch split (streaming tiles under mixed pixels first, blend beside the rest):
 # parity of the blend / stream paths, then C2 and C4 bench lines with MCS_MB_SPLIT=1 / 0 alternating
 set -o pipefail

@@ -1,3 +1,7 @@
+# RETIRED (round 4): libmcs no longer reads MCS_STREAM_B32 -- the knob was stripped
+# from the product path, so this script now times the same build on both sides of its A/B.
+# Kept as the record of how the numbers DESIGN.md cites were taken; to repeat such an A/B,
+# build the variants as compile-time defines with tools/build_variant.py (MCS_LIBRARY=...).
 # A/B of the streaming kernel's DMA form: buffer resource (default) vs 64-bit global addresses
 # (MCS_STREAM_B32=0), paste-only bench lines, alternating
 set -o pipefail
