@@ -31,6 +31,7 @@ struct mcs_plan {
     mcs::TileHdr *d_tiles = nullptr;
     uint32_t *d_desc = nullptr;
     uint32_t *d_desc4 = nullptr;      // compact per-pixel words (the streaming kernel reads these)
+    uint16_t *d_spans = nullptr;      // per tile footprint row: the chunks its windows read
     int *d_fallback = nullptr;
     // side stream for the direct-gather tiles, forked from / joined to the caller's stream
     hipStream_t side = nullptr;
@@ -735,7 +736,7 @@ void release_tables(const Api *A, mcs_plan *p)
     if (p->side) (void)A->hipStreamSynchronize(p->side);
     if (p->side2) (void)A->hipStreamSynchronize(p->side2);
     for (void *q : {(void *)p->d_tiles, (void *)p->d_desc, (void *)p->d_desc4,
-                    (void *)p->d_fallback,
+                    (void *)p->d_spans, (void *)p->d_fallback,
                     (void *)p->d_owner, (void *)p->d_binfo, (void *)p->d_blist,
                     (void *)p->d_mbdesc, (void *)p->d_mbtab, (void *)p->d_mbfoot, (void *)p->d_mbg1,
                     (void *)p->d_mbg2, (void *)p->d_bands, (void *)p->d_tile_bt,
@@ -761,6 +762,7 @@ void release_tables(const Api *A, mcs_plan *p)
     p->d_tiles = nullptr;
     p->d_desc = nullptr;
     p->d_desc4 = nullptr;
+    p->d_spans = nullptr;
     p->d_fallback = nullptr;
     p->d_big = nullptr;
     p->n_big = 0;
@@ -816,6 +818,7 @@ int prepare(const Api *A, mcs_plan *p, hipStream_t s)
     HIP_TRY(A->hipMalloc((void **)&p->d_tiles, tiles * sizeof(mcs::TileHdr)));
     HIP_TRY(A->hipMalloc((void **)&p->d_desc, tiles * mcs::kTilePx * mcs::kDescWords * 4));
     HIP_TRY(A->hipMalloc((void **)&p->d_desc4, tiles * mcs::kTilePx * 4));
+    HIP_TRY(A->hipMalloc((void **)&p->d_spans, tiles * mcs::kMaxTileJobs * sizeof(uint16_t)));
     HIP_TRY(A->hipMalloc((void **)&p->d_fallback, 2 * (tiles + 1) * sizeof(int)));
     p->d_big = p->d_fallback + tiles + 1;
     HIP_TRY(A->hipMemsetAsync(p->d_fallback, 0, sizeof(int), s));
@@ -827,6 +830,7 @@ int prepare(const Api *A, mcs_plan *p, hipStream_t s)
     args.desc4 = p->d_desc4;
     args.fallback = p->d_fallback;
     args.big = p->d_big;
+    args.spans = p->d_spans;
     size_t sz = sizeof(args);
     void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, (void *)&args, HIP_LAUNCH_PARAM_BUFFER_SIZE,
                    &sz, HIP_LAUNCH_PARAM_END};
@@ -939,6 +943,7 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
         args.tiles = p->d_tiles;
         args.desc = p->d_desc;
         args.desc4 = p->d_desc4;
+        args.spans = p->d_spans;
         args.n_frames = n_frames;
         args.pad_ = 0;
         args.pad2_ = 0;
@@ -973,6 +978,7 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
     args.tiles = p->d_tiles;
     args.desc = p->d_desc;
     args.desc4 = p->d_desc4;
+    args.spans = p->d_spans;
     args.n_frames = n_frames;
     args.pad_ = 0;
     args.pad2_ = 0;

@@ -495,16 +495,25 @@ __device__ __forceinline__ void tile_pixel(int bx, int by, int lane, int wave, i
 }
 
 
+// Footprint DMA per row over the span its windows read (1) or the camera box's full width (0:
+// variant builds, the round-4 form, for A/B timing).
+#ifndef MCS_ROW_SPANS
+#define MCS_ROW_SPANS 1
+#endif
+
 struct FootprintLds {
     int rmin[MCS_MAX_CAMS], rmax[MCS_MAX_CAMS], cmin[MCS_MAX_CAMS], cmax[MCS_MAX_CAMS];
 };
 
 template <int CN, int INTERP>
 __device__ __forceinline__ void prepare_tile(const KParams &P, TileHdr *tiles, uint32_t *desc,
-                                             uint32_t *desc4, int *fallback, int *big)
+                                             uint32_t *desc4, int *fallback, int *big,
+                                             uint16_t *spans)
 {
     __shared__ FootprintLds fl;
     __shared__ TileHdr th;
+    // per footprint row (DMA job): the LDS byte span [lo, hi) the tile's windows read
+    __shared__ int span_lo[kMaxTileJobs], span_hi[kMaxTileJobs];
     const int lane = threadIdx.x, wave = threadIdx.y;
     const int tid = wave * kWave + lane;
     const int tile = blockIdx.y * gridDim.x + blockIdx.x;
@@ -517,6 +526,10 @@ __device__ __forceinline__ void prepare_tile(const KParams &P, TileHdr *tiles, u
         fl.rmax[tid] = -0x7fffffff;
         fl.cmin[tid] = 0x7fffffff;
         fl.cmax[tid] = -0x7fffffff;
+    }
+    if (tid < kMaxTileJobs) {
+        span_lo[tid] = 0x7fffffff;
+        span_hi[tid] = -0x7fffffff;
     }
     __syncthreads();
     Geo g[kPx];
@@ -604,6 +617,20 @@ __device__ __forceinline__ void prepare_tile(const KParams &P, TileHdr *tiles, u
                                  (g[p].r1 == last ? e : 0));
         const bool zero = (g[p].w0 | g[p].w1) == 0u || !th.fits;
         if (zero) a0 = a1 = 0u;
+        if (!zero) {
+            // the row spans: this pixel's two windows (2 CN bytes each) in LDS row coordinates
+            const int j0 = th.jobstart[k] + g[p].r0 - rm, j1 = th.jobstart[k] + g[p].r1 - rm;
+            const int q0 = (int)a0 - bs - (g[p].r0 - rm) * st;
+            const int q1 = (int)a1 - bs - (g[p].r1 - rm) * st;
+            if (j0 >= 0 && j0 < kMaxTileJobs) {
+                atomicMin(&span_lo[j0], q0);
+                atomicMax(&span_hi[j0], q0 + 2 * CN);
+            }
+            if (j1 >= 0 && j1 < kMaxTileJobs) {
+                atomicMin(&span_lo[j1], q1);
+                atomicMax(&span_hi[j1], q1 + 2 * CN);
+            }
+        }
         d[p * kDescWords + 0] = (a0 & 0xffffu) | (a1 << 16);
         d[p * kDescWords + 1] = g[p].w0;
         d[p * kDescWords + 2] = g[p].w1;
@@ -621,6 +648,20 @@ __device__ __forceinline__ void prepare_tile(const KParams &P, TileHdr *tiles, u
     }
     reinterpret_cast<uint4 *>(desc4)[(int64_t)tile * (kTilePx / kPx) + tid] =
         make_uint4(cw[0], cw[1], cw[2], cw[3]);
+    __syncthreads();
+    if (tid < kMaxTileJobs) {
+        // first chunk | chunk count (>= 1: a row no window reads still issues its one DMA
+        // instruction, of one chunk, so every job counts in the streaming kernel's vmcnt waits)
+        int lo = span_lo[tid], hi = span_hi[tid];
+#if !MCS_ROW_SPANS
+        // (variant builds: every row fetches its camera's whole box width, the round-4 form)
+        for (int k = 0; k < th.ncam; k++)
+            if (tid >= th.jobstart[k] && tid < th.jobstart[k + 1])
+                lo = 0, hi = 16 * ((th.stride[k] >> 16) & 0xff);
+#endif
+        const int c0 = lo <= hi ? lo >> 4 : 0, c1 = lo <= hi ? (hi + 15) >> 4 : 1;
+        spans[(int64_t)tile * kMaxTileJobs + tid] = (uint16_t)(c0 | (max(c1 - c0, 1) << 8));
+    }
     uint4 *o = reinterpret_cast<uint4 *>(desc + ((int64_t)tile * kTilePx + (int64_t)tid * kPx) *
                                                     kDescWords);
 #pragma unroll
@@ -673,9 +714,13 @@ struct WaveJobs {
 };
 
 template <int CN, bool BUF, int NJ>
-__device__ __forceinline__ WaveJobs<BUF, NJ> wave_jobs(const KParams &P, const TileHdr &h, int wave)
+__device__ __forceinline__ WaveJobs<BUF, NJ> wave_jobs(const KParams &P, const TileHdr &h, int wave,
+                                                       const uint16_t *spans, int lane)
 {
+    static_assert(NJ * kWavesPerBlock <= kMaxTileJobs, "row spans per tile");
     WaveJobs<BUF, NJ> J;
+    // the wave's rows' spans: lane jj holds job wave + 8 jj's (read back lane by lane below)
+    const uint32_t sp_v = lane < NJ ? (uint32_t)spans[wave + lane * kWavesPerBlock] : 0u;
     const int njobs = uni(h.njobs);
     J.n = 0;
 #pragma unroll
@@ -692,14 +737,17 @@ __device__ __forceinline__ WaveJobs<BUF, NJ> wave_jobs(const KParams &P, const T
             const int64_t pitch = (int64_t)P.cam_w[c] * CN;
             const int r = uni(h.rmin[k]) + row;
             const int e = r == P.cam_h[c] - 1 ? (uni(h.last_shift) >> (8 * k)) & 255 : 0;
-            const int64_t in_frame = (int64_t)r * pitch + uni(h.cal[k]) - e;
+            // only the row's span of the box: chunks [lo, lo + n) of its LDS row
+            const uint32_t sp = (uint32_t)__builtin_amdgcn_readlane((int)sp_v, jj);
+            const int lo16 = 16 * (int)(sp & 0xffu);
+            const uint32_t nch = (sp >> 8) & 0xffu;
+            const int64_t in_frame = (int64_t)r * pitch + uni(h.cal[k]) - e + lo16;
             if constexpr (BUF)
                 J.src[jj] = (uint32_t)((uint64_t)(uintptr_t)P.cams[c] -
                                        (uint64_t)(uintptr_t)P.base + (uint64_t)in_frame);
             else
                 J.src[jj] = P.cams[c] + in_frame;
-            J.w[jj] = (uint32_t)(uni(h.base[k]) + row * (stride & 0xffff)) |
-                      ((uint32_t)stride & 0xffff0000u);
+            J.w[jj] = (uint32_t)(uni(h.base[k]) + row * (stride & 0xffff) + lo16) | (nch << 16);
             J.n = jj + 1;
         }
     }
@@ -765,8 +813,8 @@ __device__ __forceinline__ void wait_vmcnt_le(int n)
 template <int CN, bool BUF, int FITS = 1>
 __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *tiles,
                                             const uint32_t *desc, const uint32_t *desc4,
-                                            int n_frames, const int *order, int n_order,
-                                            uint8_t *smem)
+                                            const uint16_t *spans, int n_frames, const int *order,
+                                            int n_order, uint8_t *smem)
 {
     // FITS 1: the tiles of the main launch; 2: the large-footprint tiles (kBigJobsPerWave rows per
     // wave, kBigStreamLds bytes of LDS)
@@ -828,7 +876,8 @@ __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *til
             d[p * kDescWords + 2] = d2;
         }
     }
-    const WaveJobs<BUF, NJ> J = wave_jobs<CN, BUF, NJ>(P, h, wave);
+    const WaveJobs<BUF, NJ> J =
+        wave_jobs<CN, BUF, NJ>(P, h, wave, spans + (int64_t)tile * kMaxTileJobs, lane);
     // (BUF: raw buffer over [P.base, P.base + 4 GiB); no range clamping needed, every chunk is
     // inside a frame)
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
@@ -1038,9 +1087,9 @@ __device__ __forceinline__ void resize_px(const KResizeArgs &a)
 #define MCS_PREPARE_ENTRY(CN, IN)                                                              \
     extern "C" __global__ __launch_bounds__(512) void mcs_prepare_c##CN##_i##IN(               \
         const mcs::KParams P, mcs::TileHdr *tiles, uint32_t *desc, uint32_t *desc4,            \
-        int *fallback, int *big)                                                               \
+        int *fallback, int *big, uint16_t *spans)                                              \
     {                                                                                          \
-        mcs::prepare_tile<CN, IN>(P, tiles, desc, desc4, fallback, big);                       \
+        mcs::prepare_tile<CN, IN>(P, tiles, desc, desc4, fallback, big, spans);                \
     }
 #ifdef MCS_STREAM_WAVES_PER_EU   // experiment knob: occupancy target of the streaming kernel
 #define MCS_STREAM_ATTR __attribute__((amdgpu_waves_per_eu(MCS_STREAM_WAVES_PER_EU)))
@@ -1055,17 +1104,21 @@ __device__ __forceinline__ void resize_px(const KResizeArgs &a)
 #define MCS_STREAM_ENTRY(CN, SUF, BUF)                                                         \
     extern "C" __global__ __launch_bounds__(512) MCS_STREAM_ATTR void mcs_stream_c##CN##SUF(   \
         const mcs::KParams P, const mcs::TileHdr *tiles, const uint32_t *desc,                \
-        const uint32_t *desc4, int n_frames, const int *order, int n_order)                    \
+        const uint32_t *desc4, const uint16_t *spans, int n_frames, const int *order,          \
+        int n_order)                                                                           \
     {                                                                                          \
         extern __shared__ __attribute__((aligned(16))) uint8_t smem[];                         \
-        mcs::stream_tile<CN, BUF>(P, tiles, desc, desc4, n_frames, order, n_order, smem);      \
+        mcs::stream_tile<CN, BUF>(P, tiles, desc, desc4, spans, n_frames, order, n_order,      \
+                                  smem);                                                       \
     }                                                                                          \
     extern "C" __global__ __launch_bounds__(512) void mcs_stream_big_c##CN##SUF(               \
         const mcs::KParams P, const mcs::TileHdr *tiles, const uint32_t *desc,                \
-        const uint32_t *desc4, int n_frames, const int *order, int n_order)                    \
+        const uint32_t *desc4, const uint16_t *spans, int n_frames, const int *order,          \
+        int n_order)                                                                           \
     {                                                                                          \
         extern __shared__ __attribute__((aligned(16))) uint8_t smem[];                         \
-        mcs::stream_tile<CN, BUF, 2>(P, tiles, desc, desc4, n_frames, order, n_order, smem);   \
+        mcs::stream_tile<CN, BUF, 2>(P, tiles, desc, desc4, spans, n_frames, order, n_order,   \
+                                     smem);                                                    \
     }
 #define MCS_DIRECT_ENTRY(CN, IN, O32)                                                          \
     extern "C" __global__ __launch_bounds__(512) void mcs_direct_c##CN##_i##IN##_o##O32(       \

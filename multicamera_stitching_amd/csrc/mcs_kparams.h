@@ -109,6 +109,12 @@ struct TileHdr {
 static_assert(sizeof(TileHdr) == 128, "TileHdr layout");
 
 // Kernarg blocks.
+// Per footprint row (DMA job j of a tile, kMaxTileJobs per tile): the 16-byte chunks of its LDS
+// row that any pixel window reads -- first chunk (bits 0-7) | chunk count (bits 8-15, >= 1: every
+// job issues exactly one DMA instruction, which the counted vmcnt waits rely on).  A footprint is
+// the box of its rows x the union of their byte spans; where the map curves (a cylinder's rows
+// through a camera) each row needs only part of the box's width.
+constexpr int kMaxTileJobs = 128;
 struct KPrepareArgs {
     KParams P;
     TileHdr *tiles;
@@ -116,12 +122,14 @@ struct KPrepareArgs {
     uint32_t *desc4;               // compact words (kCw*), 4 per lane
     int *fallback;                 // [0] = count, then tile indices (direct-gather tiles)
     int *big;                      // [0] = count, then tile indices (large-footprint tiles)
+    uint16_t *spans;               // [tiles][kMaxTileJobs] row spans
 };
 struct KStreamArgs {
     KParams P;
     const TileHdr *tiles;
     const uint32_t *desc;
     const uint32_t *desc4;
+    const uint16_t *spans;         // [tiles][kMaxTileJobs] row spans
     int n_frames;
     int pad_;
     const int *order;              // tiles to stream (NULL: all, in grid order)
@@ -355,6 +363,7 @@ constexpr int lds_ring_bytes(int cn) { return lds_stream_bytes(cn) - (int)sizeof
 // wave and a 120 KiB ring (one block per CU) over their own list, on the side stream beside the
 // main launch (round 3 sent these 39 C4 tiles to the direct-gather kernel).
 constexpr int kBigJobsPerWave = 16;
+static_assert(kBigJobsPerWave * kWavesPerBlock <= kMaxTileJobs, "row spans per tile");
 constexpr int kBigStreamLds = 120 * 1024;
 constexpr int big_ring_bytes() { return kBigStreamLds - (int)sizeof(TileHdr); }
 // LDS row pitch of a footprint row of `bytes` DMA bytes.  The 32 lanes of an output row read
