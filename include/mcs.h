@@ -340,6 +340,18 @@ int mcs_ransac_homography_host(const float *src_xy, const float *dst_xy, int n, 
 int mcs_homography_refine_host(const float *src_xy, const float *dst_xy, int n,
                                const uint8_t *mask, double *H);
 
+/* ---- Chain geometry of one capture -----------------------------------------
+ * Stage descriptors of a left-to-right chain from its adjacent-pair homographies: pair k
+ * (pair_H + 9 k, row-major, used when pair_ok[k]) maps camera k+1 into camera k; stage k's A ->
+ * mosaic homography is T(o_k) . H_0 ... H_k with o_k camera 0's origin in the mosaic so far, and
+ * its fields follow StitcherBase.calibrate (StitcherClass.py:293-351: corners projected and
+ * truncated, the translation patched into H, ABSize, super-mode limits) in one fixed FP64 order
+ * (estimate.chain_stages restates it).  The first pair without a homography leaves its stage and
+ * every later one uncalibrated.  out: n_cams - 1 descriptors (mcs_plan_create's input).
+ * Replaces the per-capture numpy geometry of estimate.chain_stages / geometry.stage_geometry. */
+int mcs_chain_stages(int n_cams, const int *cam_w, const int *cam_h, const double *pair_H,
+                     const int *pair_ok, int super_mode, mcs_stage_desc *out);
+
 /* ---- A whole rig capture ---------------------------------------------------
  * Per capture, detectAndDescribe + matchKeypoints (StitcherClass.py:356-448) of every adjacent
  * camera pair, made per-frame by config 3: ORB of the n_cams device frames (dense w x h x
@@ -363,6 +375,18 @@ int mcs_rig_job_create(int n_cams, int w, int h, int channels, int nfeatures, in
 int mcs_rig_job_submit(mcs_rig_job *job, const uint8_t *const *d_frames, void *wait_event);
 int mcs_rig_job_wait(mcs_rig_job *job, double *H, int *ok, int *n_keypoints, int *n_matches,
                      int *n_inliers);
+/* wait + the capture's stitch, issued from libmcs (config 3 end to end, no caller code per
+ * capture): the pairs the job estimated replace H_io / ok_io (n_cams - 1 pairs, in/out: a pair
+ * whose estimate failed keeps the caller's -- the previous capture's -- homography, ok 0 and no
+ * previous one: uncalibrated from that pair on), the chain geometry of mcs_chain_stages, a plan,
+ * and mcs_stitch_direct of the submitted frames into d_out (rows out_pitch bytes apart, at most
+ * out_capacity bytes) on `stream` (enqueued; the frames and d_out must stay valid until it has
+ * run).  out_w / out_h: the mosaic's size.  Replaces estimate.CaptureEstimator.collect + stitch
+ * (chain geometry and plan built per capture in Python). */
+int mcs_rig_job_wait_stitch(mcs_rig_job *job, double *H_io, int *ok_io, int super_mode,
+                            int interp, uint8_t *d_out, int64_t out_pitch, int64_t out_capacity,
+                            void *stream, int *out_w, int *out_h, int *n_keypoints,
+                            int *n_matches, int *n_inliers);
 /* Captures the job finished on the device path (one launch chain) and on the per-call path (a
  * device ranking overflow, or MCS_RIG_PATH=calls). */
 int mcs_rig_job_counts(const mcs_rig_job *job, int *device_captures, int *call_captures);

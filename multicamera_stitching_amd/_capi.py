@@ -48,7 +48,8 @@ EXPORTS = (
     "mcs_stitch_direct", "mcs_orb_detect_device", "mcs_group_unique_id", "mcs_group_create",
     "mcs_group_gather", "mcs_group_destroy", "mcs_rccl_library", "mcs_rig_job_create",
     "mcs_rig_job_submit", "mcs_rig_job_wait", "mcs_rig_job_counts", "mcs_rig_job_destroy",
-    "mcs_seam_graphcut_device", "mcs_plan_seam_stats",
+    "mcs_seam_graphcut_device", "mcs_plan_seam_stats", "mcs_chain_stages",
+    "mcs_rig_job_wait_stitch",
 )
 MCS_GROUP_ID_BYTES = 128
 
@@ -215,6 +216,11 @@ def load() -> ctypes.CDLL:
         L.mcs_rig_job_submit.restype = I
         L.mcs_rig_job_wait.argtypes = [P, P, P, P, P, P]
         L.mcs_rig_job_wait.restype = I
+        L.mcs_rig_job_wait_stitch.argtypes = [P, P, P, I, I, P, ctypes.c_int64, ctypes.c_int64,
+                                              P, P, P, P, P, P]
+        L.mcs_rig_job_wait_stitch.restype = I
+        L.mcs_chain_stages.argtypes = [I, P, P, P, P, I, ctypes.POINTER(StageDesc)]
+        L.mcs_chain_stages.restype = I
         L.mcs_seam_graphcut_device.argtypes = [I, I, I, P, P, P, I, I, P]
         L.mcs_seam_graphcut_device.restype = I
         L.mcs_plan_seam_stats.argtypes = [P, P]
@@ -829,6 +835,22 @@ class RigJob:
         return H, {"keypoints": self._kp.tolist(), "matches": self._m.tolist(),
                    "inliers": self._inl.tolist()}
 
+    def wait_stitch(self, H_io, ok_io, out_ptr: int, out_pitch: int, out_capacity: int,
+                    stream: int = 0, super_mode: bool = False, interp: int = MCS_INTER_LINEAR):
+        """wait() + the capture's chain geometry, plan and stitch in libmcs
+        (mcs_rig_job_wait_stitch): H_io ((n - 1, 9) float64) / ok_io ((n - 1,) int32) hold the
+        pairs' homographies, updated in place (a failed pair keeps its entry); the mosaic goes to
+        out_ptr (device, rows out_pitch bytes apart) on `stream`.  Returns ((out_h, out_w),
+        stats)."""
+        w, h = ctypes.c_int(), ctypes.c_int()
+        check(self._lib.mcs_rig_job_wait_stitch(
+            self._h, H_io.ctypes.data, ok_io.ctypes.data, 1 if super_mode else 0, int(interp),
+            ctypes.c_void_p(int(out_ptr)), int(out_pitch), int(out_capacity),
+            ctypes.c_void_p(int(stream)) if stream else None, ctypes.byref(w), ctypes.byref(h),
+            self._kp.ctypes.data, self._m.ctypes.data, self._inl.ctypes.data))
+        return (h.value, w.value), {"keypoints": self._kp.tolist(), "matches": self._m.tolist(),
+                                    "inliers": self._inl.tolist()}
+
     def counts(self):
         """(captures finished on the device path, on the per-call path)."""
         a, b = ctypes.c_int(), ctypes.c_int()
@@ -845,6 +867,22 @@ class RigJob:
             self.close()
         except Exception:
             pass
+
+
+def chain_stages(pair_H, pair_ok, cam_shapes, super_mode: bool = False):
+    """mcs_chain_stages: the StageDesc of every stage of a chain from its adjacent-pair
+    homographies (pair_H (n - 1, 9) float64, pair_ok (n - 1,) flags; cam_shapes (h, w[, C]) per
+    camera) -- libmcs's restatement of estimate.chain_stages (host arithmetic, no GPU)."""
+    L = load()
+    n = len(cam_shapes)
+    H = np.ascontiguousarray(np.asarray(pair_H, np.float64).reshape(max(n - 1, 0), 9))
+    ok = np.ascontiguousarray(np.asarray(pair_ok, np.int32).reshape(max(n - 1, 0)))
+    cw = np.array([s[1] for s in cam_shapes], np.int32)
+    ch = np.array([s[0] for s in cam_shapes], np.int32)
+    out = (StageDesc * max(1, n - 1))()
+    check(L.mcs_chain_stages(n, cw.ctypes.data, ch.ctypes.data, H.ctypes.data, ok.ctypes.data,
+                             1 if super_mode else 0, out))
+    return [out[k] for k in range(n - 1)]
 
 
 def seam_graphcut_host(labels, cover, samples):

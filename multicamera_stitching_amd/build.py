@@ -30,7 +30,8 @@ ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.environ.get("HIPCC", os.path.join(ROCM, "bin", "hipcc"))
 CXX = os.environ.get("CXX", "g++")
 HOST_SRC = ["mcs_plan.cpp", "hip_rt.cpp", "mcs_runtime.cpp", "mcs_capi.cpp", "mcs_features.cpp",
-            "mcs_stream.cpp", "mcs_seam.cpp", "mcs_refine.cpp", "mcs_group.cpp", "mcs_rig.cpp"]
+            "mcs_stream.cpp", "mcs_seam.cpp", "mcs_refine.cpp", "mcs_group.cpp", "mcs_rig.cpp",
+            "mcs_chain.cpp"]
 HEADERS = ["mcs_kparams.h", "mcs_fparams.h", "mcs_common.h", "hip_rt.h", "mcs_blend.h", "mcs_ransac_core.h",
            "mcs_orb_core.h", "mcs_orb_pattern.h", "mcs_feat_int.h"]
 INC = ["-I" + os.path.join(ROOT, "include"), "-I" + CSRC]

@@ -657,6 +657,51 @@ int mcs_rig_job_wait(mcs_rig_job *j, double *H, int *ok, int *n_keypoints, int *
     return MCS_OK;
 }
 
+int mcs_rig_job_wait_stitch(mcs_rig_job *j, double *H_io, int *ok_io, int super_mode, int interp,
+                            uint8_t *d_out, int64_t out_pitch, int64_t out_capacity, void *stream,
+                            int *out_w, int *out_h, int *n_keypoints, int *n_matches,
+                            int *n_inliers)
+{
+    mcs::clear_error();
+    if (!j || !H_io || !ok_io || !d_out || !out_w || !out_h)
+        return mcs::fail(MCS_E_INVALID, "mcs_rig_job_wait_stitch: NULL argument");
+    const int np = j->n_cams - 1;
+    double H[9 * MCS_MAX_CAMS];
+    int ok[MCS_MAX_CAMS];
+    int rc = mcs_rig_job_wait(j, H, ok, n_keypoints, n_matches, n_inliers);
+    if (rc) return rc;
+    // a pair whose estimate failed keeps the caller's (the previous capture's) homography
+    for (int k = 0; k < np; k++)
+        if (ok[k]) {
+            std::memcpy(H_io + 9 * k, H + 9 * k, sizeof(double) * 9);
+            ok_io[k] = 1;
+        }
+    mcs_stage_desc st[MCS_MAX_CAMS];
+    int cw[MCS_MAX_CAMS], ch[MCS_MAX_CAMS];
+    for (int c = 0; c < j->n_cams; c++) cw[c] = j->w, ch[c] = j->h;
+    rc = mcs_chain_stages(j->n_cams, cw, ch, H_io, ok_io, super_mode, st);
+    if (rc) return rc;
+    mcs_plan *plan = nullptr;
+    rc = mcs_plan_create(st, np, j->w, j->h, j->channels, interp, j->device, &plan);
+    if (rc) return rc;
+    int w = 0, h = 0, c = 0;
+    rc = mcs_plan_out_shape(plan, &w, &h, &c);
+    if (rc == MCS_OK && ((int64_t)w * c > out_pitch || (int64_t)h * out_pitch > out_capacity))
+        rc = mcs::fail(MCS_E_SHAPE, "mosaic %d x %d does not fit the output (pitch %lld, %lld "
+                       "bytes)", w, h, (long long)out_pitch, (long long)out_capacity);
+    if (rc == MCS_OK) {
+        int64_t fs[MCS_MAX_CAMS];
+        for (int i = 0; i < j->n_cams; i++) fs[i] = (int64_t)j->w * j->h * j->channels;
+        // (the plan's geometry travels in the kernel arguments: it may go right after the launch)
+        rc = mcs_stitch_direct(plan, j->frames.data(), fs, d_out, out_pitch, out_pitch * h, 1,
+                               stream);
+    }
+    mcs_plan_destroy(plan);
+    *out_w = w;
+    *out_h = h;
+    return rc;
+}
+
 int mcs_rig_job_counts(const mcs_rig_job *j, int *device_captures, int *call_captures)
 {
     mcs::clear_error();

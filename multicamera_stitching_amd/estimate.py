@@ -17,10 +17,11 @@ re-estimates them for every capture; this module closes that loop on the GPU:
      in flight (slots 0 and 1) overlaps one capture's ORB with the previous one's pairs and
      stitch.  features() / pair_homography() are the same steps issued from Python (kept as the
      cross-check of the job: both give identical homographies);
-  3. the chain geometry on the host: stage k maps camera k+1 into the mosaic of cameras 0..k,
+  3. the chain geometry: stage k maps camera k+1 into the mosaic of cameras 0..k,
      H_k = T(o_k) . H_0 . H_1 ... H_k (pair homographies composed into camera 0's frame, o_k =
-     camera 0's origin in that mosaic), and each stage's plan fields come from geometry.py --
-     the arithmetic of StitcherBase.calibrate (:293-351), bit-identical to the reference's;
+     camera 0's origin in that mosaic), and each stage's plan fields follow the arithmetic of
+     StitcherBase.calibrate (:293-351) in one fixed FP64 order -- in libmcs (mcs_chain_stages,
+     csrc/mcs_chain.cpp, which the rig job runs itself) and restated here (chain_stages);
   4. a plan for this capture (host flattening, microseconds) and mcs_stitch_direct: every output
      pixel mapped by the exact FP64 OpenCV map in the kernel itself, no prepared tables.
 
@@ -43,7 +44,7 @@ from types import SimpleNamespace
 
 import numpy as np
 
-from . import _capi, geometry
+from . import _capi
 
 
 def _T(tx, ty):
@@ -57,16 +58,62 @@ def ratio_filter(idx, dist, ratio: float = 0.75):
     return np.nonzero(ok)[0]
 
 
+def _proj(M, x, y):
+    """M . (x, y, 1) / w truncated toward zero -- get_projection_point_dst (Utils.py:23-37) in one
+    fixed FP64 order, ((m0 x + m1 y) + m2), as csrc/mcs_chain.cpp computes it."""
+    p0 = (M[0][0] * x + M[0][1] * y) + M[0][2]
+    p1 = (M[1][0] * x + M[1][1] * y) + M[1][2]
+    p2 = (M[2][0] * x + M[2][1] * y) + M[2][2]
+    return int(p0 / p2), int(p1 / p2)
+
+
+def _mm(A, B):
+    """A . B of 3 x 3 lists, ((a0 b0 + a1 b1) + a2 b2) per entry."""
+    return [[(A[i][0] * B[0][j] + A[i][1] * B[1][j]) + A[i][2] * B[2][j] for j in range(3)]
+            for i in range(3)]
+
+
+def _stage_fields(H, a_shape, b_shape):
+    """StitcherBase.calibrate's plan fields (StitcherClass.py:293-351, geometry.stage_geometry)
+    of one stage, in the fixed FP64 order of _proj (H: a 3 x 3 list, patched in place)."""
+    ha, wa = a_shape[0], a_shape[1]
+    hb, wb = b_shape[0], b_shape[1]
+    ca = [(0, 0), (wa, 0), (wa, ha), (0, ha)]
+    a_proj = [_proj(H, x, y) for x, y in ca]
+    both = a_proj + [(0, 0), (wb, 0), (wb, hb), (0, hb)]
+    x_min = min(pt[0] for pt in both)
+    y_min = min(pt[1] for pt in both)
+    H[0][2] += float(-x_min)
+    H[1][2] += float(-y_min)
+    tx, ty = -x_min, -y_min
+    Bpts = [(tx, ty), (tx + wb, ty), (tx + wb, hb + ty), (tx, hb + ty)]
+    Apts = [_proj(H, x, y) for x, y in ca]
+    xs = [pt[0] for pt in Apts + Bpts]
+    ys = [pt[1] for pt in Apts + Bpts]
+    ABSize = (abs(max(xs)), abs(max(ys)))
+    x_limits = [max([v for v in xs if v < ABSize[0] * 0.5]),
+                min([v for v in xs if v > ABSize[0] * 0.5])]
+    y_limits = [max([v for v in ys if v < ABSize[1] * 0.5]),
+                min([v for v in ys if v > ABSize[1] * 0.5])]
+    return dict(cachedAH=np.array(H, np.float64), ABSize=ABSize, Bpts=Bpts, x_limits=x_limits,
+                y_limits=y_limits)
+
+
 def chain_stages(pair_H, cam_shapes, super_mode: bool = False):
     """Stage records (the StitcherBase fields the plan needs) of a left-to-right chain whose
     adjacent-pair homographies pair_H[k] map camera k+1 into camera k (None: uncalibrated).
     cam_shapes: (h, w[, C]) of every camera in sorted-label order.  The first None leaves its
     stage and every later one uncalibrated (pass-through): the later homographies are relative
-    to cameras with no place in the mosaic (see the module docstring)."""
+    to cameras with no place in the mosaic (see the module docstring).
+
+    The arithmetic is calibrate's (StitcherClass.py:293-351), restated in plain Python floats in
+    one fixed FP64 order -- the order csrc/mcs_chain.cpp (mcs_chain_stages, the rig job's own
+    geometry) follows, so the two agree bit for bit (tests/test_chain_cpu.py).  (numpy's 3 x 3
+    matmul runs OpenBLAS FMA kernels whose rounding depends on the host CPU.)"""
     stages = []
     b_shape = tuple(cam_shapes[0])
     ox, oy = 0, 0               # camera 0's origin in the mosaic B_k
-    P = np.eye(3)               # camera k+1 -> camera 0
+    P = [[1.0, 0.0, 0.0], [0.0, 1.0, 0.0], [0.0, 0.0, 1.0]]    # camera k+1 -> camera 0
     broken = False
     for k in range(len(cam_shapes) - 1):
         a_shape = tuple(cam_shapes[k + 1])
@@ -76,10 +123,12 @@ def chain_stages(pair_H, cam_shapes, super_mode: bool = False):
             broken = True       # (the rest of the chain has no reference frame)
             stages.append(rec)
             continue
-        P = P @ np.asarray(pair_H[k], np.float64)
-        H = _T(ox, oy) @ P
-        H = H / H[2, 2]
-        g = geometry.stage_geometry(H, a_shape, b_shape)
+        Q = [[float(v) for v in row] for row in np.asarray(pair_H[k], np.float64)]
+        P = _mm(P, Q)
+        H = _mm([[1.0, 0.0, float(ox)], [0.0, 1.0, float(oy)], [0.0, 0.0, 1.0]], P)
+        h22 = H[2][2]
+        H = [[v / h22 for v in row] for row in H]
+        g = _stage_fields(H, a_shape, b_shape)
         rec.cachedAH = g["cachedAH"]
         rec.ABSize, rec.Bpts = g["ABSize"], g["Bpts"]
         rec.x_limits, rec.y_limits = g["x_limits"], g["y_limits"]
@@ -156,6 +205,33 @@ class CaptureEstimator:
             pair_H.append(self.last_H[k])
         self.stats = st
         return pair_H
+
+    def collect_stitch(self, slot: int, out_ptr: int, out_pitch: int, out_capacity: int,
+                       stream: int = 0):
+        """collect(slot) and the stitch of that capture with its homographies, in libmcs
+        (mcs_rig_job_wait_stitch: the chain geometry of mcs_chain_stages, a plan, the direct
+        stitch on `stream`) -- no Python geometry or plan per capture.  Captures must be collected
+        in submission order (a failed pair keeps the previous capture's estimate).  Returns the
+        mosaic's (out_h, out_w)."""
+        if not hasattr(self, "_Hio"):
+            self._Hio = np.zeros((self.n_cams - 1, 9), np.float64)
+            self._okio = np.zeros(self.n_cams - 1, np.int32)
+            for k, H in enumerate(self.last_H):
+                if H is not None:
+                    self._Hio[k] = np.asarray(H, np.float64).reshape(9)
+                    self._okio[k] = 1
+        shape, st = self._jobs[slot].wait_stitch(self._Hio, self._okio, out_ptr, out_pitch,
+                                                 out_capacity, stream, self.super_mode,
+                                                 self.interp)
+        self.stats = st
+        return shape
+
+    def homographies(self):
+        """The current pair homographies (after collect_stitch: the ones the last stitch used)."""
+        if hasattr(self, "_Hio"):
+            return [self._Hio[k].reshape(3, 3).copy() if self._okio[k] else None
+                    for k in range(self.n_cams - 1)]
+        return list(self.last_H)
 
     def features(self, frame_ptrs, pool=None):
         """ORB of every camera frame (device pointers, dense h x w x C, producers finished)."""

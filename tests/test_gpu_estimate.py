@@ -59,6 +59,61 @@ def test_estimate_then_stitch_full_size(super_mode):
         est.close()
 
 
+@pytest.mark.parametrize("super_mode", [False, True])
+def test_rig_job_wait_stitch_equals_python_path(super_mode):
+    """mcs_rig_job_wait_stitch (the capture's chain geometry, plan and stitch in libmcs: no
+    Python per capture) renders the same mosaic as the Python-built path (estimate ->
+    chain_stages -> Plan -> mcs_stitch_direct) and as the CPU restatement of that geometry, and
+    keeps a failed pair's previous homography like collect() does."""
+    import torch
+    from multicamera_stitching_amd import estimate
+    W, H, N = 1920, 1080, 4
+    _, frames, _ = rig.estimation_rig(N, W, H, 3, seed=0)
+    dev = torch.device("cuda", 0)
+    d = [torch.from_numpy(f).to(dev) for f in frames]
+    torch.cuda.synchronize()
+    ptrs = [t.data_ptr() for t in d]
+    pitch = 8192 * 3
+    a = estimate.CaptureEstimator(N, W, H, 3, super_mode=super_mode)
+    b = estimate.CaptureEstimator(N, W, H, 3, super_mode=super_mode)
+    try:
+        out_a = torch.zeros((2048, pitch), dtype=torch.uint8, device=dev)
+        out_b = torch.zeros_like(out_a)
+        pair_H = a.estimate(ptrs)
+        plan = a.stitch(ptrs, pair_H, out_a.data_ptr(), pitch, out_a.numel())
+        b.submit(ptrs, 0, 0)
+        oh, ow = b.collect_stitch(0, out_b.data_ptr(), pitch, out_b.numel())
+        torch.cuda.synchronize()
+        assert (oh, ow) == (plan.out_h, plan.out_w)
+        for x, y in zip(pair_H, b.homographies()):
+            assert np.array_equal(x, y)
+        assert torch.equal(out_a[:oh], out_b[:oh])
+        got = out_b[:oh, :ow * 3].cpu().numpy().reshape(oh, ow, 3)
+        want = oracle.flat_stitch(plan.describe(), frames)
+        assert int(np.abs(got.astype(np.int16) - want.astype(np.int16)).max()) == 0
+        plan.close()
+        # a capture whose pair 1 fails (camera 2 blank: no keypoints) keeps pair 1's previous
+        # homography (and pair 2's, which also needs camera 2), as collect() does
+        blank = torch.zeros_like(d[2])
+        ptrs2 = list(ptrs)
+        ptrs2[2] = blank.data_ptr()
+        b.submit(ptrs2, 0, 0)
+        out_c = torch.zeros_like(out_a)
+        oh2, ow2 = b.collect_stitch(0, out_c.data_ptr(), pitch, out_c.numel())
+        torch.cuda.synchronize()
+        assert b.stats["inliers"][1] == 0 and b.stats["inliers"][2] == 0
+        for x, y in zip(pair_H, b.homographies()):
+            assert np.array_equal(x, y)
+        assert (oh2, ow2) == (oh, ow)
+        want2 = oracle.flat_stitch(plan.describe(), [frames[0], frames[1],
+                                                     np.zeros_like(frames[2]), frames[3]])
+        got2 = out_c[:oh, :ow * 3].cpu().numpy().reshape(oh, ow, 3)
+        assert int(np.abs(got2.astype(np.int16) - want2.astype(np.int16)).max()) == 0
+    finally:
+        a.close()
+        b.close()
+
+
 def test_rig_job_equals_python_issued_steps():
     """mcs_rig_job's device path (the capture as one launch chain: ORB batched over the cameras,
     matching / ratio / RANSAC / best model batched over the pairs, csrc/mcs_rig.cpp) gives the very

@@ -112,6 +112,10 @@ def main():
                          "device frame sets) while capture f is estimated and stitched")
     ap.add_argument("--depth", type=int, default=2,
                     help="with --pipelined: captures in flight (frame sets, rig jobs, outputs)")
+    ap.add_argument("--python-stitch", action="store_true",
+                    help="pipelined: the capture's chain geometry and plan built in Python "
+                         "(estimate.chain_stages + Plan + stitch_direct) instead of inside the rig "
+                         "job (mcs_rig_job_wait_stitch, the default with --overlap)")
     ap.add_argument("--resident", action="store_true",
                     help="with --pipelined: the frames stay in HBM (no per-capture upload): the "
                          "GPU-bound rate of estimate + stitch")
@@ -235,8 +239,10 @@ def stitch_main(args, frames, truth, W, Hh, N):
         "mosaic": [oh, ow, 3], "data": "synthetic (shared-world rig, seed 0)",
         "config": {"workload": "BASELINE configs[2] + per-capture stitch: ORB nfeatures %d, 8 "
                                "levels x 1.2, FAST 20; Hamming kNN-2, ratio 0.75; RANSAC 3.0 px, "
-                               "2000 hypotheses + LM; chain geometry + plan on the host; "
-                               "mcs_stitch_direct (paste)" % args.nfeatures,
+                               "2000 hypotheses + LM; chain geometry + plan on the host "
+                               "(%s); mcs_stitch_direct (paste)" % (
+                                   args.nfeatures, "in libmcs: mcs_rig_job_wait_stitch"
+                                   if lib_stitch else "in Python"),
                    "host_frames": "pageable, uploaded every capture",
                    "host_threads": args.threads},
         "stage_ms_per_capture": {k: round(v / args.steps * 1e3, 3) for k, v in tot.items()},
@@ -309,6 +315,14 @@ def pipelined_main(args, frames, truth, W, Hh, N):
             slot = i % D
             if i + D - 1 < n:
                 start(i + D - 1, t_start)
+            if lib_stitch:
+                # the capture's geometry, plan and stitch inside libmcs: one call per capture
+                oh, ow = est.collect_stitch(slot, out[slot].data_ptr(), pitch,
+                                            out[slot].numel(), st.cuda_stream)
+                lat.append(time.perf_counter() - t_start[slot])
+                ev_done[slot].record(st)
+                mpix += ow * oh / 1e6
+                continue
             if args.overlap:
                 pair_H = est.collect(slot)
             else:
@@ -325,8 +339,15 @@ def pipelined_main(args, frames, truth, W, Hh, N):
             pending[slot] = plan
             mpix += plan.out_w * plan.out_h / 1e6
         torch.cuda.synchronize()
+        if lib_stitch:
+            # (the plan of the last capture's geometry, for the check: chain_stages restates
+            # mcs_chain_stages bit for bit)
+            pair_H = est.homographies()
+            plan, _ = est.plan(pair_H)
+            pending.append(plan)
         return mpix, pair_H, plan, slot
 
+    lib_stitch = args.overlap and not args.python_stitch
     run(args.warmup)
     t0 = time.perf_counter()
     mpix, pair_H, plan, slot = run(args.steps)
@@ -365,8 +386,10 @@ def pipelined_main(args, frames, truth, W, Hh, N):
         "mosaic": [oh, ow, 3], "data": "synthetic (shared-world rig, seed 0)",
         "config": {"workload": "BASELINE configs[2] + per-capture stitch: ORB nfeatures %d, 8 "
                                "levels x 1.2, FAST 20; Hamming kNN-2, ratio 0.75; RANSAC 3.0 px, "
-                               "2000 hypotheses + LM; chain geometry + plan on the host; "
-                               "mcs_stitch_direct (paste)" % args.nfeatures,
+                               "2000 hypotheses + LM; chain geometry + plan on the host "
+                               "(%s); mcs_stitch_direct (paste)" % (
+                                   args.nfeatures, "in libmcs: mcs_rig_job_wait_stitch"
+                                   if lib_stitch else "in Python"),
                    "host_frames": "pinned, uploaded every capture on their own stream while the "
                                   "previous captures are estimated and stitched",
                    "pipeline_depth": D, "rig_jobs": bool(args.overlap),
