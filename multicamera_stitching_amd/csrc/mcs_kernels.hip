@@ -691,6 +691,9 @@ __device__ __forceinline__ void prepare_tile(const KParams &P, TileHdr *tiles, u
 #ifndef MCS_EXP_NOSTORE
 #define MCS_EXP_NOSTORE 0
 #endif
+#ifndef MCS_NARROW_GLOBAL
+#define MCS_NARROW_GLOBAL 0
+#endif
 
 
 // Block-uniform value read from LDS (broadcast read + readfirstlane -> SGPR).
@@ -953,14 +956,20 @@ __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *til
 #endif
                 }
             } else {
+#if MCS_NARROW_GLOBAL
+                // (variant builds: the round-4 form, 64-bit addresses -- 72 VGPRs)
+                for (int bb = 0; bb < npx * CN; bb++)
+                    o[bb] = (uint8_t)(w.at(bb >> 2) >> (8 * (bb & 3)));
+#else
                 // (a frame-edge lane: byte stores through a buffer resource over this capture's
-                // mosaic -- 32-bit offsets instead of a 64-bit address per byte)
+                // mosaic -- 32-bit offsets instead of a 64-bit address per byte: 61 VGPRs, was 72)
                 const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
                     (void *)(P.out + (int64_t)f * P.out_fstride), 0, 0x7fffffff, 0x00020000);
                 const uint32_t lo = (uint32_t)(dst - P.out);
                 for (int bb = 0; bb < npx * CN; bb++)
                     __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(w.at(bb >> 2) >> (8 * (bb & 3))),
                                                          ro, lo + (uint32_t)bb, 0, 0);
+#endif
             }
         }
         wait_vmcnt_le(full ? waitn : 0);

@@ -1,4 +1,4 @@
-"""Copies one tools/gpu_r04_final.sh (or r03) run's outputs from gpurun_out/ into profiles/<prefix>_*
+"""Copies one tools/gpu_r05_final.sh (or r04 / r03) run's outputs from gpurun_out/ into profiles/<prefix>_*
 (the committed record; gpurun_out/ is scratch).  Usage: python tools/save_record.py r03b_final"""
 import glob
 import os
@@ -46,6 +46,7 @@ for f in ("pmc_latest.json", "pmc_latest_cyl.json"):
 last_json("c3_serial.log", "c3_serial.json")
 last_json("c3_overlap.log", "c3_overlap_depth4.json")
 last_json("c3_resident.log", "c3_resident_depth4.json")
+last_json("c3_resident_pystitch.log", "c3_resident_depth4_python_stitch.json")
 last_json("c3_estimate.log", "c3_estimate_only.json")
 last_json("match.log", "match_bench.json")
 last_json("seam.log", "seam_c4.json")
