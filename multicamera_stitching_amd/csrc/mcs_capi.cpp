@@ -984,7 +984,7 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
     args.pad2_ = 0;
     if (fork) HIP_TRY(A->hipEventRecord(p->ev_fork, s));
     if (aside) HIP_TRY(A->hipStreamWaitEvent(p->side, p->ev_fork, 0));
-    if (p->n_big > 0) {
+    auto big_launch = [&](hipStream_t q) -> int {
         mcs::KStreamArgs bg = args;
         bg.order = p->d_big + 1;
         bg.n_order = p->n_big;
@@ -993,8 +993,13 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
                        &sz, HIP_LAUNCH_PARAM_END};
         HIP_TRY(A->hipModuleLaunchKernel(k->stream_big[p->fd.channels][b32 ? 1 : 0],
                                          8u * (((unsigned)p->n_big + 7u) / 8u), 1, 1, mcs::kWave,
-                                         mcs::kWavesPerBlock, 1, (unsigned)mcs::kBigStreamLds,
-                                         p->side, nullptr, cfg));
+                                         mcs::kWavesPerBlock, 1, (unsigned)mcs::kBigStreamLds, q,
+                                         nullptr, cfg));
+        return MCS_OK;
+    };
+    if (p->n_big > 0) {
+        const int rc = big_launch(p->side);
+        if (rc) return rc;
     }
     if (p->n_fallback > 0) {
         mcs::KDirectArgs da;
@@ -1018,7 +1023,7 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
     const bool split = mb && p->d_order && p->n_early > 0 && n_frames <= p->mb_chunk;
     if (mb) {
         HIP_TRY(A->hipStreamWaitEvent(p->side2, p->ev_fork, 0));
-        const int rc = launch_mb_levels(A, p, k, m, 0, std::min(p->mb_chunk, n_frames), p->side2);
+        int rc = launch_mb_levels(A, p, k, m, 0, std::min(p->mb_chunk, n_frames), p->side2);
         if (rc) return rc;
         if (!split) HIP_TRY(A->hipEventRecord(p->ev_join2, p->side2));
     }
@@ -1093,11 +1098,16 @@ int ensure_side(const Api *A, mcs_plan *p)
 {
     const bool mb = p->blend == MCS_BLEND_MULTIBAND && p->n_blend > 0;
     const bool aside = p->n_fallback > 0 || p->n_big > 0;
+    int least = 0, greatest = 0;
+    if (aside && !p->side) HIP_TRY(A->hipDeviceGetStreamPriorityRange(&least, &greatest));
     if ((aside || mb) && !p->ev_fork)
         HIP_TRY(A->hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming));
     if (aside && !p->side) {
         HIP_TRY(A->hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming));
-        HIP_TRY(A->hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking));
+        // (the least priority: a stream of its own priority level does not share a hardware
+        // queue with side2, whose band pass otherwise waited behind the large-footprint tiles --
+        // C4 multi-band launch 1.345-1.352 -> 1.315-1.317 ms same box, round 5)
+        HIP_TRY(A->hipStreamCreateWithPriority(&p->side, hipStreamNonBlocking, least));
     }
     if (mb && !p->side2) {
         HIP_TRY(A->hipEventCreateWithFlags(&p->ev_join2, hipEventDisableTiming));
