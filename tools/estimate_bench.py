@@ -240,9 +240,7 @@ def stitch_main(args, frames, truth, W, Hh, N):
         "config": {"workload": "BASELINE configs[2] + per-capture stitch: ORB nfeatures %d, 8 "
                                "levels x 1.2, FAST 20; Hamming kNN-2, ratio 0.75; RANSAC 3.0 px, "
                                "2000 hypotheses + LM; chain geometry + plan on the host "
-                               "(%s); mcs_stitch_direct (paste)" % (
-                                   args.nfeatures, "in libmcs: mcs_rig_job_wait_stitch"
-                                   if lib_stitch else "in Python"),
+                               "(in Python); mcs_stitch_direct (paste)" % args.nfeatures,
                    "host_frames": "pageable, uploaded every capture",
                    "host_threads": args.threads},
         "stage_ms_per_capture": {k: round(v / args.steps * 1e3, 3) for k, v in tot.items()},
