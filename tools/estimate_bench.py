@@ -267,7 +267,12 @@ def pipelined_main(args, frames, truth, W, Hh, N):
         t = torch.empty(f.shape, dtype=torch.uint8, pin_memory=True)
         t.numpy()[...] = f
         host.append(t)
-    d = [[torch.empty(f.shape, dtype=torch.uint8, device=dev) for f in frames] for _ in range(D)]
+    # each frame set is one allocation (the capture's cameras side by side in HBM): the direct
+    # stitch then addresses every camera with 32-bit offsets from one base (mcs_direct_*_o32; four
+    # separate allocations can land more than 4 GiB apart and take the 64-bit form, ~1.5x slower)
+    sets = [torch.empty((len(frames),) + tuple(frames[0].shape), dtype=torch.uint8, device=dev)
+            for _ in range(D)]
+    d = [[ts[i] for i in range(len(frames))] for ts in sets]
     ptrs = [[t.data_ptr() for t in ds] for ds in d]
     pitch = 8192 * 3
     out = [torch.empty((2048, pitch), dtype=torch.uint8, device=dev) for _ in range(D)]
