@@ -471,6 +471,11 @@ def rig_line(args, ctx, cpu):
                  "mb_mixed_px_per_capture": plan_stats["mb_mixed_px"],
                  "mb_r1_entries_per_capture": plan_stats["mb_r1_entries"],
                  "table_mb": round(plan_stats["table_bytes"] / 1e6, 2),
+                 # streaming reads per launch: what the footprint DMAs fetch (row spans in 16-B
+                 # chunks) and the footprint boxes they are cut from, beside the touched source
+                 "stream_dma_gb_per_launch": round(F * plan_stats["dma_bytes_per_capture"] / 1e9, 4),
+                 "stream_box_gb_per_launch": round(F * plan_stats["box_bytes_per_capture"] / 1e9, 4),
+                 "touched_source_gb_per_launch": round(F * sum(fp) * C / 1e9, 4),
                  "seams": None if seam_k is None else {
                      "method": "graph-cut (mcs_plan_find_seams, device push-relabel)",
                      "grid_log2": seam_k, "ms_once": round(seam_ms, 2),

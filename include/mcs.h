@@ -153,14 +153,16 @@ int mcs_plan_describe(const mcs_plan *plan, mcs_flat_desc *out);
  * call it on first use.  stream: hipStream_t or NULL for the plan's own stream. */
 int mcs_plan_prepare(mcs_plan *plan, void *stream);
 
-/* stats[0..13] = prepared, tiles, tiles on the LDS path, tiles on the direct path, table bytes,
+/* stats[0..15] = prepared, tiles, tiles on the LDS path, tiles on the direct path, table bytes,
  * blend mode, 32 x 64 tiles the blend kernels recompute per frame, the most owners any
  * multi-band tile blends (<= 8), multi-band tiles degraded to the feather rule (their
  * neighbourhood -- the tile grown by 16 px -- holds more than 8 owners), multi-band bands of the
  * level pass, of those the bands whose source rows are staged in the LDS ring (the rest read
  * their windows from global memory), and of the LDS-path tiles those whose footprints need the
  * large-footprint streaming launch (16 rows per wave, 120 KiB ring), then per capture the
- * multi-band blend's computed ("mixed") pixels and R1 entries.  Entries past 13 read 0. */
+ * multi-band blend's computed ("mixed") pixels and R1 entries, then per capture the bytes the
+ * LDS-path tiles' footprint DMAs read (each row's span in 16-byte chunks) and the bytes of their
+ * footprint boxes (every row at the box width).  Entries past 15 read 0. */
 int mcs_plan_stats(const mcs_plan *plan, int64_t *stats, int n);
 
 /* Blend mode of the plan (MCS_BLEND_*; default NONE = the reference's paste).  Changing it drops

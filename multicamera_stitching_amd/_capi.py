@@ -499,13 +499,14 @@ class Plan:
         check(self._lib.mcs_plan_prepare(self._h, ctypes.c_void_p(int(stream))))
 
     def stats(self) -> dict:
-        arr = (ctypes.c_int64 * 14)()
-        check(self._lib.mcs_plan_stats(self._h, arr, 14))
+        arr = (ctypes.c_int64 * 16)()
+        check(self._lib.mcs_plan_stats(self._h, arr, 16))
         return {"prepared": bool(arr[0]), "tiles": arr[1], "lds_tiles": arr[2],
                 "direct_tiles": arr[3], "table_bytes": arr[4], "blend": arr[5],
                 "blend_tiles": arr[6], "mb_owners": arr[7], "mb_degraded_tiles": arr[8],
                 "mb_bands": arr[9], "mb_bands_lds": arr[10], "big_tiles": arr[11],
-                "mb_mixed_px": arr[12], "mb_r1_entries": arr[13]}
+                "mb_mixed_px": arr[12], "mb_r1_entries": arr[13],
+                "dma_bytes_per_capture": arr[14], "box_bytes_per_capture": arr[15]}
 
     def set_blend(self, mode: int):
         """MCS_BLEND_NONE (reference paste), MCS_BLEND_FEATHER, MCS_BLEND_MULTIBAND or

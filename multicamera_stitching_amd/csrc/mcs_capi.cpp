@@ -75,6 +75,9 @@ struct mcs_plan {
     uint4 *d_bdesc16 = nullptr;    // LDS-ring band pass: descriptors + group offsets per row
     int n_bands_lds = 0;
     int64_t mb_mixed_px = 0, mb_r1 = 0;   // per capture: blend pixels computed, R1 entries
+    // per capture, streaming tiles: bytes the footprint DMAs read (row spans, 16-byte chunks) and
+    // the bytes of the footprint boxes (every row at its camera's full box width)
+    int64_t dma_bytes = 0, box_bytes = 0;
     // cylindrical plans: per-column (sin, cos) and per-row h, host copy and device table
     bool cyl = false;
     std::vector<double> cyl_tab;
@@ -753,6 +756,7 @@ void release_tables(const Api *A, mcs_plan *p)
     p->d_bdesc = nullptr;
     p->n_bands = p->n_bands_in = p->gxb = 0;
     p->mb_mixed_px = p->mb_r1 = 0;
+    p->dma_bytes = p->box_bytes = 0;
     p->d_mbdesc = nullptr;
     p->d_mbtab = nullptr;
     p->d_mbfoot = nullptr;
@@ -842,6 +846,27 @@ int prepare(const Api *A, mcs_plan *p, hipStream_t s)
     HIP_TRY(A->hipStreamSynchronize(s));
     p->n_fallback = nf;
     p->n_big = nb;
+    {
+        // the streaming launch's read volume per capture, from the tables just built (once)
+        std::vector<mcs::TileHdr> th(tiles);
+        std::vector<uint16_t> sp(tiles * mcs::kMaxTileJobs);
+        HIP_TRY(A->hipMemcpyAsync(th.data(), p->d_tiles, tiles * sizeof(mcs::TileHdr),
+                                  hipMemcpyDeviceToHost, s));
+        HIP_TRY(A->hipMemcpyAsync(sp.data(), p->d_spans, sp.size() * sizeof(uint16_t),
+                                  hipMemcpyDeviceToHost, s));
+        HIP_TRY(A->hipStreamSynchronize(s));
+        p->dma_bytes = p->box_bytes = 0;
+        for (size_t t = 0; t < tiles; t++) {
+            const mcs::TileHdr &h = th[t];
+            if (h.fits == 0) continue;
+            for (int k = 0; k < h.ncam; k++) {
+                const int rows = h.jobstart[k + 1] - h.jobstart[k];
+                p->box_bytes += (int64_t)rows * 16 * ((h.stride[k] >> 16) & 0xff);
+            }
+            for (int j = 0; j < h.njobs && j < mcs::kMaxTileJobs; j++)
+                p->dma_bytes += 16 * (int64_t)((sp[t * mcs::kMaxTileJobs + j] >> 8) & 0xff);
+        }
+    }
     if (!p->d_order) {
         // one launch list of every tile (the multi-band split builds its own, early tiles first)
         std::vector<int> tl(tiles);
@@ -1869,12 +1894,13 @@ int mcs_plan_stats(const mcs_plan *p, int64_t *stats, int n)
 {
     if (!p || !stats) return mcs::fail(MCS_E_INVALID, "NULL plan/stats");
     const int64_t tiles = (int64_t)p->gx * p->gy;
-    const int64_t v[14] = {p->prepared ? 1 : 0, tiles, tiles - p->n_fallback, p->n_fallback,
+    const int64_t v[16] = {p->prepared ? 1 : 0, tiles, tiles - p->n_fallback, p->n_fallback,
                            tiles * (int64_t)(sizeof(mcs::TileHdr) +
                                              mcs::kTilePx * (mcs::kDescWords + 1) * 4),
                            p->blend, p->n_blend, p->mb_slots, p->n_degraded, p->n_bands,
-                           p->n_bands_lds, p->n_big, p->mb_mixed_px, p->mb_r1};
-    for (int i = 0; i < n; i++) stats[i] = i < 14 ? v[i] : 0;
+                           p->n_bands_lds, p->n_big, p->mb_mixed_px, p->mb_r1,
+                           p->dma_bytes, p->box_bytes};
+    for (int i = 0; i < n; i++) stats[i] = i < 16 ? v[i] : 0;
     return MCS_OK;
 }
 

@@ -694,6 +694,11 @@ __device__ __forceinline__ void prepare_tile(const KParams &P, TileHdr *tiles, u
 #ifndef MCS_NARROW_GLOBAL
 #define MCS_NARROW_GLOBAL 0
 #endif
+// The streaming loop: 1 = steady-state and tail loops, computed-jump waits, running offsets
+// (round 5); 0 = the round-4 loop (variant builds, A/B only).
+#ifndef MCS_STREAM_LOOP2
+#define MCS_STREAM_LOOP2 1
+#endif
 
 
 // Block-uniform value read from LDS (broadcast read + readfirstlane -> SGPR).
@@ -783,6 +788,113 @@ __device__ __forceinline__ void stage_capture(const WaveJobs<BUF, NJ> &J,
     }
 }
 
+// DMA jobs as 1 KiB LDS windows (MCS_DMA_WINDOWS=1): a camera's footprint rows lie in LDS at a
+// uniform pitch (a multiple of 128 B), so the 64 lanes of one LDS-DMA instruction -- lane L writes
+// 16 bytes at M0 + 16 L -- can cover 1 KiB of consecutive rows: lane L takes row
+// (16 L + 1024 w) / pitch, chunk ((16 L + 1024 w) % pitch) / 16, and is enabled only where that
+// chunk lies in its row's span.  A 512-B pitch (C2's 128-pixel tiles) moves 2 rows per
+// instruction instead of 1, a 256-B pitch 4: half the DMA instructions per capture or fewer, and
+// the same bytes.  Every window issues its instruction (a window no span reaches enables lane 0,
+// whose 16 bytes land outside every span: no pixel reads them), so the counted vmcnt waits hold.
+#ifndef MCS_DMA_WINDOWS
+#define MCS_DMA_WINDOWS 1
+#endif
+constexpr int kDmaWindow = 16 * kWave;     // bytes of LDS one window job fills
+
+template <bool BUF, int NJ>
+struct WaveWins {
+    typedef typename std::conditional<BUF, uint32_t, const uint8_t *>::type src_t;
+    src_t src[NJ];       // per lane: frame-0 offset (BUF) / address of its 16 bytes
+    uint32_t lds[NJ];    // LDS offset of the window in slot 0 (wave-uniform)
+    bool on[NJ];         // per lane: the chunk is in its row's span
+    int n;               // windows of this wave
+    int total;           // windows of the tile
+};
+
+template <int CN, bool BUF, int NJ>
+__device__ __forceinline__ WaveWins<BUF, NJ> wave_windows(const KParams &P, const TileHdr &h,
+                                                          int wave, const uint16_t *spans, int lane)
+{
+    WaveWins<BUF, NJ> J;
+    const int ncam = uni(h.ncam);
+    int wst[kTileCams + 1];
+    wst[0] = 0;
+#pragma unroll
+    for (int k = 0; k < kTileCams; k++) {
+        const int rows = uni(h.jobstart[k + 1]) - uni(h.jobstart[k]);
+        const int pitch = uni(h.stride[k]) & 0xffff;
+        wst[k + 1] = wst[k] + (k < ncam ? (rows * pitch + kDmaWindow - 1) / kDmaWindow : 0);
+    }
+    J.total = wst[kTileCams];
+    J.n = 0;
+#pragma unroll
+    for (int jj = 0; jj < NJ; jj++) {
+        const int j = wave + jj * kWavesPerBlock;
+        J.src[jj] = 0;
+        J.lds[jj] = 0;
+        J.on[jj] = false;
+        if (j < J.total) {
+            int k = 0;
+            while (k < kTileCams - 1 && j >= wst[k + 1]) k++;
+            const int c = uni(h.cam[k]);
+            const int pitch = uni(h.stride[k]) & 0xffff;
+            const int rows = uni(h.jobstart[k + 1]) - uni(h.jobstart[k]);
+            const int off = (j - wst[k]) * kDmaWindow + 16 * lane;
+            const int ri = off / pitch, ch = (off - ri * pitch) >> 4;
+            const uint32_t sp = ri < rows ? (uint32_t)spans[uni(h.jobstart[k]) + ri] : 0u;
+            const int lo = (int)(sp & 0xffu), n = (int)((sp >> 8) & 0xffu);
+            bool on = ri < rows && ch >= lo && ch < lo + n;
+            // (a window no span reaches still issues its instruction: lane 0, row ri's chunk 0)
+            const bool none = __builtin_amdgcn_ballot_w64(on) == 0;
+            const int cch = none ? 0 : ch;
+            on = on || (none && lane == 0);
+            const int r = uni(h.rmin[k]) + min(ri, rows - 1);
+            const int64_t pitch_f = (int64_t)P.cam_w[c] * CN;
+            const int e = r == P.cam_h[c] - 1 ? (uni(h.last_shift) >> (8 * k)) & 255 : 0;
+            const int64_t in_frame = (int64_t)r * pitch_f + uni(h.cal[k]) - e + 16 * cch;
+            if constexpr (BUF)
+                J.src[jj] = (uint32_t)((uint64_t)(uintptr_t)P.cams[c] -
+                                       (uint64_t)(uintptr_t)P.base + (uint64_t)in_frame);
+            else
+                J.src[jj] = P.cams[c] + in_frame;
+            // (LDS offset from the block's LDS base: the ring follows the tile header)
+            J.lds[jj] = (uint32_t)(sizeof(TileHdr) + uni(h.base[k]) + (j - wst[k]) * kDmaWindow);
+            J.on[jj] = on;
+            J.n = jj + 1;
+        }
+    }
+    return J;
+}
+
+// Issues capture f's footprint windows into `slot`: one LDS-DMA wave instruction per window,
+// windows JJ .. n-1 of the wave (a uniform exit after the last: no mask test per absent window).
+template <int JJ, bool BUF, int NJ>
+__device__ __forceinline__ void stage_windows_from(const WaveWins<BUF, NJ> &J,
+                                                   __amdgpu_buffer_rsrc_t rs, uint8_t *slot,
+                                                   int64_t foff)
+{
+    if constexpr (JJ < NJ) {
+        if (JJ >= J.n) return;
+        if (J.on[JJ]) {
+            if constexpr (BUF)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, ((lds_u8 *)slot) + J.lds[JJ], 16,
+                                                         J.src[JJ], (int)(uint32_t)foff, 0,
+                                                         MCS_DMA_AUX);
+            else
+                __builtin_amdgcn_global_load_lds(J.src[JJ] + foff, ((lds_u8 *)slot) + J.lds[JJ],
+                                                 16, 0, MCS_DMA_AUX);
+        }
+        stage_windows_from<JJ + 1, BUF, NJ>(J, rs, slot, foff);
+    }
+}
+template <bool BUF, int NJ>
+__device__ __forceinline__ void stage_windows(const WaveWins<BUF, NJ> &J,
+                                              __amdgpu_buffer_rsrc_t rs, uint8_t *slot,
+                                              int64_t foff)
+{
+    stage_windows_from<0, BUF, NJ>(J, rs, slot, foff);
+}
+
 // s_waitcnt vmcnt(n) + lgkmcnt(0) for a block-uniform run-time n (n clamped to 15 by the caller;
 // waiting for fewer outstanding operations is always safe).
 __device__ __forceinline__ void wait_vmcnt_le(int n)
@@ -805,6 +917,38 @@ __device__ __forceinline__ void wait_vmcnt_le(int n)
     case 14: asm volatile("s_waitcnt vmcnt(14) lgkmcnt(0)" ::: "memory"); break;
     default: asm volatile("s_waitcnt vmcnt(15) lgkmcnt(0)" ::: "memory"); break;
     }
+}
+
+// The same wait as a computed jump: `entry` = 8 n + 12 selects entry n of a table of
+// `s_waitcnt vmcnt(n) lgkmcnt(0); s_branch end` pairs (8 bytes each) that starts 12 bytes past
+// the s_getpc_b64 result (the address of the instruction after it: s_add_u32, s_addc_u32 and
+// s_setpc_b64 are 4 bytes each).  5 scalar instructions per wait instead of the switch's compare
+// tree (~25); vcc is the 64-bit temporary.
+__device__ __forceinline__ uint32_t vmcnt_entry(int n) { return 8u * (uint32_t)n + 12u; }
+__device__ __forceinline__ void wait_vmcnt_jump(uint32_t entry)
+{
+    asm volatile("s_getpc_b64 vcc\n\t"
+                 "s_add_u32 vcc_lo, vcc_lo, %0\n\t"
+                 "s_addc_u32 vcc_hi, vcc_hi, 0\n\t"
+                 "s_setpc_b64 vcc\n\t"
+                 "s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_branch .Lmcs_vm_end%=\n\t"
+                 "s_waitcnt vmcnt(1) lgkmcnt(0)\n\ts_branch .Lmcs_vm_end%=\n\t"
+                 "s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_branch .Lmcs_vm_end%=\n\t"
+                 "s_waitcnt vmcnt(3) lgkmcnt(0)\n\ts_branch .Lmcs_vm_end%=\n\t"
+                 "s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_branch .Lmcs_vm_end%=\n\t"
+                 "s_waitcnt vmcnt(5) lgkmcnt(0)\n\ts_branch .Lmcs_vm_end%=\n\t"
+                 "s_waitcnt vmcnt(6) lgkmcnt(0)\n\ts_branch .Lmcs_vm_end%=\n\t"
+                 "s_waitcnt vmcnt(7) lgkmcnt(0)\n\ts_branch .Lmcs_vm_end%=\n\t"
+                 "s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_branch .Lmcs_vm_end%=\n\t"
+                 "s_waitcnt vmcnt(9) lgkmcnt(0)\n\ts_branch .Lmcs_vm_end%=\n\t"
+                 "s_waitcnt vmcnt(10) lgkmcnt(0)\n\ts_branch .Lmcs_vm_end%=\n\t"
+                 "s_waitcnt vmcnt(11) lgkmcnt(0)\n\ts_branch .Lmcs_vm_end%=\n\t"
+                 "s_waitcnt vmcnt(12) lgkmcnt(0)\n\ts_branch .Lmcs_vm_end%=\n\t"
+                 "s_waitcnt vmcnt(13) lgkmcnt(0)\n\ts_branch .Lmcs_vm_end%=\n\t"
+                 "s_waitcnt vmcnt(14) lgkmcnt(0)\n\ts_branch .Lmcs_vm_end%=\n\t"
+                 "s_waitcnt vmcnt(15) lgkmcnt(0)\n\t"
+                 ".Lmcs_vm_end%=:" ::"s"(entry)
+                 : "vcc", "memory");
 }
 
 // grid (8 * ceil(n_order / 8)), block (64, 8); the launch streams tiles order[0, n_order) (or
@@ -879,36 +1023,131 @@ __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *til
             d[p * kDescWords + 2] = d2;
         }
     }
+#if MCS_DMA_WINDOWS
+    const WaveWins<BUF, NJ> J =
+        wave_windows<CN, BUF, NJ>(P, h, wave, spans + (int64_t)tile * kMaxTileJobs, lane);
+#define MCS_STAGE(slot, foff) stage_windows<BUF, NJ>(J, rs, (slot) - sizeof(TileHdr), (foff))
+    const int njobs = J.total;   // DMA instructions per capture of the block
+#else
     const WaveJobs<BUF, NJ> J =
         wave_jobs<CN, BUF, NJ>(P, h, wave, spans + (int64_t)tile * kMaxTileJobs, lane);
+#define MCS_STAGE(slot, foff) stage_capture<BUF, NJ>(J, rs, (slot), (foff), lane)
+    const int njobs = uni(h.njobs);
+#endif
     // (BUF: raw buffer over [P.base, P.base + 4 GiB); no range clamping needed, every chunk is
     // inside a frame)
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         (void *)(BUF ? P.base : P.out), 0, 0xffffffff, 0x00020000);
-    const int ring = uni(h.ring), buf_bytes = uni(h.buf_bytes), njobs = uni(h.njobs);
+    const int ring = uni(h.ring), buf_bytes = uni(h.buf_bytes);
     const int d_min = njobs / kWavesPerBlock;
     const int waitn = min((ring - 2) * d_min, 15);
     uint8_t *dst = P.out + (int64_t)min(y, P.out_h - 1) * P.out_pitch + (int64_t)xg * CN;
     const bool wide = npx == kPx && (((uintptr_t)dst | (uintptr_t)P.out_fstride) & 3) == 0;
     const int64_t fstride = P.cam_fstride[0];
     for (int q = 0; q < ring - 1 && f_beg + q < f_end; q++)
-        stage_capture<BUF, NJ>(J, rs, ring0 + q * buf_bytes, (int64_t)(f_beg + q) * fstride,
-                               lane);
-    wait_vmcnt_le(0);
+        MCS_STAGE(ring0 + q * buf_bytes, (int64_t)(f_beg + q) * fstride);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    // Steady state: waitn = DMA instructions this wave has certainly issued after those of
-    // capture f+1 ((ring-2) later captures x D_min rows).  The DMAs (loads) complete in issue
-    // order among themselves, so with at most waitn VMEM operations of any kind outstanding,
-    // capture f+1 has landed for this wave (stores are not counted: loads and stores may complete
-    // out of order with respect to each other); the barrier makes it so for the block.  Tail
-    // captures wait for everything.
+#if MCS_STREAM_LOOP2
+    // Capture f's pixels from its ring slot at LDS offset `sf`, stored to the mosaic at byte
+    // offset `of` = f * out_fstride.  Every lane computes (a lane past the mosaic edge holds zero
+    // descriptors and reads slot byte 0); only the stores are per lane.  A wave whose lanes all
+    // store 12 aligned bytes (every interior tile) takes one branch-free store.
+    const bool all_wide =
+        __builtin_amdgcn_ballot_w64(live && wide) == __builtin_amdgcn_read_exec();
+    auto emit = [&](uint32_t sf, int64_t of) __attribute__((always_inline)) {
+        const uint8_t *b = ring0 + sf;
+#if MCS_EXP_NOCOMPUTE
+        OutWords w;
+        w.w0 = d[0] ^ (uint32_t)of;
+        w.w1 = d[1];
+        w.w2 = d[2];
+        w.w3 = d[3];
+#else
+        uint32_t rr[kPx * CN];
+        uint32_t raw[kPx][6];
+#pragma unroll
+        for (int p = 0; p < kPx; p++) {
+            const uint32_t win = d[p * kDescWords];
+            const lds_u32 *w0 = (const lds_u32 *)(((const lds_u8 *)b) + ((win & 0xffffu) & ~3u));
+            const lds_u32 *w1 = (const lds_u32 *)(((const lds_u8 *)b) + ((win >> 16) & ~3u));
+            raw[p][0] = w0[0], raw[p][1] = w0[1], raw[p][2] = w0[2];
+            raw[p][3] = w1[0], raw[p][4] = w1[1], raw[p][5] = w1[2];
+        }
+#pragma unroll
+        for (int p = 0; p < kPx; p++) {
+            const uint32_t win = d[p * kDescWords], s0 = win & 3u, s1 = (win >> 16) & 3u;
+            const uint2 r0 = make_uint2(__builtin_amdgcn_alignbyte(raw[p][1], raw[p][0], s0),
+                                        __builtin_amdgcn_alignbyte(raw[p][2], raw[p][1], s0));
+            const uint2 r1 = make_uint2(__builtin_amdgcn_alignbyte(raw[p][4], raw[p][3], s1),
+                                        __builtin_amdgcn_alignbyte(raw[p][5], raw[p][4], s1));
+#pragma unroll
+            for (int k = 0; k < CN; k++)
+                rr[p * CN + k] = blend<CN>(r0, r1, d[p * kDescWords + 1], d[p * kDescWords + 2], k);
+        }
+        const OutWords w = pack_words<CN>(rr);
+#endif
+        if (MCS_EXP_NOSTORE) return;
+        uint32_t *o32 = reinterpret_cast<uint32_t *>(dst + of);
+        if (all_wide) {
+#pragma unroll
+            for (int i = 0; i < CN; i++) {
+#if MCS_STORE_NT
+                __builtin_nontemporal_store(w.at(i), &o32[i]);
+#else
+                o32[i] = w.at(i);
+#endif
+            }
+        } else if (live) {
+            if (wide) {
+#pragma unroll
+                for (int i = 0; i < CN; i++) __builtin_nontemporal_store(w.at(i), &o32[i]);
+            } else {
+                // (a frame-edge lane: byte stores through a buffer resource over this capture's
+                // mosaic -- 32-bit offsets instead of a 64-bit address per byte)
+                const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+                    (void *)(P.out + of), 0, 0x7fffffff, 0x00020000);
+                const uint32_t lo = (uint32_t)(dst - P.out);
+                for (int bb = 0; bb < npx * CN; bb++)
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(w.at(bb >> 2) >> (8 * (bb & 3))),
+                                                         ro, lo + (uint32_t)bb, 0, 0);
+            }
+        }
+    };
+    // Steady state (captures whose iteration stages capture f + ring - 1): the wait leaves
+    // `waitn` DMA instructions outstanding -- those this wave issued after capture f + 1's
+    // ((ring - 2) later captures x D_min rows).  The DMAs (loads) complete in issue order among
+    // themselves, so with at most waitn VMEM operations of any kind outstanding, capture f + 1
+    // has landed for this wave (stores are not counted: loads and stores may complete out of
+    // order with respect to each other); the barrier makes it so for the block.  The last
+    // ring - 1 captures stage nothing and wait for everything.  Slots as LDS byte offsets,
+    // capture offsets as running sums: no multiplies in the loop.  (One loop body: a separate
+    // tail loop, a second copy of emit, costs 8 VGPRs.)
+    const uint32_t slot_end = (uint32_t)(ring * buf_bytes);
+    uint32_t sf = 0, sa = (uint32_t)((ring - 1) * buf_bytes);
+    int64_t of = (int64_t)f_beg * P.out_fstride, fa = (int64_t)(f_beg + ring - 1) * fstride;
+    const int n = f_end - f_beg, n_steady = max(0, n - (ring - 1));
+    const uint32_t wait_steady = vmcnt_entry(waitn), wait_all = vmcnt_entry(0);
+    for (int i = 0; i < n; i++) {
+        const bool steady = i < n_steady;
+        if (steady && !MCS_EXP_NODMA) MCS_STAGE(ring0 + sa, fa);
+        emit(sf, of);
+        wait_vmcnt_jump(steady ? wait_steady : wait_all);
+        __builtin_amdgcn_s_barrier();
+        sf += (uint32_t)buf_bytes;
+        sf = sf == slot_end ? 0u : sf;
+        sa += (uint32_t)buf_bytes;
+        sa = sa == slot_end ? 0u : sa;
+        fa += fstride;
+        of += P.out_fstride;
+    }
+#else
+    // (variant builds: the round-4 loop -- per-iteration staging test, run-time wait switch)
     int slot_f = 0, slot_a = ring - 1;     // slots of capture f and of capture f + ring - 1
     for (int f = f_beg; f < f_end; f++) {
         const int ahead = f + ring - 1;
         const bool full = ahead < f_end && !MCS_EXP_NODMA;
-        if (full)
-            stage_capture<BUF, NJ>(J, rs, ring0 + slot_a * buf_bytes, (int64_t)ahead * fstride,
-                                   lane);
+        if (full) MCS_STAGE(ring0 + slot_a * buf_bytes, (int64_t)ahead * fstride);
         const uint8_t *b = ring0 + slot_f * buf_bytes;
         if (live && !MCS_EXP_NOSTORE) {
 #if MCS_EXP_NOCOMPUTE
@@ -977,6 +1216,8 @@ __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *til
         slot_f = slot_f + 1 == ring ? 0 : slot_f + 1;
         slot_a = slot_a + 1 == ring ? 0 : slot_a + 1;
     }
+#endif
+#undef MCS_STAGE
 }
 
 // Direct global gather for the tiles prepare could not fit in LDS (list in fallback[1..]):
