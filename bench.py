@@ -394,7 +394,7 @@ def rig_line(args, ctx, cpu):
                 f"super{int(args.super_mode)}-F{F}-{args.blend}")
     if cyl:
         workload = f"cyl-f{args.focal:g}-" + workload + ("-gc2" if seam_k is not None else "")
-    traffic_src = None
+    traffic_src = traffic_sized = None
     try:
         pmc_json = args.pmc_json
         if pmc_json is None:
@@ -405,6 +405,7 @@ def rig_line(args, ctx, cpu):
         # of the embedded code objects (mcs_build_id), else traffic stays null
         if pm.get("workload") == workload and pm.get("build_id") == _capi.build_id():
             traffic = pm.get("hbm_bytes_per_launch")
+            traffic_sized = pm.get("hbm_bytes_sized_per_launch")
             traffic_src = os.path.relpath(pmc_json, ROOT)
     except (OSError, ValueError):
         pass
@@ -494,6 +495,9 @@ def rig_line(args, ctx, cpu):
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
             "traffic_source": traffic_src,
+            # the same counters' read side from the sized request counts (32 / 64 / 128 B)
+            # instead of FETCH_SIZE x 2 (the guide's correction assumes 128-B requests)
+            "traffic_sized": traffic_sized,
             "traffic_workload": workload,
             "build_id": _capi.build_id(),
             "bytes": "SURVEY.md 8d B_frame: every camera frame read once + the mosaic "

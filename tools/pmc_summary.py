@@ -1,6 +1,6 @@
 """Summarise tools/gpu_pmc.sh output: per-launch averages of every counter for the streaming
 kernel, HBM bytes per launch (FETCH_SIZE x 2 per the gfx950 correction in MI355X_MICROARCH.md,
-+ WRITE_SIZE; both KiB-denominated), derived ratios.  Writes profiles/pmc_latest.json (read by
++ WRITE_SIZE; both KiB-denominated) and from the sized read-request counts, derived ratios.  Writes profiles/pmc_latest.json (read by
 bench.py's roofline.traffic when the workload matches) and prints a text summary."""
 import csv
 import glob
@@ -55,6 +55,17 @@ def derived(avg):
         fetch = avg["FETCH_SIZE"] * 1024 * 2
         write = avg["WRITE_SIZE"] * 1024
         res.update(fetch_bytes=fetch, write_bytes=write, hbm_bytes=int(fetch + write))
+    if "TCC_EA0_RDREQ_sum" in avg and "TCC_EA0_RDREQ_128B_sum" in avg:
+        # read bytes from the sized request counts (32 / 64 / 128-B requests of the L2's memory
+        # side): no width assumption, unlike FETCH_SIZE x 2 (which is exact only when every
+        # request is 128 B)
+        n, n64, n128 = (avg["TCC_EA0_RDREQ_sum"], avg["TCC_EA0_RDREQ_64B_sum"],
+                        avg["TCC_EA0_RDREQ_128B_sum"])
+        sized = 128 * n128 + 64 * n64 + 32 * max(n - n64 - n128, 0)
+        res.update(read_bytes_sized=sized, read_req_128b_frac=n128 / max(n, 1),
+                   read_req_64b_frac=n64 / max(n, 1))
+        if "WRITE_SIZE" in avg:
+            res["hbm_bytes_sized"] = int(sized + avg["WRITE_SIZE"] * 1024)
     if "SQ_WAVE_CYCLES" in avg:
         for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU",
                   "SQ_ACTIVE_INST_LDS"):
@@ -85,7 +96,7 @@ def main(prefixes=("mcs_stream_c3",), workload=None, out=None, launches=None):
     # the kernels these counters belong to: bench.py reports "traffic" only for this build
     res = {"kernels": list(prefixes), "workload": workload, "build_id": _capi.build_id(),
            "per_kernel": {}}
-    total = 0
+    total = total_sized = 0
     res["launches_per_pass"] = launches
     for pre in prefixes:
         avg = family_counters(pre)
@@ -95,9 +106,12 @@ def main(prefixes=("mcs_stream_c3",), workload=None, out=None, launches=None):
         d["dispatches_per_launch"] = n / launches
         per_launch = derived({c: v / launches for c, v in tot.items()})
         d["hbm_bytes_per_launch"] = per_launch.get("hbm_bytes")
+        d["hbm_bytes_sized_per_launch"] = per_launch.get("hbm_bytes_sized")
         res["per_kernel"][pre] = d
         total += per_launch.get("hbm_bytes", 0)
+        total_sized += per_launch.get("hbm_bytes_sized", 0)
     res["hbm_bytes_per_launch"] = int(total) if total else None
+    res["hbm_bytes_sized_per_launch"] = int(total_sized) if total_sized else None
     text = json.dumps(res, indent=1, sort_keys=True)
     print(text)
     if out:
