@@ -469,6 +469,8 @@ def rig_line(args, ctx, cpu):
                  "direct_tiles": plan_stats["direct_tiles"],
                  "blend_tiles_32x64": plan_stats["blend_tiles"],
                  "mb_bands": plan_stats["mb_bands"],
+                 "mb_bands_lds_ring": plan_stats["mb_bands_lds"],
+                 "big_footprint_tiles": plan_stats["big_tiles"],
                  "mb_mixed_px_per_capture": plan_stats["mb_mixed_px"],
                  "mb_r1_entries_per_capture": plan_stats["mb_r1_entries"],
                  "table_mb": round(plan_stats["table_bytes"] / 1e6, 2),
