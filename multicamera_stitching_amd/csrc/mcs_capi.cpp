@@ -545,7 +545,13 @@ int band_lds_tables(const Api *A, mcs_plan *p, std::vector<mcs::MbBand> &bands, 
         const int w = slot == 0 ? p->kp.cam0_w : p->kp.st[slot - 1].src_w;
         const int h = slot == 0 ? p->kp.cam0_h : p->kp.st[slot - 1].src_h;
         const int64_t pitch = (int64_t)w * C, fb = pitch * h;
-        if (pitch % 4 || pitch < SP) continue;
+#ifdef MCS_BAND_DIAG   // (variant builds only: why bands keep the global form)
+        static int why[6];
+        auto diag = [&](int k) { why[k]++; fprintf(stderr, "band_lds %zu/%zu: pitch %d invalid %d rows %d span %d sched %d lds %d\n", i, nb, why[0], why[1], why[2], why[3], why[4], why[5]); };
+#else
+        auto diag = [](int) {};
+#endif
+        if (pitch % 4 || pitch < SP) { diag(0); continue; }
         uint64_t *d = desc.data() + i * DR * L;
         int y0 = INT32_MAX, y1 = -1;
         bool ok = true;
@@ -557,7 +563,7 @@ int band_lds_tables(const Api *A, mcs_plan *p, std::vector<mcs::MbBand> &bands, 
             y0 = std::min(y0, ya);
             y1 = std::max(y1, yb);
         }
-        if (!ok || y1 - y0 + 1 > 4 * (NG - 2)) continue;
+        if (!ok || y1 - y0 + 1 > 4 * (NG - 2)) { diag(ok ? 2 : 1); continue; }
         const int nr = y1 - y0 + 1;
         std::vector<int64_t> lo(nr, INT64_MAX), hi(nr, -1), bs(nr, 0);
         std::vector<int> glo(R, INT32_MAX), ghi(R, -1);
@@ -580,9 +586,11 @@ int band_lds_tables(const Api *A, mcs_plan *p, std::vector<mcs::MbBand> &bands, 
             bs[y] = std::min(hi[y] < 0 ? 0 : lo[y] & ~(int64_t)15, room);
             ok = bs[y] >= 0 && (hi[y] < 0 || hi[y] - bs[y] <= SP);
         }
+        if (!ok) { diag(3); continue; }
         for (int r = 0; r < R && ok; r++)
             ok = issue(ghi[r]) <= r - mcs::kMbLdsGLead && issue(glo[r] + K / 4) >= r;
-        if (!ok) continue;
+        if (!ok) { diag(4); continue; }
+        diag(5);
         // group table: lane l loads chunk l % 16 of row 4g + l / 16; chunks no sample of the row
         // reads, rows no sample reads and rows past the band: an offset past the frame (the
         // kernel's buffer load fetches nothing for them)
