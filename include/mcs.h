@@ -389,6 +389,23 @@ int mcs_rig_job_wait_stitch(mcs_rig_job *job, double *H_io, int *ok_io, int supe
                             int interp, uint8_t *d_out, int64_t out_pitch, int64_t out_capacity,
                             void *stream, int *out_w, int *out_h, int *n_keypoints,
                             int *n_matches, int *n_inliers);
+/* A job of n_captures captures at once (n_cams x n_captures <= MCS_MAX_CAMS): one launch chain
+ * over all their cameras, so each launch carries n_captures times the work (the rig's captures
+ * are independent; the results equal n_captures single-capture jobs bit for bit: no kernel of
+ * the chain depends on a pair's index).  submit takes n_captures x n_cams frames, capture q's
+ * cameras at q n_cams; wait returns capture-major arrays (H n_captures x (n_cams - 1) x 9,
+ * n_keypoints n_captures x n_cams, ...); wait_stitch_batch stitches capture q into d_out[q]
+ * (out_w / out_h per capture) with H_io / ok_io carried from capture to capture in order.
+ * mcs_rig_job_create is create_batch with n_captures = 1; mcs_rig_job_wait_stitch refuses a
+ * batch job. */
+int mcs_rig_job_create_batch(int n_cams, int n_captures, int w, int h, int channels,
+                             int nfeatures, int nlevels, float scale_factor, int fast_threshold,
+                             float ratio, double reproj_thresh, int iters, uint32_t seed,
+                             int device, mcs_rig_job **out);
+int mcs_rig_job_wait_stitch_batch(mcs_rig_job *job, double *H_io, int *ok_io, int super_mode,
+                                  int interp, uint8_t *const *d_out, int64_t out_pitch,
+                                  int64_t out_capacity, void *stream, int *out_w, int *out_h,
+                                  int *n_keypoints, int *n_matches, int *n_inliers);
 /* Captures the job finished on the device path (one launch chain) and on the per-call path (a
  * device ranking overflow, or MCS_RIG_PATH=calls). */
 int mcs_rig_job_counts(const mcs_rig_job *job, int *device_captures, int *call_captures);

@@ -49,7 +49,7 @@ EXPORTS = (
     "mcs_group_gather", "mcs_group_destroy", "mcs_rccl_library", "mcs_rig_job_create",
     "mcs_rig_job_submit", "mcs_rig_job_wait", "mcs_rig_job_counts", "mcs_rig_job_destroy",
     "mcs_seam_graphcut_device", "mcs_plan_seam_stats", "mcs_chain_stages",
-    "mcs_rig_job_wait_stitch",
+    "mcs_rig_job_wait_stitch", "mcs_rig_job_create_batch", "mcs_rig_job_wait_stitch_batch",
 )
 MCS_GROUP_ID_BYTES = 128
 
@@ -212,6 +212,8 @@ def load() -> ctypes.CDLL:
                                          ctypes.c_double, I, ctypes.c_uint32, I,
                                          ctypes.POINTER(P)]
         L.mcs_rig_job_create.restype = I
+        L.mcs_rig_job_create_batch.argtypes = [I] + L.mcs_rig_job_create.argtypes
+        L.mcs_rig_job_create_batch.restype = I
         L.mcs_rig_job_submit.argtypes = [P, P, P]
         L.mcs_rig_job_submit.restype = I
         L.mcs_rig_job_wait.argtypes = [P, P, P, P, P, P]
@@ -219,6 +221,8 @@ def load() -> ctypes.CDLL:
         L.mcs_rig_job_wait_stitch.argtypes = [P, P, P, I, I, P, ctypes.c_int64, ctypes.c_int64,
                                               P, P, P, P, P, P]
         L.mcs_rig_job_wait_stitch.restype = I
+        L.mcs_rig_job_wait_stitch_batch.argtypes = L.mcs_rig_job_wait_stitch.argtypes
+        L.mcs_rig_job_wait_stitch_batch.restype = I
         L.mcs_chain_stages.argtypes = [I, P, P, P, P, I, ctypes.POINTER(StageDesc)]
         L.mcs_chain_stages.restype = I
         L.mcs_seam_graphcut_device.argtypes = [I, I, I, P, P, P, I, I, P]
@@ -803,54 +807,71 @@ def orb_detect_device(ptr: int, w: int, h: int, channels: int, nfeatures: int = 
 class RigJob:
     """mcs_rig_job: the per-capture estimation of config 3 (ORB of every camera, then BF Hamming
     kNN-2 + ratio + RANSAC/LM per adjacent pair) on libmcs's worker threads.  submit() returns at
-    once; wait() gives (H list with None for failed pairs, stats dict)."""
+    once; wait() gives (H list with None for failed pairs, stats dict).  captures > 1
+    (mcs_rig_job_create_batch): one launch chain over that many captures' cameras; submit takes
+    captures x n_cams pointers, wait() returns one (H list, stats) per capture."""
 
     def __init__(self, n_cams: int, w: int, h: int, channels: int = 3, nfeatures: int = 2000,
                  nlevels: int = 8, scale_factor: float = 1.2, fast_threshold: int = 20,
                  ratio: float = 0.75, reproj_thresh: float = 3.0, iters: int = 2000,
-                 seed: int = 0, device: int = 0):
+                 seed: int = 0, device: int = 0, captures: int = 1):
         self._lib = load()
-        self.n = n_cams
+        self.n, self.q = n_cams, captures
         h_ = ctypes.c_void_p()
-        check(self._lib.mcs_rig_job_create(n_cams, w, h, channels, nfeatures, nlevels,
-                                           float(scale_factor), fast_threshold, float(ratio),
-                                           float(reproj_thresh), iters, int(seed) & 0xffffffff,
-                                           device, ctypes.byref(h_)))
+        check(self._lib.mcs_rig_job_create_batch(n_cams, captures, w, h, channels, nfeatures,
+                                                 nlevels, float(scale_factor), fast_threshold,
+                                                 float(ratio), float(reproj_thresh), iters,
+                                                 int(seed) & 0xffffffff, device, ctypes.byref(h_)))
         self._h = h_
-        self._H = np.zeros((n_cams - 1, 9), np.float64)
-        self._ok = np.zeros(n_cams - 1, np.int32)
-        self._kp = np.zeros(n_cams, np.int32)
-        self._m = np.zeros(n_cams - 1, np.int32)
-        self._inl = np.zeros(n_cams - 1, np.int32)
+        self._H = np.zeros((captures * (n_cams - 1), 9), np.float64)
+        self._ok = np.zeros(captures * (n_cams - 1), np.int32)
+        self._kp = np.zeros(captures * n_cams, np.int32)
+        self._m = np.zeros(captures * (n_cams - 1), np.int32)
+        self._inl = np.zeros(captures * (n_cams - 1), np.int32)
 
     def submit(self, frame_ptrs, wait_event: int = 0):
-        arr = (ctypes.c_void_p * self.n)(*[int(p) for p in frame_ptrs])
+        if len(frame_ptrs) != self.n * self.q:
+            raise McsError(MCS_E_INVALID, f"rig job: {self.n * self.q} frames expected, "
+                           f"{len(frame_ptrs)} given")
+        arr = (ctypes.c_void_p * (self.n * self.q))(*[int(p) for p in frame_ptrs])
         check(self._lib.mcs_rig_job_submit(self._h, arr, ctypes.c_void_p(int(wait_event)) if
                                            wait_event else None))
+
+    def _stats(self, q):
+        n, m = self.n, self.n - 1
+        return {"keypoints": self._kp[q * n:(q + 1) * n].tolist(),
+                "matches": self._m[q * m:(q + 1) * m].tolist(),
+                "inliers": self._inl[q * m:(q + 1) * m].tolist()}
 
     def wait(self):
         check(self._lib.mcs_rig_job_wait(self._h, self._H.ctypes.data, self._ok.ctypes.data,
                                          self._kp.ctypes.data, self._m.ctypes.data,
                                          self._inl.ctypes.data))
-        H = [self._H[k].reshape(3, 3).copy() if self._ok[k] else None for k in range(self.n - 1)]
-        return H, {"keypoints": self._kp.tolist(), "matches": self._m.tolist(),
-                   "inliers": self._inl.tolist()}
+        m = self.n - 1
+        res = [([self._H[q * m + k].reshape(3, 3).copy() if self._ok[q * m + k] else None
+                 for k in range(m)], self._stats(q)) for q in range(self.q)]
+        return res[0] if self.q == 1 else res
 
-    def wait_stitch(self, H_io, ok_io, out_ptr: int, out_pitch: int, out_capacity: int,
+    def wait_stitch(self, H_io, ok_io, out_ptr, out_pitch: int, out_capacity: int,
                     stream: int = 0, super_mode: bool = False, interp: int = MCS_INTER_LINEAR):
         """wait() + the capture's chain geometry, plan and stitch in libmcs
-        (mcs_rig_job_wait_stitch): H_io ((n - 1, 9) float64) / ok_io ((n - 1,) int32) hold the
-        pairs' homographies, updated in place (a failed pair keeps its entry); the mosaic goes to
-        out_ptr (device, rows out_pitch bytes apart) on `stream`.  Returns ((out_h, out_w),
-        stats)."""
-        w, h = ctypes.c_int(), ctypes.c_int()
-        check(self._lib.mcs_rig_job_wait_stitch(
+        (mcs_rig_job_wait_stitch[_batch]): H_io ((n - 1, 9) float64) / ok_io ((n - 1,) int32)
+        hold the pairs' homographies, updated in place capture by capture (a failed pair keeps
+        its entry); the mosaic goes to out_ptr (device, rows out_pitch bytes apart; a list of
+        `captures` pointers for a batch job) on `stream`.  Returns ((out_h, out_w), stats), or a
+        list of them for a batch job."""
+        ptrs = list(out_ptr) if self.q > 1 else [out_ptr]
+        if len(ptrs) != self.q:
+            raise McsError(MCS_E_INVALID, f"rig job: {self.q} outputs expected")
+        outs = (ctypes.c_void_p * self.q)(*[int(p) for p in ptrs])
+        w, h = (ctypes.c_int * self.q)(), (ctypes.c_int * self.q)()
+        check(self._lib.mcs_rig_job_wait_stitch_batch(
             self._h, H_io.ctypes.data, ok_io.ctypes.data, 1 if super_mode else 0, int(interp),
-            ctypes.c_void_p(int(out_ptr)), int(out_pitch), int(out_capacity),
-            ctypes.c_void_p(int(stream)) if stream else None, ctypes.byref(w), ctypes.byref(h),
+            outs, int(out_pitch), int(out_capacity),
+            ctypes.c_void_p(int(stream)) if stream else None, w, h,
             self._kp.ctypes.data, self._m.ctypes.data, self._inl.ctypes.data))
-        return (h.value, w.value), {"keypoints": self._kp.tolist(), "matches": self._m.tolist(),
-                                    "inliers": self._inl.tolist()}
+        res = [((h[q], w[q]), self._stats(q)) for q in range(self.q)]
+        return res[0] if self.q == 1 else res
 
     def counts(self):
         """(captures finished on the device path, on the per-call path)."""

@@ -122,6 +122,10 @@ struct RigDevice {
 
 struct mcs_rig_job {
     int n_cams, w, h, channels;
+    // captures per job (mcs_rig_job_create_batch): the chain runs over ci = n_cams x n_caps
+    // cameras, capture q's at q n_cams ..; the pairs across a capture boundary are computed with
+    // the others and never reported
+    int n_caps = 1, ci = 0;
     int nfeatures, nlevels, fast_threshold, iters;
     float scale_factor, ratio;
     double thresh;
@@ -131,7 +135,7 @@ struct mcs_rig_job {
     std::vector<const uint8_t *> frames;
     void *wait_event = nullptr;
     std::vector<Feat> feat;
-    std::vector<double> H;            // (n_cams - 1) x 9
+    std::vector<double> H;            // (ci - 1) x 9
     std::vector<int> ok, n_matches, n_inliers;
     std::vector<int> prc;             // per pair status
     std::vector<std::string> perr;
@@ -222,7 +226,7 @@ void orb_task(mcs_rig_job *j, int c)
     // a pair starts as soon as both of its cameras' features are in (pair c - 1 and pair c use
     // camera c)
     for (int k = c - 1; k <= c; k++)
-        if (k >= 0 && k < j->n_cams - 1 && j->need[k].fetch_sub(1) == 1)
+        if (k >= 0 && k < j->ci - 1 && j->need[k].fetch_sub(1) == 1)
             Pool::get().run([j, k] { pair_task(j, k); });
 }
 
@@ -244,7 +248,7 @@ int device_setup(mcs_rig_job *j)
     rc = mcs::feat::orb_geom(j->w, j->h, j->nfeatures, j->nlevels, j->scale_factor, &d.geo);
     if (rc) return rc;
     const mcs::feat::OrbGeom &g = d.geo;
-    const int C = j->n_cams, P = j->n_cams - 1, L = j->nlevels;
+    const int C = j->ci, P = j->ci - 1, L = j->nlevels;
     const int K = d.K = std::max(g.n_bound, 1);
     const size_t pix = g.off[L];
     size_t o = 0;
@@ -406,7 +410,7 @@ int enqueue_chain(mcs_rig_job *j, const mcs::rt::Api *A, const mcs::feat::Featur
 {
     RigDevice &d = j->dev;
     using mcs::feat::launch;
-    const int C = j->n_cams, P = j->n_cams - 1, L = j->nlevels;
+    const int C = j->ci, P = j->ci - 1, L = j->nlevels;
     const mcs::feat::OrbGeom &g = d.geo;
     const size_t pix = g.off[L];
     int rc = MCS_OK;
@@ -469,7 +473,7 @@ int device_capture(mcs_rig_job *j, bool *overflow)
     if (dg.err != hipSuccess)
         return mcs::fail(MCS_E_HIP, "hipSetDevice(%d): %s", j->device, A->hipGetErrorString(dg.err));
     if ((rc = mcs::feat::feature_kernels(A, j->device, &k)) != MCS_OK) return rc;
-    const int C = j->n_cams, P = j->n_cams - 1;
+    const int C = j->ci, P = j->ci - 1;
     hipStream_t s = d.s;
     if (j->wait_event) HIP_TRY(A->hipStreamWaitEvent(s, (hipEvent_t)j->wait_event, 0));
     hipError_t e = hipSuccess;
@@ -545,9 +549,9 @@ int device_capture(mcs_rig_job *j, bool *overflow)
 
 void start_calls(mcs_rig_job *j)
 {
-    j->left.store(j->n_cams - 1);
-    for (int k = 0; k < j->n_cams - 1; k++) j->need[k].store(2);
-    for (int c = 0; c < j->n_cams; c++) Pool::get().run([j, c] { orb_task(j, c); });
+    j->left.store(j->ci - 1);
+    for (int k = 0; k < j->ci - 1; k++) j->need[k].store(2);
+    for (int c = 0; c < j->ci; c++) Pool::get().run([j, c] { orb_task(j, c); });
 }
 
 void capture_task(mcs_rig_job *j)
@@ -562,7 +566,7 @@ void capture_task(mcs_rig_job *j)
     if (rc != MCS_OK) {
         // report through the pairs' status, as the per-call path does
         const char *m = mcs_last_error();
-        for (int p = 0; p < j->n_cams - 1; p++) {
+        for (int p = 0; p < j->ci - 1; p++) {
             j->prc[p] = rc;
             j->perr[p] = m ? m : "";
             j->ok[p] = 0;
@@ -579,39 +583,51 @@ void capture_task(mcs_rig_job *j)
 
 extern "C" {
 
-int mcs_rig_job_create(int n_cams, int w, int h, int channels, int nfeatures, int nlevels,
-                       float scale_factor, int fast_threshold, float ratio, double reproj_thresh,
-                       int iters, uint32_t seed, int device, mcs_rig_job **out)
+int mcs_rig_job_create_batch(int n_cams, int n_captures, int w, int h, int channels,
+                             int nfeatures, int nlevels, float scale_factor, int fast_threshold,
+                             float ratio, double reproj_thresh, int iters, uint32_t seed,
+                             int device, mcs_rig_job **out)
 {
     mcs::clear_error();
     if (!out) return mcs::fail(MCS_E_INVALID, "NULL out");
     *out = nullptr;
-    if (n_cams < 2 || n_cams > MCS_MAX_CAMS || w < 1 || h < 1 ||
+    if (n_cams < 2 || n_cams > MCS_MAX_CAMS || n_captures < 1 ||
+        n_cams * n_captures > MCS_MAX_CAMS || w < 1 || h < 1 ||
         (channels != 1 && channels != 3) || nfeatures < 1 || nlevels < 1 ||
         nlevels > mcs::kOrbMaxLevels || iters < 1 || iters > (1 << 20) ||
         !(ratio > 0.f) || !(reproj_thresh >= 0.0))
-        return mcs::fail(MCS_E_INVALID, "n_cams %d, %dx%dx%d, nfeatures %d, iters %d", n_cams, w,
-                         h, channels, nfeatures, iters);
+        return mcs::fail(MCS_E_INVALID, "n_cams %d x %d captures, %dx%dx%d, nfeatures %d, iters %d",
+                         n_cams, n_captures, w, h, channels, nfeatures, iters);
     mcs_rig_job *j = new (std::nothrow) mcs_rig_job();
     if (!j) return mcs::fail(MCS_E_NOMEM, "rig job");
-    j->n_cams = n_cams, j->w = w, j->h = h, j->channels = channels;
+    const int ci = n_cams * n_captures;
+    j->n_cams = n_cams, j->n_caps = n_captures, j->ci = ci;
+    j->w = w, j->h = h, j->channels = channels;
     j->nfeatures = nfeatures, j->nlevels = nlevels, j->fast_threshold = fast_threshold;
     j->iters = iters, j->scale_factor = scale_factor, j->ratio = ratio;
     j->thresh = reproj_thresh, j->seed = seed, j->device = device;
-    j->feat.resize(n_cams);
-    j->H.assign(9 * (size_t)(n_cams - 1), 0.0);
-    j->ok.assign(n_cams - 1, 0);
-    j->n_matches.assign(n_cams - 1, 0);
-    j->n_inliers.assign(n_cams - 1, 0);
-    j->prc.assign(n_cams - 1, MCS_OK);
-    j->perr.assign(n_cams - 1, std::string());
-    j->need.reset(new (std::nothrow) std::atomic<int>[n_cams - 1]);
+    j->feat.resize(ci);
+    j->H.assign(9 * (size_t)(ci - 1), 0.0);
+    j->ok.assign(ci - 1, 0);
+    j->n_matches.assign(ci - 1, 0);
+    j->n_inliers.assign(ci - 1, 0);
+    j->prc.assign(ci - 1, MCS_OK);
+    j->perr.assign(ci - 1, std::string());
+    j->need.reset(new (std::nothrow) std::atomic<int>[ci - 1]);
     if (!j->need) {
         delete j;
         return mcs::fail(MCS_E_NOMEM, "rig job");
     }
     *out = j;
     return MCS_OK;
+}
+
+int mcs_rig_job_create(int n_cams, int w, int h, int channels, int nfeatures, int nlevels,
+                       float scale_factor, int fast_threshold, float ratio, double reproj_thresh,
+                       int iters, uint32_t seed, int device, mcs_rig_job **out)
+{
+    return mcs_rig_job_create_batch(n_cams, 1, w, h, channels, nfeatures, nlevels, scale_factor,
+                                    fast_threshold, ratio, reproj_thresh, iters, seed, device, out);
 }
 
 int mcs_rig_job_submit(mcs_rig_job *j, const uint8_t *const *d_frames, void *wait_event)
@@ -624,7 +640,7 @@ int mcs_rig_job_submit(mcs_rig_job *j, const uint8_t *const *d_frames, void *wai
         j->busy = true;
         j->done = false;
     }
-    j->frames.assign(d_frames, d_frames + j->n_cams);
+    j->frames.assign(d_frames, d_frames + j->ci);
     j->wait_event = wait_event;
     Pool::get().run([j] { capture_task(j); });
     return MCS_OK;
@@ -641,19 +657,75 @@ int mcs_rig_job_wait(mcs_rig_job *j, double *H, int *ok, int *n_keypoints, int *
         j->cv.wait(lk, [j] { return j->done; });
         j->busy = false;
     }
-    const int np = j->n_cams - 1;
-    if (H) std::memcpy(H, j->H.data(), sizeof(double) * 9 * (size_t)np);
-    for (int k = 0; k < np; k++) {
-        if (ok) ok[k] = j->ok[k];
-        if (n_matches) n_matches[k] = j->n_matches[k];
-        if (n_inliers) n_inliers[k] = j->n_inliers[k];
-    }
-    for (int c = 0; c < j->n_cams; c++) {
+    // capture q's pair k is chain pair q n_cams + k (the pair across the boundary is skipped)
+    const int N = j->n_cams, np = N - 1;
+    for (int q = 0; q < j->n_caps; q++)
+        for (int k = 0; k < np; k++) {
+            const int p = q * N + k, o = q * np + k;
+            if (H) std::memcpy(H + 9 * o, j->H.data() + 9 * p, sizeof(double) * 9);
+            if (ok) ok[o] = j->ok[p];
+            if (n_matches) n_matches[o] = j->n_matches[p];
+            if (n_inliers) n_inliers[o] = j->n_inliers[p];
+        }
+    for (int c = 0; c < j->ci; c++) {
         if (n_keypoints) n_keypoints[c] = j->feat[c].n;
         if (j->feat[c].rc) return mcs::fail(j->feat[c].rc, "camera %d ORB: %s", c, j->feat[c].err);
     }
-    for (int k = 0; k < np; k++)
-        if (j->prc[k]) return mcs::fail(j->prc[k], "pair %d: %s", k, j->perr[k].c_str());
+    for (int q = 0; q < j->n_caps; q++)
+        for (int k = 0; k < np; k++) {
+            const int p = q * N + k;
+            if (j->prc[p]) return mcs::fail(j->prc[p], "pair %d: %s", p, j->perr[p].c_str());
+        }
+    return MCS_OK;
+}
+
+int mcs_rig_job_wait_stitch_batch(mcs_rig_job *j, double *H_io, int *ok_io, int super_mode,
+                                  int interp, uint8_t *const *d_out, int64_t out_pitch,
+                                  int64_t out_capacity, void *stream, int *out_w, int *out_h,
+                                  int *n_keypoints, int *n_matches, int *n_inliers)
+{
+    mcs::clear_error();
+    if (!j || !H_io || !ok_io || !d_out || !out_w || !out_h)
+        return mcs::fail(MCS_E_INVALID, "mcs_rig_job_wait_stitch: NULL argument");
+    const int N = j->n_cams, np = N - 1;
+    std::vector<double> H(9 * (size_t)np * j->n_caps);
+    std::vector<int> ok((size_t)np * j->n_caps);
+    int rc = mcs_rig_job_wait(j, H.data(), ok.data(), n_keypoints, n_matches, n_inliers);
+    if (rc) return rc;
+    for (int q = 0; q < j->n_caps; q++) {
+        if (!d_out[q]) return mcs::fail(MCS_E_INVALID, "mcs_rig_job_wait_stitch: NULL output %d", q);
+        // a pair whose estimate failed keeps the caller's -- the previous capture's -- homography
+        for (int k = 0; k < np; k++)
+            if (ok[q * np + k]) {
+                std::memcpy(H_io + 9 * k, H.data() + 9 * ((size_t)q * np + k), sizeof(double) * 9);
+                ok_io[k] = 1;
+            }
+        mcs_stage_desc st[MCS_MAX_CAMS];
+        int cw[MCS_MAX_CAMS], ch[MCS_MAX_CAMS];
+        for (int c = 0; c < N; c++) cw[c] = j->w, ch[c] = j->h;
+        rc = mcs_chain_stages(N, cw, ch, H_io, ok_io, super_mode, st);
+        if (rc) return rc;
+        mcs_plan *plan = nullptr;
+        rc = mcs_plan_create(st, np, j->w, j->h, j->channels, interp, j->device, &plan);
+        if (rc) return rc;
+        int w = 0, h = 0, c = 0;
+        rc = mcs_plan_out_shape(plan, &w, &h, &c);
+        if (rc == MCS_OK && ((int64_t)w * c > out_pitch || (int64_t)h * out_pitch > out_capacity))
+            rc = mcs::fail(MCS_E_SHAPE, "mosaic %d x %d does not fit the output (pitch %lld, "
+                           "%lld bytes)", w, h, (long long)out_pitch, (long long)out_capacity);
+        if (rc == MCS_OK) {
+            int64_t fs[MCS_MAX_CAMS];
+            for (int i = 0; i < N; i++) fs[i] = (int64_t)j->w * j->h * j->channels;
+            // (the plan's geometry travels in the kernel arguments: it may go right after the
+            // launch)
+            rc = mcs_stitch_direct(plan, j->frames.data() + (size_t)q * N, fs, d_out[q], out_pitch,
+                                   out_pitch * h, 1, stream);
+        }
+        mcs_plan_destroy(plan);
+        out_w[q] = w;
+        out_h[q] = h;
+        if (rc) return rc;
+    }
     return MCS_OK;
 }
 
@@ -662,44 +734,12 @@ int mcs_rig_job_wait_stitch(mcs_rig_job *j, double *H_io, int *ok_io, int super_
                             int *out_w, int *out_h, int *n_keypoints, int *n_matches,
                             int *n_inliers)
 {
-    mcs::clear_error();
-    if (!j || !H_io || !ok_io || !d_out || !out_w || !out_h)
-        return mcs::fail(MCS_E_INVALID, "mcs_rig_job_wait_stitch: NULL argument");
-    const int np = j->n_cams - 1;
-    double H[9 * MCS_MAX_CAMS];
-    int ok[MCS_MAX_CAMS];
-    int rc = mcs_rig_job_wait(j, H, ok, n_keypoints, n_matches, n_inliers);
-    if (rc) return rc;
-    // a pair whose estimate failed keeps the caller's (the previous capture's) homography
-    for (int k = 0; k < np; k++)
-        if (ok[k]) {
-            std::memcpy(H_io + 9 * k, H + 9 * k, sizeof(double) * 9);
-            ok_io[k] = 1;
-        }
-    mcs_stage_desc st[MCS_MAX_CAMS];
-    int cw[MCS_MAX_CAMS], ch[MCS_MAX_CAMS];
-    for (int c = 0; c < j->n_cams; c++) cw[c] = j->w, ch[c] = j->h;
-    rc = mcs_chain_stages(j->n_cams, cw, ch, H_io, ok_io, super_mode, st);
-    if (rc) return rc;
-    mcs_plan *plan = nullptr;
-    rc = mcs_plan_create(st, np, j->w, j->h, j->channels, interp, j->device, &plan);
-    if (rc) return rc;
-    int w = 0, h = 0, c = 0;
-    rc = mcs_plan_out_shape(plan, &w, &h, &c);
-    if (rc == MCS_OK && ((int64_t)w * c > out_pitch || (int64_t)h * out_pitch > out_capacity))
-        rc = mcs::fail(MCS_E_SHAPE, "mosaic %d x %d does not fit the output (pitch %lld, %lld "
-                       "bytes)", w, h, (long long)out_pitch, (long long)out_capacity);
-    if (rc == MCS_OK) {
-        int64_t fs[MCS_MAX_CAMS];
-        for (int i = 0; i < j->n_cams; i++) fs[i] = (int64_t)j->w * j->h * j->channels;
-        // (the plan's geometry travels in the kernel arguments: it may go right after the launch)
-        rc = mcs_stitch_direct(plan, j->frames.data(), fs, d_out, out_pitch, out_pitch * h, 1,
-                               stream);
-    }
-    mcs_plan_destroy(plan);
-    *out_w = w;
-    *out_h = h;
-    return rc;
+    if (j && j->n_caps != 1)
+        return mcs::fail(MCS_E_INVALID, "mcs_rig_job_wait_stitch: a %d-capture job needs "
+                         "mcs_rig_job_wait_stitch_batch", j->n_caps);
+    return mcs_rig_job_wait_stitch_batch(j, H_io, ok_io, super_mode, interp, &d_out, out_pitch,
+                                         out_capacity, stream, out_w, out_h, n_keypoints,
+                                         n_matches, n_inliers);
 }
 
 int mcs_rig_job_counts(const mcs_rig_job *j, int *device_captures, int *call_captures)

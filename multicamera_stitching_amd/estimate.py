@@ -154,8 +154,12 @@ class CaptureEstimator:
                  nfeatures: int = 2000, nlevels: int = 8, scale_factor: float = 1.2,
                  fast_threshold: int = 20, ratio: float = 0.75, reproj_thresh: float = 3.0,
                  iters: int = 2000, seed: int = 0, super_mode: bool = False,
-                 interp: int = _capi.MCS_INTER_LINEAR, device: int = 0, threads: int = None):
+                 interp: int = _capi.MCS_INTER_LINEAR, device: int = 0, threads: int = None,
+                 captures_per_job: int = 1):
         self.n_cams, self.w, self.h, self.c = n_cams, width, height, channels
+        # rig jobs of several captures (mcs_rig_job_create_batch: one launch chain over all their
+        # cameras; submit / collect_stitch then take that many captures at once)
+        self.batch = captures_per_job
         self.orb = (nfeatures, nlevels, scale_factor, fast_threshold)
         self.ratio, self.thresh, self.iters, self.seed = ratio, reproj_thresh, iters, seed
         self.super_mode, self.interp, self.device = super_mode, interp, device
@@ -184,7 +188,7 @@ class CaptureEstimator:
             nf, nl, sf, ft = self.orb
             self._jobs[slot] = _capi.RigJob(self.n_cams, self.w, self.h, self.c, nf, nl, sf, ft,
                                             self.ratio, self.thresh, self.iters, self.seed,
-                                            self.device)
+                                            self.device, captures=self.batch)
         return self._jobs[slot]
 
     def submit(self, frame_ptrs, wait_event: int = 0, slot: int = 0):
@@ -197,14 +201,17 @@ class CaptureEstimator:
     def collect(self, slot: int = 0):
         """Pair homographies of the capture submitted in `slot` (blocks until done); a failed
         pair keeps the previous capture's estimate."""
-        res, st = self._jobs[slot].wait()
-        pair_H = []
-        for k, H in enumerate(res):
-            if H is not None:
-                self.last_H[k] = H
-            pair_H.append(self.last_H[k])
-        self.stats = st
-        return pair_H
+        out = self._jobs[slot].wait()
+        per = []
+        for res, st in (out if self.batch > 1 else [out]):
+            pair_H = []
+            for k, H in enumerate(res):
+                if H is not None:
+                    self.last_H[k] = H
+                pair_H.append(self.last_H[k])
+            self.stats = st
+            per.append(pair_H)
+        return per if self.batch > 1 else per[0]
 
     def collect_stitch(self, slot: int, out_ptr: int, out_pitch: int, out_capacity: int,
                        stream: int = 0):
@@ -212,7 +219,8 @@ class CaptureEstimator:
         (mcs_rig_job_wait_stitch: the chain geometry of mcs_chain_stages, a plan, the direct
         stitch on `stream`) -- no Python geometry or plan per capture.  Captures must be collected
         in submission order (a failed pair keeps the previous capture's estimate).  Returns the
-        mosaic's (out_h, out_w)."""
+        mosaic's (out_h, out_w); with captures_per_job > 1, out_ptr is a list of that many outputs
+        and the result a list of shapes."""
         if not hasattr(self, "_Hio"):
             self._Hio = np.zeros((self.n_cams - 1, 9), np.float64)
             self._okio = np.zeros(self.n_cams - 1, np.int32)
@@ -220,9 +228,12 @@ class CaptureEstimator:
                 if H is not None:
                     self._Hio[k] = np.asarray(H, np.float64).reshape(9)
                     self._okio[k] = 1
-        shape, st = self._jobs[slot].wait_stitch(self._Hio, self._okio, out_ptr, out_pitch,
-                                                 out_capacity, stream, self.super_mode,
-                                                 self.interp)
+        out = self._jobs[slot].wait_stitch(self._Hio, self._okio, out_ptr, out_pitch,
+                                           out_capacity, stream, self.super_mode, self.interp)
+        if self.batch > 1:
+            self.stats = out[-1][1]
+            return [shape for shape, _ in out]
+        shape, st = out
         self.stats = st
         return shape
 

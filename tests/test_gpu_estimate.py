@@ -114,6 +114,67 @@ def test_rig_job_wait_stitch_equals_python_path(super_mode):
         b.close()
 
 
+def test_rig_job_batch_equals_single_jobs():
+    """A 3-capture rig job (mcs_rig_job_create_batch: one launch chain over 12 cameras) gives
+    every capture exactly what a single-capture job gives it -- homographies bit for bit, the
+    keypoint / match / inlier counts -- and wait_stitch_batch renders each capture's mosaic as the
+    single job's wait_stitch does, carrying a failed pair's homography from the capture before
+    (capture 1 here has a blank camera 2)."""
+    import torch
+    from multicamera_stitching_amd import _capi
+    W, H, N = 1920, 1080, 4
+    _, frames, _ = rig.estimation_rig(N, W, H, 3, seed=0)
+    dev = torch.device("cuda", 0)
+    d = [torch.from_numpy(f).to(dev) for f in frames]
+    shifted = [torch.roll(t, shifts=(7, 5), dims=(0, 1)).contiguous() for t in d]
+    blank = torch.zeros_like(d[2])
+    caps = [[t.data_ptr() for t in d], [t.data_ptr() for t in d],
+            [t.data_ptr() for t in shifted]]
+    caps[1][2] = blank.data_ptr()
+    torch.cuda.synchronize()
+    pitch = 8192 * 3
+    single = _capi.RigJob(N, W, H, 3)
+    batch = _capi.RigJob(N, W, H, 3, captures=3)
+    try:
+        want = []
+        Hio = np.zeros((N - 1, 9), np.float64)
+        okio = np.zeros(N - 1, np.int32)
+        outs_a = [torch.zeros((2048, pitch), dtype=torch.uint8, device=dev) for _ in range(3)]
+        for q in range(3):
+            single.submit(caps[q])
+            want.append(single.wait())
+            single.submit(caps[q])
+            shape, _ = single.wait_stitch(Hio, okio, outs_a[q].data_ptr(), pitch,
+                                          outs_a[q].numel())
+            want[-1] = want[-1] + (shape,)
+        batch.submit([p for c in caps for p in c])
+        got = batch.wait()
+        assert len(got) == 3
+        for (Hw, sw, _), (Hg, sg) in zip(want, got):
+            assert sw == sg
+            for x, y in zip(Hw, Hg):
+                assert (x is None) == (y is None)
+                assert x is None or np.array_equal(x, y)
+        assert got[1][1]["inliers"][1] == 0          # the blank camera's pairs failed
+        Hio2 = np.zeros((N - 1, 9), np.float64)
+        okio2 = np.zeros(N - 1, np.int32)
+        outs_b = [torch.zeros_like(o) for o in outs_a]
+        batch.submit([p for c in caps for p in c])
+        res = batch.wait_stitch(Hio2, okio2, [o.data_ptr() for o in outs_b], pitch,
+                                outs_b[0].numel())
+        torch.cuda.synchronize()
+        assert np.array_equal(Hio, Hio2) and np.array_equal(okio, okio2)
+        for q in range(3):
+            assert res[q][0] == want[q][2]
+            oh = res[q][0][0]
+            assert torch.equal(outs_a[q][:oh], outs_b[q][:oh])
+        with pytest.raises(_capi.McsError):
+            batch.submit(caps[0])                     # 12 frames expected
+    finally:
+        single.close()
+        batch.close()
+
+
 def test_rig_job_equals_python_issued_steps():
     """mcs_rig_job's device path (the capture as one launch chain: ORB batched over the cameras,
     matching / ratio / RANSAC / best model batched over the pairs, csrc/mcs_rig.cpp) gives the very

@@ -119,6 +119,12 @@ def main():
     ap.add_argument("--resident", action="store_true",
                     help="with --pipelined: the frames stay in HBM (no per-capture upload): the "
                          "GPU-bound rate of estimate + stitch")
+    ap.add_argument("--batch", type=int, default=1,
+                    help="with --pipelined --overlap: captures per rig job "
+                         "(mcs_rig_job_create_batch: one launch chain over all their cameras)")
+    ap.add_argument("--stitch-streams", action="store_true",
+                    help="pipelined: each slot's stitches on a stream of their own (default: one "
+                         "stitch stream)")
     ap.add_argument("--pinned", action="store_true",
                     help="camera frames in pinned host buffers (default: pageable numpy arrays, "
                          "as the reference's capture loop holds them)")
@@ -154,9 +160,9 @@ def main():
     line = {
         "metric": "rig homography estimations/sec (C3: 4-cam 1080p, ORB + BF Hamming kNN-2 + "
                   "RANSAC per capture)",
-        "value": round(args.steps / elapsed, 2), "unit": "captures/s", "n_gpus": 1,
-        "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+        "value": round(captures / elapsed, 2), "unit": "captures/s", "n_gpus": 1,
+        "steps": captures, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / captures * 1e3, 3), "higher_is_better": True,
         "dtype": "u8 / int popcount / f64", "data": "synthetic (shared-world rig, seed 0)",
         "config": {"workload": "BASELINE configs[2]: ORB nfeatures %d, 8 levels x 1.2, FAST 20; "
                                "Hamming kNN-2, ratio 0.75; RANSAC 3.0 px, 2000 hypotheses; 3 "
@@ -261,6 +267,9 @@ def pipelined_main(args, frames, truth, W, Hh, N):
     from multicamera_stitching_amd import estimate
     from oracle import oracle
     D = max(2, args.depth)
+    B = max(1, args.batch)          # captures per rig job (and per frame set / output slot)
+    if B > 1 and not (args.overlap and not args.python_stitch):
+        raise SystemExit("--batch needs --overlap (rig jobs) and the in-library stitch")
     dev = torch.device("cuda", 0)
     host = []
     for f in frames:
@@ -270,18 +279,24 @@ def pipelined_main(args, frames, truth, W, Hh, N):
     # each frame set is one allocation (the capture's cameras side by side in HBM): the direct
     # stitch then addresses every camera with 32-bit offsets from one base (mcs_direct_*_o32; four
     # separate allocations can land more than 4 GiB apart and take the 64-bit form, ~1.5x slower)
-    sets = [torch.empty((len(frames),) + tuple(frames[0].shape), dtype=torch.uint8, device=dev)
-            for _ in range(D)]
-    d = [[ts[i] for i in range(len(frames))] for ts in sets]
+    sets = [torch.empty((B * len(frames),) + tuple(frames[0].shape), dtype=torch.uint8,
+                        device=dev) for _ in range(D)]
+    d = [[ts[i] for i in range(B * len(frames))] for ts in sets]
     ptrs = [[t.data_ptr() for t in ds] for ds in d]
+    host_b = host * B               # capture q of a set: cameras q N .. q N + N - 1
     pitch = 8192 * 3
-    out = [torch.empty((2048, pitch), dtype=torch.uint8, device=dev) for _ in range(D)]
-    up, st = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = [torch.empty((B, 2048, pitch), dtype=torch.uint8, device=dev) for _ in range(D)]
+    out = [o[B - 1] for o in outs]  # (the set's last capture: the one the parity check reads)
+    up = torch.cuda.Stream()
+    # the stitches: one stream per slot with --stitch-streams (the captures' stitches are
+    # independent: they overlap on the GPU), else one stream for all
+    sts = [torch.cuda.Stream() for _ in range(D if args.stitch_streams else 1)]
     ev_up = [torch.cuda.Event() for _ in range(D)]
     ev_done = [torch.cuda.Event() for _ in range(D)]
     for e in ev_done:
-        e.record(st)
-    est = estimate.CaptureEstimator(N, W, Hh, 3, nfeatures=args.nfeatures, threads=args.threads)
+        e.record(sts[0])
+    est = estimate.CaptureEstimator(N, W, Hh, 3, nfeatures=args.nfeatures, threads=args.threads,
+                                    captures_per_job=B)
     pending = [None] * D          # plan of the capture last stitched from frame set / output i
     lat = []
 
@@ -289,13 +304,13 @@ def pipelined_main(args, frames, truth, W, Hh, N):
         with torch.cuda.stream(up):
             up.wait_event(ev_done[slot])          # that set's previous stitch has read it
             if not args.resident:
-                for t, h in zip(d[slot], host):
+                for t, h in zip(d[slot], host_b):
                     t.copy_(h, non_blocking=True)
             ev_up[slot].record(up)
 
     if args.resident:                             # the frames stay in HBM: uploaded once
         for ds in d:
-            for t, h in zip(ds, host):
+            for t, h in zip(ds, host_b):
                 t.copy_(h)
         torch.cuda.synchronize()
 
@@ -309,6 +324,7 @@ def pipelined_main(args, frames, truth, W, Hh, N):
             est.submit(ptrs[slot], 0 if args.resident else ev_up[slot].cuda_event, slot)
 
     def run(n):
+        n = max(1, n // B)          # rig jobs (B captures each)
         mpix = 0.0
         t_start = [0.0] * D
         lat.clear()
@@ -320,11 +336,12 @@ def pipelined_main(args, frames, truth, W, Hh, N):
                 start(i + D - 1, t_start)
             if lib_stitch:
                 # the capture's geometry, plan and stitch inside libmcs: one call per capture
-                oh, ow = est.collect_stitch(slot, out[slot].data_ptr(), pitch,
-                                            out[slot].numel(), st.cuda_stream)
+                shapes = est.collect_stitch(
+                    slot, [o.data_ptr() for o in outs[slot]] if B > 1 else out[slot].data_ptr(),
+                    pitch, out[slot].numel(), sts[slot % len(sts)].cuda_stream)
                 lat.append(time.perf_counter() - t_start[slot])
-                ev_done[slot].record(st)
-                mpix += ow * oh / 1e6
+                ev_done[slot].record(sts[slot % len(sts)])
+                mpix += sum(ow * oh for oh, ow in (shapes if B > 1 else [shapes])) / 1e6
                 continue
             if args.overlap:
                 pair_H = est.collect(slot)
@@ -337,8 +354,8 @@ def pipelined_main(args, frames, truth, W, Hh, N):
                 ev_done[slot].synchronize()
                 pending[slot].close()
             plan = est.stitch(ptrs[slot], pair_H, out[slot].data_ptr(), pitch, out[slot].numel(),
-                              stream=st.cuda_stream)
-            ev_done[slot].record(st)
+                              stream=sts[slot % len(sts)].cuda_stream)
+            ev_done[slot].record(sts[slot % len(sts)])
             pending[slot] = plan
             mpix += plan.out_w * plan.out_h / 1e6
         torch.cuda.synchronize()
@@ -355,19 +372,20 @@ def pipelined_main(args, frames, truth, W, Hh, N):
     t0 = time.perf_counter()
     mpix, pair_H, plan, slot = run(args.steps)
     elapsed = time.perf_counter() - t0
+    captures = max(1, args.steps // B) * B
     # the host link's H2D ceiling for the same transfers (pinned frames -> device, back to back
     # on the upload stream): the uploaded form's bound
     link = None
     if not args.resident:
         with torch.cuda.stream(up):
             for _ in range(2):
-                for t, h in zip(d[0], host):
+                for t, h in zip(d[0][:len(host)], host):
                     t.copy_(h, non_blocking=True)
             torch.cuda.synchronize()
             tl = time.perf_counter()
             reps = 20
             for _ in range(reps):
-                for t, h in zip(d[0], host):
+                for t, h in zip(d[0][:len(host)], host):
                     t.copy_(h, non_blocking=True)
             torch.cuda.synchronize()
             link = reps * sum(h.numel() for h in host) / (time.perf_counter() - tl) / 1e9
@@ -396,13 +414,14 @@ def pipelined_main(args, frames, truth, W, Hh, N):
                    "host_frames": "pinned, uploaded every capture on their own stream while the "
                                   "previous captures are estimated and stitched",
                    "pipeline_depth": D, "rig_jobs": bool(args.overlap),
+                   "captures_per_rig_job": B, "stitch_streams": len(sts),
                    "host_threads": args.threads},
         "frames_resident_in_hbm": bool(args.resident),
         "h2d_gb_per_s": None if link is None else
-        round(args.steps * sum(h.numel() for h in host) / elapsed / 1e9, 2),
+        round(captures * sum(h.numel() for h in host) / elapsed / 1e9, 2),
         "h2d_link_ceiling_gb_per_s": None if link is None else round(link, 2),
         "frac_of_h2d_link": None if link is None else
-        round(args.steps * sum(h.numel() for h in host) / elapsed / 1e9 / link, 3),
+        round(captures * sum(h.numel() for h in host) / elapsed / 1e9 / link, 3),
         "latency_ms_upload_to_homographies": round(float(np.mean(lat)) * 1e3, 3),
         "keypoints": est.stats.get("keypoints"), "matches": est.stats.get("matches"),
         "inliers": est.stats.get("inliers"), "max_reproj_err_px_vs_truth": errs,
