@@ -908,6 +908,21 @@ int launch_mb_levels(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KMb
         const int form = band_form(p, b.P);
         const int kind = p->n_bands_in == 0 ? 1 : (p->n_bands > p->n_bands_in ? 2 : 0);
         if (kind == 1) b.band0 = 0;
+#ifdef MCS_MB_BAND_SPLIT   // (variant builds: interior and edge bands as two launches)
+        if (kind == 2) {
+            b.band0 = 0;
+            b.nb = p->n_bands_in;
+            int rc = launch_args(A, k->mb_bands[p->fd.channels][form][0],
+                                 xcd_grid((int64_t)b.nb * gy), 1, mcs::kMbBandLanes, 1, &b,
+                                 sizeof(b), s);
+            if (rc) return rc;
+            b.band0 = p->n_bands_in;
+            b.nb = p->n_bands - p->n_bands_in;
+            return launch_args(A, k->mb_bands[p->fd.channels][form][1],
+                               xcd_grid((int64_t)b.nb * gy), 1, mcs::kMbBandLanes, 1, &b,
+                               sizeof(b), s);
+        }
+#endif
         return launch_args(A, k->mb_bands[p->fd.channels][form][kind],
                            xcd_grid((int64_t)p->n_bands * gy), 1, mcs::kMbBandLanes, 1, &b,
                            sizeof(b), s);

@@ -1448,7 +1448,10 @@ extern "C" __global__ __launch_bounds__(256) void mcs_blend_classify(const mcs::
 // (3 waves per SIMD: 129 VGPRs and no scratch; at 4 the register cap spilled 3 dwords whose
 // reloads in the global-form store path drained every load in flight, s_waitcnt vmcnt(0) --
 // C4 launch -1 %, C2 unchanged, profiles/r04_band_wpe_ab.txt)
-#define MCS_MB_BAND_ATTR(CN) __attribute__((amdgpu_waves_per_eu(3)))
+#ifndef MCS_MB_BAND_WPE
+#define MCS_MB_BAND_WPE 3
+#endif
+#define MCS_MB_BAND_ATTR(CN) __attribute__((amdgpu_waves_per_eu(MCS_MB_BAND_WPE)))
 // (the aligned entries hold the LDS ring of mode 2; the others none)
 #define MCS_MB_BAND_RING(AL)                                                                   \
     __shared__ __attribute__((aligned(16))) uint8_t ring_[(AL) ? mcs::kMbLdsBytes : 16];       \
