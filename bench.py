@@ -190,8 +190,8 @@ def main():
     if not args.no_also and args.rig == "chain" and args.blend == "multiband":
         # BASELINE configs[3] and configs[4] at this N, in these same rank processes
         also = {"c4_cylinder_multiband": guarded(lambda: rig_line(c4_args(args), ctx, cpu=False),
-                                                 ctx),
-                "c5_stream_4k": guarded(lambda: stream_line(args, ctx), ctx)}
+                                                 ctx, "c4"),
+                "c5_stream_4k": guarded(lambda: stream_line(args, ctx), ctx, "c5")}
         if rank == 0:
             if world == 1:
                 also.update(companion_lines())
@@ -204,14 +204,70 @@ def main():
     return result
 
 
-def guarded(fn, ctx):
-    """A companion line: its result, or an error string in its place (the headline line stands).
-    Every rank runs it; a rank that fails still joins the others' collectives only if the failure
-    is outside them, so errors are reported, not hidden."""
+class PeerFailed(RuntimeError):
+    """Another rank's line failed (it said so at this collective)."""
+
+
+def _flag_min(ctx, ok: bool) -> bool:
+    """All ranks' agreement (MIN of a 0/1 flag): one collective."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=ctx.dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(int(t.item()))
+
+
+def guarded(fn, ctx, name="line"):
+    """A companion line: its result, or an error in its place (the headline line stands).
+
+    Every rank runs it.  At N > 1 each collective inside the line is preceded by an agreement
+    flag (shard.set_collective_guard): a rank whose line raises contributes 0 at the others' next
+    collective point -- they stop with PeerFailed instead of waiting out the 300 s collective
+    timeout -- and every rank's error message is gathered to rank 0, which reports them all
+    ({"error": ..., "rank_errors": {rank: message}}).  Protocol: a failing rank makes exactly
+    one flag call (in its handler); a healthy rank makes one per collective point plus one at the
+    end unless a flag already told it of a failure -- so the calls always pair.  (A failure inside
+    a collective itself is not covered: the timeout bounds that.)"""
+    from multicamera_stitching_amd import shard
+    if ctx.world == 1:
+        try:
+            return fn()
+        except Exception as e:   # noqa: BLE001 -- recorded in the line
+            return {"error": f"{type(e).__name__}: {str(e)[:300]}"}
+    import torch.distributed as dist
+
+    def check():
+        if not _flag_min(ctx, True):
+            raise PeerFailed(f"another rank's {name} line failed")
+    prev = shard.set_collective_guard(check)
+    res, err, flagged = None, None, False
     try:
-        return fn()
+        res = fn()
+    except PeerFailed as e:
+        err, flagged = f"{type(e).__name__}: {e}", True
     except Exception as e:   # noqa: BLE001 -- recorded in the line
-        return {"error": f"{type(e).__name__}: {str(e)[:300]}"} if ctx.rank == 0 else None
+        err = f"{type(e).__name__}: {str(e)[:300]}"
+    finally:
+        shard.set_collective_guard(prev)
+    if not flagged and not _flag_min(ctx, err is None) and err is None:
+        err = f"PeerFailed: another rank's {name} line failed"
+    errs = [None] * ctx.world
+    dist.all_gather_object(errs, err)
+    if ctx.rank != 0:
+        return None
+    bad = {r: e for r, e in enumerate(errs) if e is not None}
+    if not bad:
+        return res
+    first = min(bad, key=lambda r: (bad[r].startswith("PeerFailed"), r))
+    return {"error": f"rank {first}: {bad[first]}", "rank_errors": bad}
+
+
+def _inject_failure(ctx, line):
+    """Test hook (tests/test_bench_dist.py): MCS_BENCH_INJECT_FAIL=rank:line makes that rank's
+    line raise after its timed region, before its parity / gather collectives."""
+    v = os.environ.get("MCS_BENCH_INJECT_FAIL", "")
+    if v and v == f"{ctx.rank}:{line}":
+        raise RuntimeError(f"injected failure on rank {ctx.rank} in line {line}")
 
 
 def c4_args(args):
@@ -333,6 +389,7 @@ def rig_line(args, ctx, cpu):
     mpix_per_launch = F * out_w * out_h / 1e6
     timed = timed_rate(step, args.steps, args.warmup, torch.cuda.synchronize, mpix_per_launch,
                        ctx, record)
+    _inject_failure(ctx, "c4" if cyl else "c2")
     launch_ms = shard.max_over_ranks([float(np.mean([a.elapsed_time(b) for a, b in ev]))],
                                      device=dev)[0]
     value = timed["value"]
@@ -543,6 +600,7 @@ def gather_all(d_out, args, stitch, group, recv, stream, ctx, mpix_per_launch, r
     best = None
     for _ in range(reps):
         torch.cuda.synchronize()
+        shard._guard()
         dist.barrier()
         t = time.perf_counter()
         shard.gather_mosaics_group(group, d_out, recv, 0, stream.cuda_stream)
@@ -604,21 +662,40 @@ def stream_line(args, ctx, w: int = 3840, h: int = 2160, depth: int = 3):
     outs = [np.empty(plan.out_shape(), np.uint8) for _ in range(depth)]
     n = [0]
     last = [None]
+    # N > 1: the ranks of a node share its host memory, so every frame crosses host DRAM once --
+    # the producer's frames live in the pipeline's pinned slots (written there once, as a camera
+    # driver or decoder would write them: mcs_stream_input / submit(NULL)) and the mosaics are
+    # read in the pinned output slots (wait without a copy), no memcpy in the timed loop.  At
+    # N = 1 the caller-array path (the Stitcher-like API: copy in, copy out).
+    zero_copy = ctx.world > 1
+    slot_set = [j % 2 for j in range(depth)]
+    if zero_copy:
+        for j in range(depth):
+            for v, c in zip(pipe.input_views(j), sets[slot_set[j]]):
+                np.copyto(v, c)
 
     def submit():
+        if zero_copy:
+            slot = pipe.submit_inplace()
+            return (slot, slot_set[slot])
         k = n[0] % 2
         n[0] += 1
         return (pipe.submit(sets[k]), k)
 
     def collect(tok):
         slot, k = tok
-        pipe.wait(slot, outs[slot])
+        if zero_copy:
+            pipe.wait(slot, copy=False)
+        else:
+            pipe.wait(slot, outs[slot])
         last[0] = (slot, k)
     frames = args.stream_frames
     tr = pipeline_loop(submit, collect, depth, frames, 2 * depth, mpix, ctx)
     slot, k = last[0]
-    mosaic = outs[slot].copy()
+    mosaic = pipe.output_view(slot).copy() if zero_copy else outs[slot].copy()
     pipe.close()
+    _inject_failure(ctx, "c5")
+    host = copy_workers_all_ranks(ctx)
     in_b = sum(c.nbytes for c in cams)
     pcie = frames * (in_b + mosaic.nbytes) / tr["seconds_rank"] / 1e9
     link = link_probe(in_b, mosaic.nbytes, reps=10)
@@ -646,7 +723,27 @@ def stream_line(args, ctx, w: int = 3840, h: int = 2160, depth: int = 3):
                                       f"own host link"},
             "pcie_gb_per_s_rank0": round(pcie, 2), "link_rank0": link,
             "frac_of_link_min_over_ranks": round(frac_min, 3),
-            "max_abs_diff": max_abs, "gather": gather}
+            "host_frames": ("zero-copy: frames in the pinned input slots, mosaics read in the "
+                            "pinned output slots (no host memcpy per capture)" if zero_copy else
+                            "caller arrays: copied into / out of the pinned slots by the copy "
+                            "pool"),
+            "host": host, "max_abs_diff": max_abs, "gather": gather}
+
+
+def copy_workers_all_ranks(ctx):
+    """The host copy-pool helpers of every rank (mcs_stream_copy_workers: the node's CPU quota
+    shared by LOCAL_WORLD_SIZE ranks) and the quota itself, as rank 0 reports them."""
+    from multicamera_stitching_amd import _capi
+    mine = _capi.stream_copy_workers()
+    allw = [mine] * ctx.world
+    if ctx.world > 1:
+        import torch.distributed as dist
+        from multicamera_stitching_amd import shard
+        shard._guard()
+        allw = [None] * ctx.world
+        dist.all_gather_object(allw, mine)
+    return {"copy_workers_per_rank": allw, "host_cpus": host_cpus(),
+            "local_world_size": int(os.environ.get("LOCAL_WORLD_SIZE", "1"))}
 
 
 def gather_last_mosaics(mosaic, ctx):
@@ -728,7 +825,7 @@ def stub_main(args, world, rank):
         dist.init_process_group("gloo")
     ctx = Ctx(world, rank, torch.device("cpu"))
 
-    def stub_rig_line(F, out_h, out_w, C, metric, with_gather):
+    def stub_rig_line(F, out_h, out_w, C, metric, with_gather, line_name="c2"):
         # capture g of the job = a known byte pattern rolled by g; rank r holds g = f * N + r
         base = torch.arange(out_h * out_w * C, dtype=torch.int64).remainder(251).to(torch.uint8)
         d_out = torch.empty((F, out_h * out_w * C), dtype=torch.uint8)
@@ -739,6 +836,7 @@ def stub_main(args, world, rank):
             time.sleep(0.002 * (rank + 1))      # ranks of different speed: max over ranks
         mpix = F * out_w * out_h / 1e6
         tr = timed_rate(stitch, args.steps, args.warmup, lambda: None, mpix, ctx)
+        _inject_failure(ctx, line_name)
         # every rank checks captures 0, F/2, F-1 against an independent restatement (numpy)
         diffs = []
         for f in check_captures(F):
@@ -785,6 +883,7 @@ def stub_main(args, world, rank):
             time.sleep(0.001 * (rank + 1))
             last[0] = tok
         tr = pipeline_loop(submit, collect, depth, frames, depth, 1e-4, ctx)
+        _inject_failure(ctx, "c5")
         slot, k = last[0]
         diff = int(np.abs(outs[slot].astype(np.int16) - src[k].astype(np.int16)).max())
         max_abs = shard.max_abs_over_ranks(diff, device=ctx.dev)
@@ -793,18 +892,20 @@ def stub_main(args, world, rank):
             got, ok = shard.gather_and_verify(torch.from_numpy(outs[slot].copy()), dst=0,
                                               device=ctx.dev)
             gather = {"verified": ok, "ranks": None if got is None else len(got)}
+        workers = copy_workers_all_ranks(ctx)
         if rank != 0:
             return None
         return {"metric": "stub stream", "value": round(frames * world / tr["seconds_max"], 3),
                 "unit": "captures/s", "n_gpus": world, "frames_per_rank": frames,
-                "max_abs_diff": max_abs, "gather": gather}
+                "max_abs_diff": max_abs, "gather": gather, "host": workers}
 
     result = stub_rig_line(4, 32, 48, 3, "stub (orchestration rehearsal, no GPU)",
                            with_gather=True)
     also = None
     if not args.no_also:
-        also = {"c4_cylinder_multiband": stub_rig_line(4, 16, 96, 3, "stub C4", True),
-                "c5_stream_4k": stub_stream_line()}
+        also = {"c4_cylinder_multiband": guarded(
+                    lambda: stub_rig_line(4, 16, 96, 3, "stub C4", True, "c4"), ctx, "c4"),
+                "c5_stream_4k": guarded(stub_stream_line, ctx, "c5")}
     if rank == 0:
         if also is not None:
             result["also"] = also

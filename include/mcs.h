@@ -258,6 +258,10 @@ int mcs_plan_footprint(mcs_plan *plan, int64_t *touched_px, int n_cams);
  * submit -- the pipeline then moves bytes only over PCIe. */
 typedef struct mcs_stream mcs_stream;
 int mcs_stream_create(mcs_plan *plan, int depth, int use_graphs, mcs_stream **out);
+/* Helper threads of this process's host copy pool (caller frames -> pinned slots, slots ->
+ * caller mosaics): half of the CPUs it may use (affinity, cgroup quota) divided among the
+ * LOCAL_WORLD_SIZE ranks of the node, minus one, at most 7.  Host only (no device). */
+int mcs_stream_copy_workers(void);
 uint8_t *mcs_stream_input(mcs_stream *stream, int slot, int cam);
 /* The pinned host mosaic of `slot` (out_h x out_w x C, dense), NULL for a bad slot. */
 const uint8_t *mcs_stream_output(const mcs_stream *stream, int slot);

@@ -457,9 +457,22 @@ def _note_orb_fallback(owner):
 
 
 # C-ABI statuses (include/mcs.h) _run_chain turns into a logged fallback image: run-time failures
-# and inputs the reference handles but the kernels do not (more cameras than MCS_MAX_CAMS, a
-# channel count outside 1-4, more than 8 cameras meeting in one multi-band tile neighbourhood)
-_RUNTIME_FAILURES = (-2, -3, -5)   # MCS_E_HIP, MCS_E_NOMEM, MCS_E_UNSUPPORTED
+# of the device.  The capacity limits -- inputs the reference handles but the kernels do not
+# (more cameras than MCS_MAX_CAMS, a channel count outside 1-4) -- are checked before the call
+# (_capacity_exceeded) and take the same logged fallback; every other status, MCS_E_UNSUPPORTED
+# included (API misuse), raises.  (More than 8 cameras meeting in one multi-band neighbourhood is
+# not an error: those tiles take the feather rule on the GPU.)
+_RUNTIME_FAILURES = (_capi.MCS_E_HIP, _capi.MCS_E_NOMEM)
+
+
+def _capacity_exceeded(cams):
+    """Why the kernels cannot take these camera images (None when they can)."""
+    if len(cams) > _capi.MCS_MAX_CAMS:
+        return "{} cameras (at most {})".format(len(cams), _capi.MCS_MAX_CAMS)
+    c = _channels(cams[0]) if cams else 1
+    if not 1 <= c <= 4:
+        return "{} channels (1-4)".format(c)
+    return None
 
 
 def _run_chain(owner, chain, cams, fallback):
@@ -472,6 +485,11 @@ def _run_chain(owner, chain, cams, fallback):
     Argument and programming errors (MCS_E_INVALID, MCS_E_SHAPE) are raised: the reference has no
     catch for them either.  (There is no CPU stitch behind it: a missing libmcs.so fails at import.)"""
     cams, cam0_hw, sizes = _conform_cameras(owner, chain, cams)
+    why = _capacity_exceeded(cams)
+    if why is not None:
+        owner.debugger(DEBUG_LEVEL_0, "[STITCHER] GPU stitch unsupported ({}); returning the "
+                       "fallback image".format(why), log_type="err")
+        return fallback
     cache = owner._cache()
     with cache.lock:
         try:

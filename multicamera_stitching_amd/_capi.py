@@ -40,6 +40,7 @@ EXPORTS = (
     "mcs_plan_stats", "mcs_stitch_host_sized", "mcs_resize_linear_device",
     "mcs_match_hamming_knn2", "mcs_match_hamming_knn2_host", "mcs_plan_set_blend",
     "mcs_ransac_homography_host", "mcs_stream_create", "mcs_stream_input", "mcs_stream_next_slot",
+    "mcs_stream_copy_workers",
     "mcs_stream_submit", "mcs_stream_wait", "mcs_stream_destroy", "mcs_orb_detect_host",
     "mcs_plan_create_cylindrical", "mcs_plan_find_seams", "mcs_plan_seam_labels",
     "mcs_seam_graphcut_host", "mcs_plan_create_warp", "mcs_plan_create_undistort",
@@ -189,6 +190,8 @@ def load() -> ctypes.CDLL:
         L.mcs_homography_refine_host.restype = I
         L.mcs_stream_create.argtypes = [P, I, I, ctypes.POINTER(P)]
         L.mcs_stream_create.restype = I
+        L.mcs_stream_copy_workers.argtypes = []
+        L.mcs_stream_copy_workers.restype = I
         L.mcs_stream_input.argtypes = [P, I, I]
         L.mcs_stream_input.restype = P
         L.mcs_stream_output.argtypes = [P, I]
@@ -503,14 +506,16 @@ class Plan:
         check(self._lib.mcs_plan_prepare(self._h, ctypes.c_void_p(int(stream))))
 
     def stats(self) -> dict:
-        arr = (ctypes.c_int64 * 16)()
-        check(self._lib.mcs_plan_stats(self._h, arr, 16))
+        arr = (ctypes.c_int64 * 20)()
+        check(self._lib.mcs_plan_stats(self._h, arr, 20))
         return {"prepared": bool(arr[0]), "tiles": arr[1], "lds_tiles": arr[2],
                 "direct_tiles": arr[3], "table_bytes": arr[4], "blend": arr[5],
                 "blend_tiles": arr[6], "mb_owners": arr[7], "mb_degraded_tiles": arr[8],
                 "mb_bands": arr[9], "mb_bands_lds": arr[10], "big_tiles": arr[11],
                 "mb_mixed_px": arr[12], "mb_r1_entries": arr[13],
-                "dma_bytes_per_capture": arr[14], "box_bytes_per_capture": arr[15]}
+                "dma_bytes_per_capture": arr[14], "box_bytes_per_capture": arr[15],
+                "mb_sweep_strips": arr[16], "mb_sweep_px": arr[17],
+                "mb_sweep_threads": arr[18], "mb_sweep_desc_rows": arr[19]}
 
     def set_blend(self, mode: int):
         """MCS_BLEND_NONE (reference paste), MCS_BLEND_FEATHER, MCS_BLEND_MULTIBAND or
@@ -780,6 +785,12 @@ class Group:
             pass
 
 
+def stream_copy_workers() -> int:
+    """Helper threads of this process's host copy pool (mcs_stream_copy_workers): the CPUs it
+    may use, shared by the node's LOCAL_WORLD_SIZE ranks."""
+    return int(load().mcs_stream_copy_workers())
+
+
 def rccl_library() -> str:
     return (load().mcs_rccl_library() or b"").decode()
 
@@ -863,6 +874,16 @@ class RigJob:
         ptrs = list(out_ptr) if self.q > 1 else [out_ptr]
         if len(ptrs) != self.q:
             raise McsError(MCS_E_INVALID, f"rig job: {self.q} outputs expected")
+        # libmcs reads and writes 9 (n - 1) doubles and (n - 1) int32 through these pointers
+        n1 = self.n - 1
+        if not (isinstance(H_io, np.ndarray) and H_io.dtype == np.float64 and
+                H_io.shape == (n1, 9) and H_io.flags.c_contiguous and H_io.flags.writeable):
+            raise McsError(MCS_E_INVALID, f"rig job: H_io must be a writable C-contiguous "
+                                          f"float64 array of shape ({n1}, 9)")
+        if not (isinstance(ok_io, np.ndarray) and ok_io.dtype == np.int32 and
+                ok_io.shape == (n1,) and ok_io.flags.c_contiguous and ok_io.flags.writeable):
+            raise McsError(MCS_E_INVALID, f"rig job: ok_io must be a writable C-contiguous "
+                                          f"int32 array of shape ({n1},)")
         outs = (ctypes.c_void_p * self.q)(*[int(p) for p in ptrs])
         w, h = (ctypes.c_int * self.q)(), (ctypes.c_int * self.q)()
         check(self._lib.mcs_rig_job_wait_stitch_batch(

@@ -24,7 +24,7 @@ CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libmcs.so")
 ARCH = os.environ.get("MCS_OFFLOAD_ARCH", "gfx950")
 # device sources -> embedded code objects (blob symbol mcs_hsaco_<name>_start)
-DEVICE = {"stitch": "mcs_kernels.hip", "features": "mcs_features.hip"}
+DEVICE = {"stitch": "mcs_kernels.hip", "features": "mcs_features.hip", "sweep": "mcs_sweep.hip"}
 HSACO = os.path.join(HERE, f"mcs_kernels.{ARCH}.hsaco")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.environ.get("HIPCC", os.path.join(ROCM, "bin", "hipcc"))
@@ -32,7 +32,7 @@ CXX = os.environ.get("CXX", "g++")
 HOST_SRC = ["mcs_plan.cpp", "hip_rt.cpp", "mcs_runtime.cpp", "mcs_capi.cpp", "mcs_features.cpp",
             "mcs_stream.cpp", "mcs_seam.cpp", "mcs_refine.cpp", "mcs_group.cpp", "mcs_rig.cpp",
             "mcs_chain.cpp"]
-HEADERS = ["mcs_kparams.h", "mcs_fparams.h", "mcs_common.h", "hip_rt.h", "mcs_blend.h", "mcs_ransac_core.h",
+HEADERS = ["mcs_kparams.h", "mcs_dev.h", "mcs_fparams.h", "mcs_common.h", "hip_rt.h", "mcs_blend.h", "mcs_ransac_core.h",
            "mcs_orb_core.h", "mcs_orb_pattern.h", "mcs_feat_int.h"]
 INC = ["-I" + os.path.join(ROOT, "include"), "-I" + CSRC]
 
@@ -89,7 +89,7 @@ def code_id(paths) -> str:
 def _stale() -> bool:
     if not (os.path.exists(LIB) and os.path.exists(HSACO)):
         return True
-    t = min(os.path.getmtime(LIB), os.path.getmtime(HSACO))
+    t = os.path.getmtime(LIB)   # (each code object is checked against its own sources: _fresh)
     deps = [os.path.join(CSRC, s) for s in [*DEVICE.values(), *HOST_SRC, *HEADERS]]
     deps += [os.path.join(ROOT, "include", "mcs.h"), __file__]
     return any(os.path.getmtime(d) > t for d in deps)
@@ -110,13 +110,23 @@ def build(force: bool = False, verbose: bool = False, lib: str = None, defines=(
     return _build_to(LIB, HSACO, [], verbose)
 
 
+def _fresh(out: str, src: str) -> bool:
+    """out is newer than its device source and every header (incremental main builds)"""
+    if not os.path.exists(out):
+        return False
+    deps = [os.path.join(CSRC, src)] + [os.path.join(CSRC, h) for h in HEADERS]
+    deps += [os.path.join(ROOT, "include", "mcs.h"), __file__]
+    return all(os.path.getmtime(d) <= os.path.getmtime(out) for d in deps)
+
+
 def _build_to(LIB: str, HSACO: str, defines, verbose: bool) -> str:
     objs = {}
     for name, src in DEVICE.items():
         out = HSACO if name == "stitch" else HSACO.replace("mcs_kernels", "mcs_" + name)
-        _run([HIPCC, *DEVICE_FLAGS, *["-D" + d for d in defines], *INC, "-o", out + ".tmp",
-              os.path.join(CSRC, src)], verbose)
-        os.replace(out + ".tmp", out)
+        if defines or not _fresh(out, src):
+            _run([HIPCC, *DEVICE_FLAGS, *["-D" + d for d in defines], *INC, "-o", out + ".tmp",
+                  os.path.join(CSRC, src)], verbose)
+            os.replace(out + ".tmp", out)
         objs[name] = out
     build_id = code_id([objs[name] for name in sorted(objs)])
     blob = LIB + ".blob.S"

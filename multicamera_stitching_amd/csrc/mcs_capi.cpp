@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -75,6 +76,15 @@ struct mcs_plan {
     uint4 *d_bdesc16 = nullptr;    // LDS-ring band pass: descriptors + group offsets per row
     int n_bands_lds = 0;
     int64_t mb_mixed_px = 0, mb_r1 = 0;   // per capture: blend pixels computed, R1 entries
+    // multi-band sweep (mcs_sweep.hip, prepare_sweep): strips, their output regions (one int per
+    // output row), window descriptors, the per-pixel skip map of the stitch kernels; n_strips = 0:
+    // the band pass + blend kernels instead
+    int n_strips = 0, sw_jb = 0;
+    mcs::MbStrip *d_strips = nullptr;
+    int *d_region = nullptr;
+    uint64_t *d_sdesc = nullptr;
+    uint8_t *d_skip = nullptr;
+    int64_t sw_px = 0, sw_desc_rows = 0;   // per capture: pixels the sweep writes; descriptor rows
     // per capture, streaming tiles: bytes the footprint DMAs read (row spans, 16-byte chunks) and
     // the bytes of the footprint boxes (every row at its camera's full box width)
     int64_t dma_bytes = 0, box_bytes = 0;
@@ -123,6 +133,9 @@ struct Kernels {
     // [channels][unaligned / dword-aligned windows][interior, bottom / right edge, both]
     hipFunction_t mb_bands[5][2][3] = {};
     hipFunction_t mb_bdesc[5][2] = {};    // [channels][interp]
+    // multi-band sweep (module kModSweep): [channels][dword-aligned windows][2 / 4 owners]
+    hipFunction_t mb_sweep[4][2][2] = {};
+    hipFunction_t mb_sweep_desc[4][2] = {};   // [channels][interp]
 };
 Kernels g_k[kMaxDevices];
 std::mutex g_k_mu;
@@ -184,6 +197,19 @@ int kernels(const Api *A, int device, const Kernels **out)
                 }
             }
         }
+        for (int c = 1; c <= 3 && rc == MCS_OK; c++)
+            for (int al = 0; al < 2 && rc == MCS_OK; al++) {
+                for (int jb = 0; jb < 2 && rc == MCS_OK; jb++) {
+                    snprintf(name, sizeof(name), "mcs_mb_sweep%s_c%d_j%d", al ? "_a" : "", c,
+                             jb ? 4 : 2);
+                    rc = mcs::module_function(A, device, mcs::kModSweep, name,
+                                              &k.mb_sweep[c][al][jb]);
+                }
+                snprintf(name, sizeof(name), "mcs_mb_sweep_desc_c%d_i%d", c, al);
+                if (rc == MCS_OK)
+                    rc = mcs::module_function(A, device, mcs::kModSweep, name,
+                                              &k.mb_sweep_desc[c][al]);
+            }
         if (rc == MCS_OK) rc = fn("mcs_footprint_i0", &k.footprint[0]);
         if (rc == MCS_OK) rc = fn("mcs_footprint_i1", &k.footprint[1]);
         if (rc == MCS_OK) rc = fn("mcs_blend_owner_i0", &k.blend_owner[0]);
@@ -653,6 +679,272 @@ int band_lds_tables(const Api *A, mcs_plan *p, std::vector<mcs::MbBand> &bands, 
     return MCS_OK;
 }
 
+// The multi-band sweep of a plan (mcs_sweep.hip), once, after mb_prep: from the mixed pixels mb_prep
+// listed per 32 x 64 blend tile,
+//   1. per blend-tile row, segments: the listed tiles with mixed pixels, merged where their mixed
+//      column hulls lie within 32 px; per output row of a segment its region = the 4-aligned
+//      span of that row's mixed pixels;
+//   2. runs: a segment continues the run of the row above whose column hull, with it, still fits
+//      the window's 100 output columns and whose owners (every owner within 16 px of the run's
+//      regions: the masks the blend reads there) stay <= kSwMaxOwners; otherwise it starts one;
+//   3. per run a strip (window c0 centred on the hull, rows from ya - 16), the R1 / B2 column
+//      ranges its regions read, checked against the columns the window computes;
+//   4. the skip map (stitch kernels) and the window descriptors (mcs_mb_sweep_desc).
+// Plans the sweep cannot take -- 4 channels, narrow mosaics, a run past the ranges, a region in a
+// tile degraded to the feather rule (more than 8 owners near it), MCS_MB_SWEEP=0 -- keep the band
+// pass + blend kernels (n_strips = 0).
+int prepare_sweep(const Api *A, mcs_plan *p, const Kernels *k, hipStream_t s)
+{
+    p->n_strips = 0;
+    // opt-in (MCS_MB_SWEEP=1): bit-exact, but measured 3x slower than the band pass + blend on
+    // the C2 / C4 launches -- latency-bound at ~1 workgroup per CU
+    const char *e = getenv("MCS_MB_SWEEP");
+    if (!e || e[0] != '1') return MCS_OK;
+    const int n = p->n_blend, S = p->mb_slots, C = p->fd.channels;
+    const int W = p->fd.out_w, H = p->fd.out_h;
+    if (n == 0 || C > 3 || W < 128 || H < 128 || W >= 32768 || H >= 32768) return MCS_OK;
+    const mcs::KParams &P = p->kp;
+    for (int c = 0; c <= P.n_stages; c++) {
+        if (c == 0 && P.cam0_w == 0) continue;     // (cylindrical plans: no slot-0 camera)
+        const int64_t w = c == 0 ? P.cam0_w : P.st[c - 1].src_w;
+        const int64_t h = c == 0 ? P.cam0_h : P.st[c - 1].src_h;
+        if ((h - 1) * w * C < 16 || w < 2 || h < 2) return MCS_OK;
+    }
+    const int TW = mcs::kBlendTileW, TH = mcs::kBlendTileH;
+    const int gxb = (W + TW - 1) / TW, gyb = (H + TH - 1) / TH;
+    // the tile list, per tile its pixel count and mixed-pixel list (mb_prep), the owner map
+    const size_t words = (size_t)mcs::mb_tab_words(S);
+    const size_t cnt_at = (size_t)S * (mcs::kMbNRX * mcs::kMbNRY + mcs::kMbN2X * mcs::kMbN2Y) +
+                          mcs::kMbNRX * mcs::kMbNRY + mcs::kMbN2X * mcs::kMbN2Y;
+    const size_t rec = mcs::kMbTabCounts + mcs::kMbTilePx / 2;   // counts + pixel list (words)
+    std::vector<int> list(1 + 2 * (size_t)n);
+    std::vector<int32_t> tab((size_t)n * rec);
+    std::vector<uint8_t> own((size_t)W * H);
+    HIP_TRY(A->hipMemcpyAsync(list.data(), p->d_blist, list.size() * sizeof(int),
+                              hipMemcpyDeviceToHost, s));
+    HIP_TRY(A->hipMemcpy2DAsync(tab.data(), rec * 4, p->d_mbtab + cnt_at, words * 4, rec * 4,
+                                (size_t)n, hipMemcpyDeviceToHost, s));
+    HIP_TRY(A->hipMemcpyAsync(own.data(), p->d_owner, own.size(), hipMemcpyDeviceToHost, s));
+    HIP_TRY(A->hipStreamSynchronize(s));
+    auto owners_in = [&](int x0, int x1, int y0, int y1) -> uint32_t {
+        x0 = std::max(x0, 0), x1 = std::min(x1, W), y0 = std::max(y0, 0), y1 = std::min(y1, H);
+        uint32_t m = 0;
+        for (int y = y0; y < y1; y++) {
+            const uint8_t *r = own.data() + (size_t)y * W;
+            for (int x = x0; x < x1; x++)
+                if (r[x] != mcs::kBlendNone) m |= 1u << r[x];
+        }
+        return m;
+    };
+    // tiles degraded to the feather rule (more than kBlendSlots owners in tile + 16 px)
+    std::vector<char> dense((size_t)gxb * gyb, 0);
+    for (int ty = 0; ty < gyb; ty++)
+        for (int tx = 0; tx < gxb; tx++)
+            dense[(size_t)ty * gxb + tx] =
+                __builtin_popcount(owners_in(tx * TW - mcs::kBlendHalo, tx * TW + TW + mcs::kBlendHalo,
+                                             ty * TH - mcs::kBlendHalo,
+                                             ty * TH + TH + mcs::kBlendHalo)) > mcs::kBlendSlots;
+    // 1. segments per tile row: per output row of the segment [lo, hi] of its mixed pixels
+    struct Seg {
+        int x0, x1;                 // 4-aligned column hull
+        std::vector<int> lo, hi;    // per row of the tile row (lo > hi: none)
+    };
+    std::vector<std::vector<Seg>> segs((size_t)gyb);
+    int64_t n_mixed = 0, n_r1 = 0;
+    for (int i = 0; i < n; i++) {
+        const int32_t *c = tab.data() + (size_t)i * rec;
+        const int npx = c[0];
+        n_mixed += npx;
+        n_r1 += c[1];
+        if (npx == 0) continue;
+        const int t = list[1 + 2 * i], tx = t % gxb, ty = t / gxb;
+        const uint16_t *px = reinterpret_cast<const uint16_t *>(c + mcs::kMbTabCounts);
+        Seg g;
+        g.lo.assign(TH, 1 << 30);
+        g.hi.assign(TH, -1);
+        for (int q = 0; q < npx; q++) {
+            const int r = px[q] / TW, x = tx * TW + px[q] % TW;
+            g.lo[r] = std::min(g.lo[r], x);
+            g.hi[r] = std::max(g.hi[r], x);
+        }
+        int mn = 1 << 30, mx = -1;
+        for (int r = 0; r < TH; r++)
+            if (g.lo[r] <= g.hi[r]) mn = std::min(mn, g.lo[r]), mx = std::max(mx, g.hi[r]);
+        g.x0 = mn & ~3;
+        g.x1 = std::min((mx + 4) & ~3, W);
+        std::vector<Seg> &row = segs[(size_t)ty];
+        // (the list is in tile order; merged hulls stay within one window's output columns)
+        if (!row.empty() && g.x0 <= row.back().x1 + 32 &&
+            std::max(row.back().x1, g.x1) - row.back().x0 <= mcs::kSwValid) {
+            Seg &b = row.back();
+            b.x1 = std::max(b.x1, g.x1);
+            for (int r = 0; r < TH; r++)
+                b.lo[r] = std::min(b.lo[r], g.lo[r]), b.hi[r] = std::max(b.hi[r], g.hi[r]);
+        } else {
+            row.push_back(std::move(g));
+        }
+    }
+    p->mb_mixed_px = n_mixed;
+    p->mb_r1 = n_r1;
+    // 2. runs of segments down the tile rows
+    struct Run {
+        int x0, x1, ty0, ty1;
+        std::vector<int> seg;       // segment index per tile row ty0 .. ty1
+        uint32_t owners;
+    };
+    std::vector<Run> runs;
+    std::vector<int> open;          // runs that reached the previous tile row
+    auto run_owners = [&](int x0, int x1, int ty0, int ty1) {
+        return owners_in(x0 - 16, x1 + 16, ty0 * TH - 16, std::min(ty1 * TH + TH, H) + 16);
+    };
+    for (int ty = 0; ty < gyb; ty++) {
+        std::vector<int> next;
+        for (size_t gi = 0; gi < segs[(size_t)ty].size(); gi++) {
+            const Seg &g = segs[(size_t)ty][gi];
+            int pick = -1;
+            for (size_t oi = 0; oi < open.size() && pick < 0; oi++) {
+                Run &r = runs[(size_t)open[oi]];
+                const int x0 = std::min(r.x0, g.x0), x1 = std::max(r.x1, g.x1);
+                if (x1 - x0 > mcs::kSwValid) continue;
+                if (std::max(r.x0, g.x0) > std::min(r.x1, g.x1) + 32) continue;
+                const uint32_t ow = run_owners(x0, x1, r.ty0, ty);
+                if (__builtin_popcount(ow) > mcs::kSwMaxOwners) continue;
+                pick = open[oi];
+                open.erase(open.begin() + (long)oi);
+                r.x0 = x0, r.x1 = x1, r.ty1 = ty, r.owners = ow;
+                r.seg.push_back((int)gi);
+            }
+            if (pick < 0) {
+                Run r;
+                r.x0 = g.x0, r.x1 = g.x1, r.ty0 = r.ty1 = ty;
+                r.seg.push_back((int)gi);
+                r.owners = run_owners(g.x0, g.x1, ty, ty);
+                if (g.x1 - g.x0 > mcs::kSwValid || __builtin_popcount(r.owners) > mcs::kSwMaxOwners)
+                    return MCS_OK;   // (a segment the window cannot hold: band pass + blend)
+                runs.push_back(std::move(r));
+                pick = (int)runs.size() - 1;
+            }
+            next.push_back(pick);
+        }
+        open = next;
+    }
+    if (runs.empty()) return MCS_OK;
+    // 3. strips
+    const int w1 = (W + 1) / 2, h1 = (H + 1) / 2, w2 = (w1 + 1) / 2;
+    (void)h1;
+    auto rf = [](int i, int n_) {
+        i = i < 0 ? -i : i;
+        return i >= n_ ? 2 * n_ - 2 - i : i;
+    };
+    auto taps = [&](int x, int n_, int *idx) {   // expand taps (reflected), count
+        if ((x & 1) == 0) {
+            idx[0] = rf((x >> 1) - 1, n_), idx[1] = rf(x >> 1, n_), idx[2] = rf((x >> 1) + 1, n_);
+            return 3;
+        }
+        idx[0] = rf((x - 1) >> 1, n_), idx[1] = rf((x + 1) >> 1, n_);
+        return 2;
+    };
+    std::vector<mcs::MbStrip> strips;
+    std::vector<int> region;
+    std::vector<uint8_t> skip((size_t)W * H, 0);
+    int64_t desc_rows = 0, sw_px = 0;
+    int max_ns = 0;
+    for (const Run &r : runs) {
+        mcs::MbStrip st;
+        memset(&st, 0, sizeof(st));
+        const int width = r.x1 - r.x0;
+        st.c0 = r.x0 - mcs::kSwMargin - (((mcs::kSwValid - width) / 2) & ~3);
+        st.ya = r.ty0 * TH;
+        st.yb = std::min(r.ty1 * TH + TH, H);
+        st.r0 = st.ya - mcs::kSwLead;
+        // R0 of output row y runs in step s = (y - ya + 34) / 4 (mcs_sweep.hip phase A)
+        const int last = (st.yb - 1 - st.ya + 34) / 4;
+        st.nsteps = (last + 1 + 2) / 3 * 3;
+        st.ns = 0;
+        for (uint32_t m = r.owners; m; m &= m - 1) st.slot[st.ns++] = __builtin_ctz(m);
+        if (st.ns == 0) continue;
+        max_ns = std::max(max_ns, st.ns);
+        st.reg = (int)region.size();
+        st.dsc = (int)desc_rows;
+        desc_rows += (int64_t)st.ns * (4 * st.nsteps + mcs::kSwDescPad);
+        int e1lo = 1 << 30, e1hi = -1;
+        for (int y = st.ya; y < st.yb; y++) {
+            const Seg &g = segs[(size_t)(y / TH)][(size_t)r.seg[(size_t)(y / TH - r.ty0)]];
+            const int lo = g.lo[(size_t)(y % TH)], hi = g.hi[(size_t)(y % TH)];
+            int xa = 0, xb = 0;
+            if (lo <= hi) {
+                xa = lo & ~3;
+                xb = std::min((hi + 4) & ~3, W);
+            }
+            region.push_back(xa | (xb << 16));
+            for (int x = xa; x < xb; x++) {
+                if (dense[(size_t)(y / TH) * gxb + x / TW]) return MCS_OK;
+                skip[(size_t)y * W + x] = 1;
+                int ix[3];
+                const int nt = taps(x, w1, ix);
+                for (int q = 0; q < nt; q++) e1lo = std::min(e1lo, ix[q]), e1hi = std::max(e1hi, ix[q]);
+            }
+            sw_px += xb - xa;
+        }
+        if (e1hi < 0) continue;
+        int z2lo = 1 << 30, z2hi = -1;
+        for (int E = e1lo; E <= e1hi; E++) {
+            int iz[3];
+            const int nt = taps(E, w2, iz);
+            for (int q = 0; q < nt; q++) z2lo = std::min(z2lo, iz[q]), z2hi = std::max(z2hi, iz[q]);
+        }
+        st.e1lo = e1lo, st.e1n = e1hi - e1lo + 1, st.z2lo = z2lo, st.z2n = z2hi - z2lo + 1;
+        // the window computes level-1 columns c0/2 + [1, 62] and level-2 columns c0/4 + [2, 30]
+        bool ok = st.e1n <= mcs::kSwMaxR1 && st.z2n <= mcs::kSwMaxB2;
+        const int c1 = st.c0 >> 1, c2 = st.c0 >> 2;
+        for (int E = e1lo; E <= e1hi && ok; E++) ok = E - c1 >= 1 && E - c1 <= 62;
+        for (int Z = z2lo; Z <= z2hi && ok; Z++) {
+            ok = Z - c2 >= 2 && Z - c2 <= 30;
+            for (int v = 0; v < 5 && ok; v++) {
+                const int q = rf(2 * Z - 2 + v, w1) - c1;
+                ok = q >= 1 && q <= 62;
+            }
+        }
+        if (!ok) return MCS_OK;
+        strips.push_back(st);
+    }
+    if (strips.empty()) return MCS_OK;
+    // 4. device tables, descriptors
+    const size_t ns_ = strips.size();
+    HIP_TRY(A->hipMalloc((void **)&p->d_strips, ns_ * sizeof(mcs::MbStrip)));
+    HIP_TRY(A->hipMalloc((void **)&p->d_region, region.size() * sizeof(int)));
+    HIP_TRY(A->hipMalloc((void **)&p->d_sdesc, (size_t)desc_rows * mcs::kSwCols * 8));
+    HIP_TRY(A->hipMalloc((void **)&p->d_skip, skip.size()));
+    HIP_TRY(A->hipMemcpyAsync(p->d_strips, strips.data(), ns_ * sizeof(mcs::MbStrip),
+                              hipMemcpyHostToDevice, s));
+    HIP_TRY(A->hipMemcpyAsync(p->d_region, region.data(), region.size() * sizeof(int),
+                              hipMemcpyHostToDevice, s));
+    HIP_TRY(A->hipMemcpyAsync(p->d_skip, skip.data(), skip.size(), hipMemcpyHostToDevice, s));
+    mcs::KMbSweepArgs a;
+    memset(&a, 0, sizeof(a));
+    a.P = p->kp;
+    a.strips = p->d_strips;
+    a.sdesc = p->d_sdesc;
+    a.region = p->d_region;
+    a.owner = p->d_owner;
+    a.n_strips = (int)ns_;
+    int rc = launch_args(A, k->mb_sweep_desc[C][p->fd.interp], (unsigned)ns_, mcs::kSwMaxOwners, 256,
+                         1, &a, sizeof(a), s);
+    if (rc) return rc;
+    HIP_TRY(A->hipStreamSynchronize(s));
+    p->kp.skip = p->d_skip;
+    p->n_strips = (int)ns_;
+    // (the band pass + blend's level scratch and per-tile sample windows are not used)
+    for (void **q : {(void **)&p->d_mbg1, (void **)&p->d_mbg2, (void **)&p->d_mbdesc}) {
+        if (*q) (void)A->hipFree(*q);
+        *q = nullptr;
+    }
+    p->sw_jb = max_ns <= 2 ? 2 : 4;
+    p->sw_px = sw_px;
+    p->sw_desc_rows = desc_rows;
+    return MCS_OK;
+}
+
 // Multi-band: per (tile, owner) level-0 sample windows and per-tile masks (once), and the level
 // scratch for chunks of mb_chunk captures (budget kMbScratchBytes).
 int prepare_multiband(const Api *A, mcs_plan *p, const Kernels *k, hipStream_t s)
@@ -680,9 +972,11 @@ int prepare_multiband(const Api *A, mcs_plan *p, const Kernels *k, hipStream_t s
     p->mb_chunk = chunk;
     mcs::KMbArgs a;
     mb_args(p, p->kp, a);
-    const int rc = launch_args(A, k->mb_prep[C][p->fd.interp], (unsigned)n, 1,
-                               mcs::kMbPrepThreads, 1, &a, sizeof(a), s);
+    int rc = launch_args(A, k->mb_prep[C][p->fd.interp], (unsigned)n, 1,
+                         mcs::kMbPrepThreads, 1, &a, sizeof(a), s);
     if (rc) return rc;
+    rc = prepare_sweep(A, p, k, s);
+    if (rc || p->n_strips > 0) return rc;
     return prepare_bands(A, p, k, s);
 }
 
@@ -752,8 +1046,16 @@ void release_tables(const Api *A, mcs_plan *p)
                     (void *)p->d_mbdesc, (void *)p->d_mbtab, (void *)p->d_mbfoot, (void *)p->d_mbg1,
                     (void *)p->d_mbg2, (void *)p->d_bands, (void *)p->d_tile_bt,
                     (void *)p->d_bdesc, (void *)p->d_bgrp, (void *)p->d_bdesc16,
-                    (void *)p->d_order})
+                    (void *)p->d_order, (void *)p->d_strips, (void *)p->d_region,
+                    (void *)p->d_sdesc, (void *)p->d_skip})
         if (q) (void)A->hipFree(q);
+    p->d_strips = nullptr;
+    p->d_region = nullptr;
+    p->d_sdesc = nullptr;
+    p->d_skip = nullptr;
+    p->kp.skip = nullptr;
+    p->n_strips = p->sw_jb = 0;
+    p->sw_px = p->sw_desc_rows = 0;
     p->d_bgrp = nullptr;
     p->d_bdesc16 = nullptr;
     p->n_bands_lds = 0;
@@ -1013,11 +1315,13 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
         return rc;
     }
 #endif
-    const bool mb = p->blend == MCS_BLEND_MULTIBAND && p->n_blend > 0;
+    // multi-band: the sweep (strips) or the band pass + blend
+    const bool sweep = p->blend == MCS_BLEND_MULTIBAND && p->n_strips > 0;
+    const bool mb = !sweep && p->blend == MCS_BLEND_MULTIBAND && p->n_blend > 0;
     // side work beside the main streaming launch: the large-footprint tiles and the
     // direct-gather tiles (tiles the main launch skips), on p->side
     const bool aside = p->n_fallback > 0 || p->n_big > 0;
-    const bool fork = aside || mb;
+    const bool fork = aside || mb || sweep;
     mcs::KMbArgs m;
     if (mb) mb_args(p, P, m);
     mcs::KStreamArgs args;
@@ -1069,6 +1373,27 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
     // blend on side2 (after the band pass, those tiles and the side tiles) beside the remaining
     // streaming tiles (same-box A/B, round 2: C2 1.009 -> 0.985 ms)
     const bool split = mb && p->d_order && p->n_early > 0 && n_frames <= p->mb_chunk;
+    if (sweep) {
+        // the sweep writes only its regions' pixels, the streaming tiles every other pixel: the
+        // two run side by side from the start, no ordering between them
+        HIP_TRY(A->hipStreamWaitEvent(p->side2, p->ev_fork, 0));
+        mcs::KMbSweepArgs a;
+        a.P = P;
+        a.strips = p->d_strips;
+        a.sdesc = p->d_sdesc;
+        a.region = p->d_region;
+        a.owner = p->d_owner;
+        a.n_strips = p->n_strips;
+        a.f0 = 0;
+        a.nf = n_frames;
+        a.pad_ = 0;
+        const int al = band_form(p, P);
+        int rc = launch_args(A, k->mb_sweep[p->fd.channels][al][p->sw_jb == 4 ? 1 : 0],
+                             xcd_grid((int64_t)p->n_strips * n_frames), 1,
+                             (unsigned)(mcs::kSwCols * p->sw_jb), 1, &a, sizeof(a), p->side2);
+        if (rc) return rc;
+        HIP_TRY(A->hipEventRecord(p->ev_join2, p->side2));
+    }
     if (mb) {
         HIP_TRY(A->hipStreamWaitEvent(p->side2, p->ev_fork, 0));
         int rc = launch_mb_levels(A, p, k, m, 0, std::min(p->mb_chunk, n_frames), p->side2);
@@ -1113,8 +1438,8 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
         if (rc) return rc;
     }
     if (aside) HIP_TRY(A->hipStreamWaitEvent(s, p->ev_join, 0));
-    if (mb) HIP_TRY(A->hipStreamWaitEvent(s, p->ev_join2, 0));
-    if (p->n_blend > 0) {
+    if (mb || sweep) HIP_TRY(A->hipStreamWaitEvent(s, p->ev_join2, 0));
+    if (p->n_blend > 0 && !sweep) {
         // recompute the blended tiles over the owner-sampled mosaic (same stream: ordered)
         int rc = MCS_OK;
         if (p->blend == MCS_BLEND_FEATHER) {
@@ -1217,6 +1542,7 @@ int launch_stitch(const Api *A, mcs_plan *p, const mcs::KParams &kp, int n_frame
     mcs::KParams P = kp;
     P.cyl_tab = p->kp.cyl_tab;   // set by prepare on a cylindrical plan's first use
     P.map_tab = p->kp.map_tab;   // (table plans)
+    P.skip = p->kp.skip;         // (multi-band sweep plans: set by prepare)
     if (uniform) return launch_pair(A, p, k, P, n_frames, s);
     for (int f = 0; f < n_frames; f++) {
         for (int i = 0; i < p->fd.n_cams; i++)
@@ -1917,13 +2243,14 @@ int mcs_plan_stats(const mcs_plan *p, int64_t *stats, int n)
 {
     if (!p || !stats) return mcs::fail(MCS_E_INVALID, "NULL plan/stats");
     const int64_t tiles = (int64_t)p->gx * p->gy;
-    const int64_t v[16] = {p->prepared ? 1 : 0, tiles, tiles - p->n_fallback, p->n_fallback,
+    const int64_t v[20] = {p->prepared ? 1 : 0, tiles, tiles - p->n_fallback, p->n_fallback,
                            tiles * (int64_t)(sizeof(mcs::TileHdr) +
                                              mcs::kTilePx * (mcs::kDescWords + 1) * 4),
                            p->blend, p->n_blend, p->mb_slots, p->n_degraded, p->n_bands,
                            p->n_bands_lds, p->n_big, p->mb_mixed_px, p->mb_r1,
-                           p->dma_bytes, p->box_bytes};
-    for (int i = 0; i < n; i++) stats[i] = i < 16 ? v[i] : 0;
+                           p->dma_bytes, p->box_bytes, p->n_strips, p->sw_px,
+                           (int64_t)mcs::kSwCols * p->sw_jb, p->sw_desc_rows};
+    for (int i = 0; i < n; i++) stats[i] = i < 20 ? v[i] : 0;
     return MCS_OK;
 }
 

@@ -33,7 +33,7 @@ int seam_graphcut(int n_cams, int gw, int gh, uint8_t *lab, const uint16_t *cov,
                   const uint8_t *smp, int cn);
 
 // Embedded gfx950 code objects (one per device source, see build.py) and their kernels.
-enum Module { kModStitch = 0, kModFeatures = 1, kNumModules = 2 };
+enum Module { kModStitch = 0, kModFeatures = 1, kModSweep = 2, kNumModules = 3 };
 constexpr int kMaxDevices = 64;
 // Loads module `m` on `device` once (the device must be current) and looks up `name`.
 int module_function(const rt::Api *A, int device, Module m, const char *name, hipFunction_t *out);

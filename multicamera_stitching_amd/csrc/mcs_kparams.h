@@ -42,6 +42,9 @@ struct KParams {
     int seam_w, seam_shift;
     // kStageTable plans: map value (bilinear fixed point) of every output pixel, x then y
     const int32_t *map_tab;
+    // Multi-band sweep plans (mcs_sweep.hip): 1 for every mosaic pixel the sweep kernel writes --
+    // the streaming / direct kernels skip those pixels (no footprint, no store); NULL = none
+    const uint8_t *skip;
     const uint8_t *cams[MCS_MAX_CAMS];
     int64_t cam_fstride[MCS_MAX_CAMS];
     uint8_t *out;
@@ -93,6 +96,8 @@ constexpr uint32_t kCwLastRow1 = 1u << 28;   // row 1 is the frame's last row (+
 constexpr uint32_t kCwZero = 1u << 29;       // no live tap (no camera): output 0
 constexpr uint32_t kCwFull = 1u << 30;       // read the full form
 constexpr uint32_t kCwOneRow = 1u << 31;     // fy = 0: row 1 unused (= row 0)
+constexpr uint32_t kCwSkip = 0xffffffffu;    // (all four words) the lane's pixels belong to the
+                                             // multi-band sweep: no footprint, no store
 struct TileHdr {
     int fits;                      // 1: LDS path, 2: the large-footprint LDS path (mcs_stream_big),
                                    // 0: listed for the direct-gather launch
@@ -335,6 +340,43 @@ struct KBlendArgs {
     const uint8_t *owner;
     const int *list;
     int n_frames, pad_;
+};
+
+// Multi-band sweep (mcs_sweep.hip): the band pass and the blend fused into one kernel.  A strip
+// is a 128-column window of the mosaic over a run of blend-tile rows around one seam region; one
+// workgroup per (strip, capture) walks it top to bottom, 4 level-0 rows per step: the owners'
+// replicate-border samples -> level-1 / level-2 rows (5-tap reduces: vertical in registers,
+// horizontal through LDS) -> B2 / R1 / R0 of the blend from LDS rings, and writes every pixel of
+// its output region (mixed pixels blended, the others their owner sample; the streaming kernel
+// skips them).  No level scratch in HBM, no second launch.
+constexpr int kSwCols = 128;         // level-0 columns of a strip window (2 waves per owner)
+constexpr int kSwMaxOwners = 4;      // owners per strip (workgroup of 128 x 2 or 128 x 4 threads)
+constexpr int kSwMargin = 16;        // output columns [c0 + 16, c0 + 116) of a window (interior)
+constexpr int kSwValid = 100;
+constexpr int kSwLead = 16;          // first level-0 row sampled: ya - 16
+constexpr int kSwDescPad = 12;       // descriptor rows past the last step (12-row prefetch)
+// LDS rings (rows): level-0 owner samples, level 1, level 2, B2, R1
+constexpr int kSwNG0 = 24, kSwNG1 = 10, kSwNG2 = 4, kSwNB2 = 4, kSwNR1 = 4;
+constexpr int kSwMaxR1 = 64, kSwMaxB2 = 32;   // R1 / B2 columns of a strip
+struct MbStrip {
+    int c0;                  // first level-0 column of the window (multiple of 4)
+    int r0;                  // first level-0 row sampled (ya - kSwLead)
+    int nsteps;              // steps of 4 rows (a multiple of 3)
+    int ya, yb;              // output rows [ya, yb)
+    int ns;                  // owners (<= kSwMaxOwners)
+    int reg;                 // region table entry of row ya (one per output row: xa | xb << 16)
+    int dsc;                 // descriptor block: rows of kSwCols u64 from sdesc
+    int e1lo, e1n, z2lo, z2n;   // R1 / B2 columns (mosaic level-1 / level-2 coordinates)
+    int slot[kSwMaxOwners];  // plan slots of the owners
+};
+static_assert(sizeof(MbStrip) == 64, "MbStrip layout");
+struct KMbSweepArgs {
+    KParams P;
+    const MbStrip *strips;
+    uint64_t *sdesc;         // per strip [ns][4 nsteps + kSwDescPad][kSwCols] window descriptors
+    const int *region;
+    const uint8_t *owner;    // owner map (descriptor kernel)
+    int n_strips, f0, nf, pad_;
 };
 
 constexpr int kDirectFrames = 4;    // captures per direct-gather block

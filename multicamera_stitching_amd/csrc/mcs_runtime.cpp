@@ -6,6 +6,7 @@
 
 extern "C" const unsigned char mcs_hsaco_stitch_start[];
 extern "C" const unsigned char mcs_hsaco_features_start[];
+extern "C" const unsigned char mcs_hsaco_sweep_start[];
 
 namespace mcs {
 
@@ -15,7 +16,8 @@ std::mutex g_mod_mu;
 
 const unsigned char *blob(Module m)
 {
-    return m == kModStitch ? mcs_hsaco_stitch_start : mcs_hsaco_features_start;
+    return m == kModStitch ? mcs_hsaco_stitch_start
+                           : (m == kModSweep ? mcs_hsaco_sweep_start : mcs_hsaco_features_start);
 }
 }  // namespace
 

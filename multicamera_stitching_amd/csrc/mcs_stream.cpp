@@ -108,11 +108,14 @@ private:
         for (size_t r = 0; r < c.rows; r++)
             memcpy(c.dst + r * c.row, c.src + r * c.src_pitch, c.row);
     }
+public:
     static int workers()
     {
         // the CPUs this process may run on: the affinity set, bounded by the cgroup's CPU quota
-        // (the GPU box reports an affinity of every CPU of the machine but a quota of 16), capped
-        // at 7 helpers -- a handful of memcpy threads saturate the host memory the link reads
+        // (the GPU box reports an affinity of every CPU of the machine but a quota of 16), shared
+        // by the ranks of this node (LOCAL_WORLD_SIZE, set by torch.distributed.run: one process
+        // per GPU, every rank with its own pool), capped at 7 helpers -- a handful of memcpy
+        // threads saturate the host memory the link reads
         cpu_set_t set;
         int cpus = sched_getaffinity(0, sizeof(set), &set) == 0 ? CPU_COUNT(&set) : 1;
         if (FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
@@ -124,8 +127,14 @@ private:
             }
             fclose(f);
         }
+        if (const char *e = getenv("LOCAL_WORLD_SIZE")) {
+            const int ranks = atoi(e);
+            if (ranks > 1) cpus = std::max(1, cpus / ranks);
+        }
         return std::max(0, std::min(7, cpus / 2 - 1));
     }
+
+private:
     // helper threads that could be started (a failed std::thread leaves the pool smaller)
     explicit CopyPool(int n) : n_(0)
     {
@@ -138,9 +147,13 @@ private:
             }
         }
     }
-    bool run(std::function<void()> f) noexcept
+    // (the std::function is built inside the try: a capturing lambda larger than its small
+    // buffer allocates, and a bad_alloc must not escape this noexcept path)
+    template <class F>
+    bool run(F &&fn) noexcept
     {
         try {
+            std::function<void()> f(std::forward<F>(fn));
             {
                 std::lock_guard<std::mutex> lk(mu_);
                 q_.push_back(std::move(f));
@@ -266,6 +279,8 @@ int build(const Api *A, mcs_stream *s)
 }  // namespace
 
 extern "C" {
+
+int mcs_stream_copy_workers(void) { return CopyPool::workers(); }
 
 int mcs_stream_create(mcs_plan *plan, int depth, int use_graphs, mcs_stream **out)
 {

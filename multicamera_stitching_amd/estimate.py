@@ -221,15 +221,19 @@ class CaptureEstimator:
         in submission order (a failed pair keeps the previous capture's estimate).  Returns the
         mosaic's (out_h, out_w); with captures_per_job > 1, out_ptr is a list of that many outputs
         and the result a list of shapes."""
+        # one carry-over state: last_H (collect and collect_stitch both keep it); the C side
+        # reads and updates it through these arrays (a failed pair keeps the previous estimate)
         if not hasattr(self, "_Hio"):
             self._Hio = np.zeros((self.n_cams - 1, 9), np.float64)
             self._okio = np.zeros(self.n_cams - 1, np.int32)
-            for k, H in enumerate(self.last_H):
-                if H is not None:
-                    self._Hio[k] = np.asarray(H, np.float64).reshape(9)
-                    self._okio[k] = 1
+        for k, H in enumerate(self.last_H):
+            if H is not None:
+                self._Hio[k] = np.asarray(H, np.float64).reshape(9)
+            self._okio[k] = 1 if H is not None else 0
         out = self._jobs[slot].wait_stitch(self._Hio, self._okio, out_ptr, out_pitch,
                                            out_capacity, stream, self.super_mode, self.interp)
+        for k in range(self.n_cams - 1):
+            self.last_H[k] = self._Hio[k].reshape(3, 3).copy() if self._okio[k] else None
         if self.batch > 1:
             self.stats = out[-1][1]
             return [shape for shape, _ in out]
@@ -239,10 +243,8 @@ class CaptureEstimator:
 
     def homographies(self):
         """The current pair homographies (after collect_stitch: the ones the last stitch used)."""
-        if hasattr(self, "_Hio"):
-            return [self._Hio[k].reshape(3, 3).copy() if self._okio[k] else None
-                    for k in range(self.n_cams - 1)]
-        return list(self.last_H)
+        return [None if H is None else np.asarray(H, np.float64).reshape(3, 3).copy()
+                for H in self.last_H]
 
     def features(self, frame_ptrs, pool=None):
         """ORB of every camera frame (device pointers, dense h x w x C, producers finished)."""

@@ -20,10 +20,28 @@ def shard_frames(n_frames: int, rank: int, world: int) -> List[int]:
     return list(range(rank, n_frames, world))
 
 
+# A check every rank runs before each collective of these helpers (bench.py guarded(): a rank whose
+# line failed tells the others at their next collective instead of leaving them to time out)
+_GUARD = None
+
+
+def set_collective_guard(fn):
+    """fn() runs before every collective below (None: no check); returns the previous one."""
+    global _GUARD
+    prev, _GUARD = _GUARD, fn
+    return prev
+
+
+def _guard():
+    if _GUARD is not None:
+        _GUARD()
+
+
 def max_over_ranks(values: Sequence[float], device=None) -> List[float]:
     """Element-wise max over all ranks (the slowest rank defines the job's time)."""
     import torch
     import torch.distributed as dist
+    _guard()
     t = torch.tensor(list(values), dtype=torch.float64, device=device)
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -42,6 +60,7 @@ def gather_mosaics(local, dst: int = 0, bufs=None):
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return [local]
+    _guard()
     world, rank = dist.get_world_size(), dist.get_rank()
     if rank == dst:
         peers = iter(bufs) if bufs is not None else None
@@ -64,6 +83,7 @@ def mcs_group(device: int):
     rank = dist.get_rank() if dist.is_initialized() else 0
     box = [_capi.Group.unique_id() if rank == 0 else None]
     if world > 1:
+        _guard()
         dist.broadcast_object_list(box, src=0)
     return _capi.Group(world, rank, box[0], device)
 
@@ -72,6 +92,7 @@ def gather_mosaics_group(group, local, recv=None, dst: int = 0, stream: int = 0)
     """Every rank's mosaics (contiguous tensor `local`, same size everywhere) to rank `dst`
     through mcs_group_gather: recv (on dst) = a (world, *local.shape) tensor, rank r's at
     recv[r].  Enqueued on `stream`."""
+    _guard()
     group.gather(local.data_ptr(), local.numel() * local.element_size(),
                  recv.data_ptr() if recv is not None else 0, dst, stream)
     return recv
@@ -88,6 +109,7 @@ def timed_loop(step, steps: int, warmup: int, sync, record=None) -> float:
         step()
     sync()
     if multi:
+        _guard()
         dist.barrier()
     sync()
     t0 = time.perf_counter()

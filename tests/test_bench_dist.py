@@ -67,3 +67,34 @@ def test_bench_refuses_world_mismatch():
     r = _run(["--gpus", "1", "--stub", "--steps", "1"], env={"WORLD_SIZE": "2"})
     assert r.returncode != 0
     assert "WORLD_SIZE=2" in (r.stderr + r.stdout)
+
+
+def test_bench_gpus4_rank_failure_reported_not_hung():
+    """A companion line that fails on rank 1 (after its timed region, before its parity and
+    gather collectives): the other ranks stop at their next collective point instead of waiting
+    out the 300 s collective timeout, rank 0's JSON line carries rank 1's message in that line,
+    and the headline line and the other companion line stand (bench.py guarded)."""
+    r = _run(["--gpus", "4", "--stub", "--steps", "2", "--warmup", "1"],
+             env={"MCS_BENCH_INJECT_FAIL": "1:c4"})
+    assert r.returncode == 0, r.stderr[-2000:]
+    res = _line(r.stdout)
+    assert res["n_gpus"] == 4 and res["max_abs_diff"] == 0
+    c4 = res["also"]["c4_cylinder_multiband"]
+    assert c4["error"].startswith("rank 1: RuntimeError: injected failure on rank 1"), c4
+    assert set(c4["rank_errors"]) == {"0", "1", "2", "3"} or set(c4["rank_errors"]) == {0, 1, 2, 3}
+    c5 = res["also"]["c5_stream_4k"]
+    assert "error" not in c5 and c5["n_gpus"] == 4 and c5["gather"]["verified"]
+
+
+def test_bench_gpus4_copy_pool_shared_by_ranks():
+    """The C5 line's host copy pool is sized per rank: the node's CPU quota divided among the
+    LOCAL_WORLD_SIZE ranks (mcs_stream_copy_workers), so N ranks never start more copy threads
+    than the node's CPUs (verdict round 5: 7 per rank x 8 ranks on a 16-CPU quota)."""
+    r = _run(["--gpus", "4", "--stub", "--steps", "2", "--warmup", "1"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    host = _line(r.stdout)["also"]["c5_stream_4k"]["host"]
+    assert host["local_world_size"] == 4
+    usable = host["host_cpus"]["usable"]
+    for w in host["copy_workers_per_rank"]:
+        assert 0 <= w <= max(0, min(7, (usable // 4) // 2 - 1)), host
+    assert sum(w + 1 for w in host["copy_workers_per_rank"]) <= max(usable, 4), host

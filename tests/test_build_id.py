@@ -56,12 +56,13 @@ def test_code_id_is_path_independent(tmp_path):
 
 
 def test_embedded_id_matches_in_tree_objects():
-    """The id libmcs.so reports is code_id() of the two code objects built beside it."""
+    """The id libmcs.so reports is code_id() of the code objects built beside it."""
     here = os.path.dirname(build.LIB)
-    objs = [os.path.join(here, f"mcs_{n}.{build.ARCH}.hsaco") for n in ("features", "kernels")]
+    objs = [os.path.join(here, f"mcs_{n}.{build.ARCH}.hsaco")
+            for n in ("features", "kernels", "sweep")]
     if not all(os.path.exists(p) for p in objs) or not os.path.exists(build.LIB):
         pytest.skip("library not built")
     with open(build.LIB, "rb") as f:
         lib = f.read()
-    want = build.code_id(objs)   # sorted by name: features, stitch (= mcs_kernels)
+    want = build.code_id(objs)   # sorted by name: features, stitch (= mcs_kernels), sweep
     assert want.encode() in lib, f"libmcs.so does not embed build id {want}"

@@ -5,6 +5,7 @@ integer pyramids and IEEE-double blend reproduce the restatement exactly)."""
 import numpy as np
 import pytest
 
+from conftest import check_mb_path
 from oracle import oracle
 
 pytestmark = pytest.mark.gpu
@@ -41,7 +42,9 @@ def _diff(a, b):
     dict(n=4, w=64, h=48, ch=3, seed=10, overlap=0.8),     # seams 13 px apart: 3-4 owners/tile
     dict(n=3, w=202, h=110, ch=3, seed=13),   # rows of 606 B: the band pass's unaligned windows
 ])
-def test_blend_vs_oracle(mode, case):
+def test_blend_vs_oracle(mode, case, mb_path):
+    if mode == "feather" and mb_path == "bands":
+        pytest.skip("feather has one path")
     case = dict(case)
     interp = case.pop("interp", 1)
     plan, cams = _world_plan(interp=interp, **case)
@@ -51,9 +54,13 @@ def test_blend_vs_oracle(mode, case):
     assert _diff(got.reshape(want.shape), want) == 0
     st = plan.stats()
     assert st["blend"] == MODES[mode] and st["blend_tiles"] > 0
+    if mode == "multiband":
+        # (the sweep: mosaics of >= 128 px a side with <= 3 channels)
+        check_mb_path(st, mb_path, case["ch"] <= 3 and min(plan.out_w, plan.out_h) >= 128 and
+                      st["mb_mixed_px"] > 0)
 
 
-def test_multiband_c2_full_size_batch():
+def test_multiband_c2_full_size_batch(mb_path):
     """Config 2 at full size (4 x 1920x1080, multi-band), a device batch of 3 captures."""
     import torch
     from multicamera_stitching_amd import rig
@@ -71,13 +78,15 @@ def test_multiband_c2_full_size_batch():
     for f in (0, F - 1):
         want = oracle.blend_stitch(plan.describe(), shots[f], MODES["multiband"])
         assert _diff(got[f].reshape(want.shape), want) == 0
-    # both window forms of the band pass ran in this launch: most bands on the LDS ring, the
-    # bands with reflected rows (top / bottom mosaic edge) on dword-aligned global windows
+    # band pass: both window forms ran in this launch -- most bands on the LDS ring, the bands
+    # with reflected rows (top / bottom mosaic edge) on dword-aligned global windows
     st = plan.stats()
-    assert 0 < st["mb_bands_lds"] < st["mb_bands"], st
+    check_mb_path(st, mb_path)
+    if mb_path == "bands":
+        assert 0 < st["mb_bands_lds"] < st["mb_bands"], st
 
 
-def test_multiband_c2_full_launch_every_capture():
+def test_multiband_c2_full_launch_every_capture(mb_path):
     """The bench's own launch (BASELINE configs[1]: bench.py's rig, 64 captures of 4 x 1920x1080,
     256-B mosaic pitch) stitched three times: the three batches equal byte for byte on the device
     (an ordering race between the band pass's LDS-DMA refills and their readers showed as a few
@@ -115,10 +124,11 @@ def test_multiband_c2_full_launch_every_capture():
         if d:
             bad.append((f, d))
     assert not bad, bad
+    check_mb_path(plan.stats(), mb_path)
 
 
 @pytest.mark.parametrize("shift, pad", [(1, 0), (3, 2)])
-def test_multiband_c2_unaligned_frames(shift, pad):
+def test_multiband_c2_unaligned_frames(shift, pad, mb_path):
     """Config 2 at full size with camera frames that start off a 4-byte boundary (shift) and,
     for pad > 0, a frame stride that is not a multiple of 4: the launch takes the band pass's
     unaligned window form, whose descriptors must stay the frame-offset ones even though the
@@ -145,15 +155,18 @@ def test_multiband_c2_unaligned_frames(shift, pad):
     for f in range(F):
         want = oracle.blend_stitch(plan.describe(), shots[f], MODES["multiband"])
         assert _diff(got[f].reshape(want.shape), want) == 0, f
-    # the aligned launch of the same plan afterwards still uses the ring (descriptors intact)
+    # the aligned launch of the same plan afterwards (band pass: still on the ring, its
+    # descriptors intact)
     st = plan.stats()
-    assert 0 < st["mb_bands_lds"] < st["mb_bands"], st
+    check_mb_path(st, mb_path)
+    if mb_path == "bands":
+        assert 0 < st["mb_bands_lds"] < st["mb_bands"], st
     want = oracle.blend_stitch(plan.describe(), cams, MODES["multiband"])
     assert _diff(plan.stitch_host(cams).reshape(want.shape), want) == 0
 
 
 @pytest.mark.parametrize("F", [64, 70])
-def test_multiband_batch_split_and_chunked(F):
+def test_multiband_batch_split_and_chunked(F, mb_path):
     """A multi-band device batch of F captures: F <= 64 takes the split launch (streaming tiles
     under mixed pixels first, the blend beside the rest), F > 64 the chunked launch (levels +
     blend per 64-capture chunk of the scratch after the streaming kernel) -- every capture equal
@@ -191,7 +204,7 @@ def test_blend_mode_switch_back_to_paste():
     (6, 48, 5, 6),
     (8, 64, 5, 8),      # eight: the widest blend kernel
 ])
-def test_multiband_dense_seams_vs_oracle(n, w, step, owners):
+def test_multiband_dense_seams_vs_oracle(n, w, step, owners, mb_path):
     """Narrow-seam rigs put 5..8 owners into one neighbourhood: the <= 8-owner blend kernel
     (mcs_mb_blend_c*_s8) handles them, bit-exact vs the restatement (feather too)."""
     plan, cams = _world_plan(n, w, 30, 3, seed=11, step=step)
@@ -205,7 +218,7 @@ def test_multiband_dense_seams_vs_oracle(n, w, step, owners):
 
 
 @pytest.mark.parametrize("n, w, step", [(10, 64, 4), (12, 48, 3)])
-def test_multiband_more_than_eight_owners_degrades_to_feather(n, w, step):
+def test_multiband_more_than_eight_owners_degrades_to_feather(n, w, step, mb_path):
     """Ten (twelve) cameras 4 (3) px apart put more than eight owners into 64 x 96
     neighbourhoods: more than the blend kernels hold, so those tiles take the feather rule on the
     GPU (orc_blend.c "dense seams"), the rest stay multi-band -- bit-exact vs the restatement,
@@ -249,7 +262,7 @@ def test_dropin_dense_rig_multiband_does_not_raise(monkeypatch):
     assert any("feather" in m for m in logged), logged
 
 
-def test_plan_destroy_frees_multiband_tables():
+def test_plan_destroy_frees_multiband_tables(mb_path):
     """Creating, preparing and destroying multi-band plans (band pass, launch order, degraded
     list) in a loop leaves the device's free memory where it was (mcs_plan_destroy frees every
     prepared table)."""

@@ -38,7 +38,9 @@ def _diff(a, b):
     dict(n=4, w=128, h=96, f=70.0, ch=2, seed=5),
     dict(n=3, w=96, h=64, f=60.0, ch=3, seed=6),            # gaps between cameras: uncovered
 ])
-def test_cylinder_vs_oracle(mode, case):
+def test_cylinder_vs_oracle(mode, case, mb_path):
+    if mode != "multiband" and mb_path == "bands":
+        pytest.skip("one path")
     case = dict(case)
     interp = case.pop("interp", 1)
     plan, cams, frames, g = _rig(interp=interp, **case)
@@ -48,7 +50,7 @@ def test_cylinder_vs_oracle(mode, case):
     assert _diff(got.reshape(want.shape), want) == 0
 
 
-def test_cylinder_c4_full_size_batch():
+def test_cylinder_c4_full_size_batch(mb_path):
     """C4 at full size (8 x 1920x1080, f = 1100 -> 6912 x 1080 panorama, multi-band), a device
     batch of 2 captures checked against the restatement."""
     import torch

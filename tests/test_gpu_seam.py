@@ -69,7 +69,7 @@ def test_seams_found_once_then_reused_across_captures():
     assert got.shape == want0.shape
 
 
-def test_cylinder_c4_full_size_graphcut():
+def test_cylinder_c4_full_size_graphcut(mb_path):
     """C4 at full size (8 x 1920x1080 -> 6912 x 1080), graph-cut seams on the 1/4 grid,
     multi-band: labels and panorama bit-exact."""
     plan, frames, ref = _cyl(8, 1920, 1080, 1100.0, 3, seed=0, jitter_deg=0.5)

@@ -92,13 +92,14 @@ def test_orb_fallback_is_logged_once(caplog, monkeypatch):
     assert len(hits) == 1 and "not a contrib version" in hits[0].getMessage()
 
 
-@pytest.mark.parametrize("code, raises", [(-2, False), (-3, False), (-5, False), (-1, True),
+@pytest.mark.parametrize("code, raises", [(-2, False), (-3, False), (-5, True), (-1, True),
                                          (-4, True)])
 def test_gpu_failure_fallback_only_for_runtime_errors(monkeypatch, caplog, code, raises):
     """A run-time failure of the GPU path (MCS_E_HIP / MCS_E_NOMEM) is logged and the fallback
-    image returned, as the reference returns images on its expected failures, and so is an input
-    the reference handles but the kernels do not (MCS_E_UNSUPPORTED, advisor finding, round 4);
-    argument and programming errors (MCS_E_INVALID / MCS_E_SHAPE) raise (round 3)."""
+    image returned, as the reference returns images on its expected failures; argument and
+    programming errors (MCS_E_INVALID / MCS_E_SHAPE, round 3) and MCS_E_UNSUPPORTED from the call
+    (API misuse, advisor finding round 5) raise.  The capacity limits are checked before the call
+    (test_capacity_limits_take_the_fallback)."""
     from multicamera_stitching_amd import StitcherClass as sc, _capi
     imgs = images()
     st = Stitcher(imgs)
@@ -115,6 +116,25 @@ def test_gpu_failure_fallback_only_for_runtime_errors(monkeypatch, caplog, code,
         with caplog.at_level(logging.ERROR, logger="multicamera_stitching_amd"):
             out = st.stitch(imgs)
         assert isinstance(out, np.ndarray) and "GPU stitch failed" in caplog.text
+
+
+def test_capacity_limits_take_the_fallback(monkeypatch, caplog):
+    """Inputs the reference handles but the kernels do not -- a channel count outside 1-4 --
+    give the logged fallback image, checked before any libmcs call (advisor finding, round 5)."""
+    from multicamera_stitching_amd import StitcherClass as sc
+    imgs = images()
+    st = Stitcher(imgs)
+    st.calibrate_stitcher(imgs, save=False, homographies=[[[1, 0, 30], [0, 1, 2], [0, 0, 1]],
+                                                          [[1, 0, 40], [0, 1, 0], [0, 0, 1]]])
+    called = []
+    monkeypatch.setattr(sc, "_get_plan", lambda *a, **k: called.append(1))
+    wide = {k: np.concatenate([v, v[:, :, :2]], axis=2) for k, v in imgs.items()}   # 5 channels
+    with caplog.at_level(logging.ERROR, logger="multicamera_stitching_amd"):
+        out = st.stitch(wide)
+    assert isinstance(out, np.ndarray) and not called
+    assert "unsupported (5 channels" in caplog.text
+    assert sc._capacity_exceeded([np.zeros((4, 4, 3), np.uint8)] * 17).startswith("17 cameras")
+    assert sc._capacity_exceeded([np.zeros((4, 4, 3), np.uint8)] * 3) is None
 
 
 def test_failed_homography_resets_stage():
