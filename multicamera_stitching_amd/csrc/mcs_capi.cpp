@@ -1280,6 +1280,20 @@ int launch_mb_blend(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KMbA
 #define MCS_EXP_MB 0
 #endif
 
+// Capture ranges per large-footprint tile (mcs_stream_big).  Same-box C4 A/B over 1 / 2 / 4 / 8
+// parts (profiles/r06_big_parts_ab.txt): the paste launch gains with more parts (0.734 -> 0.720
+// ms at 8), the multi-band launch loses (1.297 -> 1.349 ms: the extra blocks take CUs from the
+// band pass and blend running beside them).  MCS_BIG_PARTS overrides both.
+int big_parts(bool multiband)
+{
+    static const int v = [] {
+        const char *e = getenv("MCS_BIG_PARTS");
+        const int n = e ? atoi(e) : 0;
+        return n >= 1 && n <= 64 ? n : 0;
+    }();
+    return v ? v : multiband ? 1 : 8;
+}
+
 int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams &P, int n_frames,
                 hipStream_t s)
 {
@@ -1295,7 +1309,7 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
         args.desc4 = p->d_desc4;
         args.spans = p->d_spans;
         args.n_frames = n_frames;
-        args.pad_ = 0;
+        args.parts = 1;
         args.pad2_ = 0;
         args.order = p->d_order;
         args.n_order = p->n_list;
@@ -1332,7 +1346,7 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
     args.desc4 = p->d_desc4;
     args.spans = p->d_spans;
     args.n_frames = n_frames;
-    args.pad_ = 0;
+    args.parts = 1;
     args.pad2_ = 0;
     if (fork) HIP_TRY(A->hipEventRecord(p->ev_fork, s));
     if (aside) HIP_TRY(A->hipStreamWaitEvent(p->side, p->ev_fork, 0));
@@ -1340,11 +1354,15 @@ int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams 
         mcs::KStreamArgs bg = args;
         bg.order = p->d_big + 1;
         bg.n_order = p->n_big;
+        // each large-footprint tile as `parts` blocks over capture ranges: one block per CU per
+        // tile otherwise streams the whole batch and sets the launch's tail (C4: 31 tiles)
+        bg.parts = std::max(1, std::min(big_parts(mb || sweep), n_frames));
         size_t sz = sizeof(bg);
         void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, (void *)&bg, HIP_LAUNCH_PARAM_BUFFER_SIZE,
                        &sz, HIP_LAUNCH_PARAM_END};
         HIP_TRY(A->hipModuleLaunchKernel(k->stream_big[p->fd.channels][b32 ? 1 : 0],
-                                         8u * (((unsigned)p->n_big + 7u) / 8u), 1, 1, mcs::kWave,
+                                         8u * (((unsigned)(p->n_big * bg.parts) + 7u) / 8u), 1, 1,
+                                         mcs::kWave,
                                          mcs::kWavesPerBlock, 1, (unsigned)mcs::kBigStreamLds, q,
                                          nullptr, cfg));
         return MCS_OK;

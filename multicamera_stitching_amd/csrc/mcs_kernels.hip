@@ -759,8 +759,8 @@ __device__ __forceinline__ void wait_vmcnt_jump(uint32_t entry)
 template <int CN, bool BUF, int FITS = 1>
 __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *tiles,
                                             const uint32_t *desc, const uint32_t *desc4,
-                                            const uint16_t *spans, int n_frames, const int *order,
-                                            int n_order, uint8_t *smem)
+                                            const uint16_t *spans, int n_frames, int parts,
+                                            const int *order, int n_order, uint8_t *smem)
 {
     // FITS 1: the tiles of the main launch; 2: the large-footprint tiles (kBigJobsPerWave rows per
     // wave, kBigStreamLds bytes of LDS)
@@ -768,13 +768,18 @@ __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *til
     const int lane = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(threadIdx.y);
     const int tid = wave * kWave + lane;
     const int gx = (P.out_w + kTileW - 1) / kTileW;
-    const int per = (n_order + 7) >> 3;
-    const int idx = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
-    if (idx >= n_order) return;
-    // launch-list entry: a tile (-1 = padding); the block streams every capture through it
+    const int per = (n_order * parts + 7) >> 3;
+    const int item = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+    if (item >= n_order * parts) return;
+    // launch-list entry: a tile (-1 = padding); the block streams the captures of its part of
+    // the batch through it (parts > 1: the large-footprint launch, whose few tiles would
+    // otherwise each hold one CU for the whole batch -- the launch's tail)
+    const int idx = item / parts, part = item - idx * parts;
     const int tile = order ? __builtin_amdgcn_readfirstlane(order[idx]) : idx;
     if (tile < 0) return;
-    const int f_beg = 0, f_end = n_frames;
+    const int f_beg = (int)((int64_t)part * n_frames / parts);
+    const int f_end = (int)((int64_t)(part + 1) * n_frames / parts);
+    if (f_beg >= f_end) return;
     const int bx = tile % gx, by = tile / gx;
     // the tile header, copied once into LDS (the kernel also stores to global memory, so the
     // compiler cannot serve `tiles` from the scalar cache)
@@ -1164,21 +1169,21 @@ __device__ __forceinline__ void resize_px(const KResizeArgs &a)
 #define MCS_STREAM_ENTRY(CN, SUF, BUF)                                                         \
     extern "C" __global__ __launch_bounds__(512) MCS_STREAM_ATTR void mcs_stream_c##CN##SUF(   \
         const mcs::KParams P, const mcs::TileHdr *tiles, const uint32_t *desc,                \
-        const uint32_t *desc4, const uint16_t *spans, int n_frames, const int *order,          \
-        int n_order)                                                                           \
+        const uint32_t *desc4, const uint16_t *spans, int n_frames, int parts,                \
+        const int *order, int n_order)                                                         \
     {                                                                                          \
         extern __shared__ __attribute__((aligned(16))) uint8_t smem[];                         \
-        mcs::stream_tile<CN, BUF>(P, tiles, desc, desc4, spans, n_frames, order, n_order,      \
-                                  smem);                                                       \
+        mcs::stream_tile<CN, BUF>(P, tiles, desc, desc4, spans, n_frames, parts, order,        \
+                                  n_order, smem);                                              \
     }                                                                                          \
     extern "C" __global__ __launch_bounds__(512) void mcs_stream_big_c##CN##SUF(               \
         const mcs::KParams P, const mcs::TileHdr *tiles, const uint32_t *desc,                \
-        const uint32_t *desc4, const uint16_t *spans, int n_frames, const int *order,          \
-        int n_order)                                                                           \
+        const uint32_t *desc4, const uint16_t *spans, int n_frames, int parts,                \
+        const int *order, int n_order)                                                         \
     {                                                                                          \
         extern __shared__ __attribute__((aligned(16))) uint8_t smem[];                         \
-        mcs::stream_tile<CN, BUF, 2>(P, tiles, desc, desc4, spans, n_frames, order, n_order,   \
-                                     smem);                                                    \
+        mcs::stream_tile<CN, BUF, 2>(P, tiles, desc, desc4, spans, n_frames, parts, order,     \
+                                     n_order, smem);                                           \
     }
 #define MCS_DIRECT_ENTRY(CN, IN, O32)                                                          \
     extern "C" __global__ __launch_bounds__(512) void mcs_direct_c##CN##_i##IN##_o##O32(       \

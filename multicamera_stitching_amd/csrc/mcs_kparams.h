@@ -136,7 +136,7 @@ struct KStreamArgs {
     const uint32_t *desc4;
     const uint16_t *spans;         // [tiles][kMaxTileJobs] row spans
     int n_frames;
-    int pad_;
+    int parts;                     // launch-list item = (tile, capture range 1 / parts of the batch)
     const int *order;              // tiles to stream (NULL: all, in grid order)
     int n_order;                   // tiles in this launch
     int pad2_;
