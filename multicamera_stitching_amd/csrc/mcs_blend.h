@@ -13,12 +13,6 @@
 //                -> mask-weighted blend per level (double) -> collapse -> bytes.
 // Both are a few percent of the mosaic's tiles for a linear rig.
 #pragma once
-// Band-pass timing decomposition (variant builds only, never the product): bit 0 = no bilinear
-// arithmetic, bit 1 = no horizontal level-1 reduce, bit 2 = no level-2 arithmetic, bit 3 = no
-// level stores, bit 4 = no descriptor refresh (wrong values).
-#ifndef MCS_EXP_BAND_PART
-#define MCS_EXP_BAND_PART 0
-#endif
 
 namespace mcs {
 
@@ -303,18 +297,8 @@ __device__ __forceinline__ void feather_tile(const KBlendArgs &a)
 // Long launches run in chunks of captures so the scratch stays a few tens of MB.
 constexpr int kMbO1 = 6, kMbO2 = 2, kMbOR = 1;       // array origins: O/2 - 6, O/4 - 2, O/2 - 1
 constexpr int kMbU = kMbUsedX * kMbUsedY;             // level-0 samples per owner
-#ifndef MCS_MB_FOOT_BYTES
-#define MCS_MB_FOOT_BYTES 28672
-#endif
-#ifndef MCS_MB_FOOT_BUFS
-#define MCS_MB_FOOT_BUFS 1
-#endif
-#ifndef MCS_MB_STAGE
-#define MCS_MB_STAGE 1      // 0: no LDS footprints (global window loads; a 31 KiB levels block)
-#endif
-constexpr int kMbFoot = MCS_MB_FOOT_BYTES;             // bytes of one LDS footprint buffer
-constexpr int kMbFootBufs = MCS_MB_FOOT_BUFS;          // 2: double buffer, 1: refilled during
-                                                       // the reduces
+constexpr int kMbFoot = 28672;      // bytes of one LDS footprint buffer
+constexpr int kMbFootBufs = 1;      // 2: double buffer, 1: refilled during the reduces
 constexpr int kMbRS = kMbO1 - kMbOR;                  // R1 region origin in the level-1 array (5)
 // Level scratch of one (tile, owner, capture), row-major (a band's lanes, adjacent columns,
 // store contiguous bytes): g1 (R1 region, 8 B entries) at row * kMbNRX + col, g2 with the
@@ -834,7 +818,7 @@ __device__ __forceinline__ void mb_prep(const KMbArgs &a)
         F.stride = (f_bmax[tid] - F.cal + 15) & ~15;
         F.e = 0;
         // (rows above the last one may run into the next row, never past the frame)
-        F.fits = MCS_MB_STAGE && F.rows * F.stride + kLdsSlack <= kMbFoot &&
+        F.fits = F.rows * F.stride + kLdsSlack <= kMbFoot &&
                  F.stride <= 16 * kWave && F.cal + F.stride <= 2 * pitch;
         if (f_rmax[tid] == h - 1 && F.cal + F.stride > pitch) {
             F.e = (int)(F.cal + F.stride - pitch);
@@ -872,7 +856,7 @@ __device__ __forceinline__ void mb_prep(const KMbArgs &a)
 // ---- levels: grid (listed tiles, slots, ceil(nf / kMbLvFrames)), block kMbLvThreads -------------
 template <int CN>
 struct MbLvLds {
-    uint8_t foot[MCS_MB_STAGE ? kMbFootBufs : 0][kMbFoot] __attribute__((aligned(16)));   // source footprints
+    uint8_t foot[kMbFootBufs][kMbFoot] __attribute__((aligned(16)));   // source footprints
     // (one spare entry past each array: the branch-free stores of out-of-range items land there)
     uint32_t g0[kMbU + 1];             // level 0: channel k in byte k
     uint2 g1[kMbN1X * kMbN1Y + 1];     // 256 G1 <= 65280 as u16 lanes: x = (c0, c2), y = (c1, c3)
@@ -1409,7 +1393,6 @@ __device__ __forceinline__ void mb_bands_body(const KMbBandArgs &a, int bi, lds_
     g8 *const g1b = (g8 *)a.g1, *const g2b = (g8 *)a.g2;
     const uint64_t *dsc = a.bdesc + (int64_t)bi * kMbBandDescRows * kMbBandLanes + l;
     const int nst = min(FR, a.nf - fl0);
-    [[maybe_unused]] const uint32_t M = 0x00ff00ffu;   // (timing experiments only)
     // Rolling vertical sums, indexed by row % 3 (compile-time inside the 12-row body): level-1
     // rows (packed u16: lo = channels 0, 2; hi = 1, 3), level-2 rows (one int per channel).  A
     // row's sum starts with '=' at its first input row, so the rows before the array (and the
@@ -1435,10 +1418,6 @@ __device__ __forceinline__ void mb_bands_body(const KMbBandArgs &a, int bi, lds_
         const uint32_t dx = (uint32_t)dv;
         const uint32_t d = AL ? (uint32_t)(dv >> 47) & 15u : (uint32_t)(dv >> 44) & 7u;
         uint32_t o = (dx & 0x7fffffffu) - d, ob = o + ((dx >> 31) ? pitch : 0u);
-#ifdef MCS_MB_BAND_ALIGNED_TEST
-        o &= ~7u;   // (timing experiment only: wrong pixels)
-        ob &= ~7u;
-#endif
 #pragma unroll
         for (int i = 0; i < FR; i++) {
             if constexpr (AL) {
@@ -1468,9 +1447,6 @@ __device__ __forceinline__ void mb_bands_body(const KMbBandArgs &a, int bi, lds_
     const __amdgpu_buffer_rsrc_t rs2 = __builtin_amdgcn_make_buffer_rsrc((void *)a.g2, 0, 0x7fffffff, 0x00020000);
     auto flush_ld = [&](auto PHc) {
         constexpr int ph = decltype(PHc)::value;
-#if MCS_EXP_BAND_PART & 8   // (timing experiment: no level stores)
-        return;
-#endif
         constexpr uint32_t none = 0xfffffff0u;
         if constexpr (ph & 1) {
 #pragma unroll
@@ -1528,16 +1504,12 @@ __device__ __forceinline__ void mb_bands_body(const KMbBandArgs &a, int bi, lds_
     auto level1_done = [&](int i, auto P2c, auto M3c, int f, uint32_t vl, uint32_t vh) {
         constexpr int P2 = decltype(P2c)::value, M3 = decltype(M3c)::value;
         // horizontal: level-1 entry at lane x = 2 qx reads lanes x - 2 .. x + 2
-#if MCS_EXP_BAND_PART & 2   // (timing experiment: no horizontal level-1 reduce -- wrong values)
-        uint32_t gl = vl, gh = vh;
-#else
         const uint32_t l1 = lane_prev(vl), l2 = lane_prev(l1), r1 = lane_next(vl),
                        r2 = lane_next(r1);
         const uint32_t h1_ = lane_prev(vh), h2_ = lane_prev(h1_), s1 = lane_next(vh),
                        s2 = lane_next(s1);
         uint32_t gl = mad6_u32(vl, (l2 + r2) + 4u * (l1 + r1));
         uint32_t gh = mad6_u32(vh, (h2_ + s2) + 4u * (h1_ + s1));
-#endif
         const int qy = Y1 + i;
         if constexpr (LD) {
             pend1 = i;
@@ -1565,24 +1537,8 @@ __device__ __forceinline__ void mb_bands_body(const KMbBandArgs &a, int bi, lds_
 #pragma unroll
         for (int k = 0; k < CN; k++)
             g[k] = (int)((((k & 1) ? gh : gl) >> ((k & 2) ? 16 : 0)) & 0xffffu);
-#if MCS_EXP_BAND_PART & 4   // (timing experiment: no level-2 arithmetic, zero entries stored)
-        if (P2 == 0) {
-            const int e = (i >> 1) - 2, zy = Y2 + e;
-            if (LD) {
-                pend2 = e;
-                ok2 = e >= 0 && e < kMbN2Y && zy < h2;
-            }
-            if (LD || (e >= 0 && e < kMbN2Y && zy < h2)) {
-                pend2 = e;
-#pragma unroll
-                for (int k = 0; k < CN; k++) p2[f][k] = g[k];
-            }
-        }
-        if (false) {
-#else
         // vertical: level-2 array row e reads level-1 rows 2e .. 2e + 4
         if (P2 == 0) {
-#endif
 #pragma unroll
             for (int k = 0; k < CN; k++) V2[f][(M3 + 1) % 3][k] += g[k];   // row m - 2 done
             const int e = (i >> 1) - 2, zy = Y2 + e;
@@ -1632,9 +1588,6 @@ __device__ __forceinline__ void mb_bands_body(const KMbBandArgs &a, int bi, lds_
     constexpr int NL = kMbLdsDescRing;
     const uint4 *d16 = a.bdesc16 + (int64_t)bi * kMbLdsDescRows * kMbBandLanes + l;
     auto issue_desc = [&](int row) {   // descriptor row `row` into ring slot row % NL
-#if MCS_EXP_BAND_PART & 16   // (timing experiment: descriptors staged once, never refreshed)
-        if (row >= NL) return;
-#endif
         __builtin_amdgcn_global_load_lds(d16 + row * kMbBandLanes,
                                          dring + (row % NL) * kMbBandLanes * 16, 16, 0, 0);
         asm volatile("" ::: "memory");
@@ -1712,10 +1665,6 @@ __device__ __forceinline__ void mb_bands_body(const KMbBandArgs &a, int bi, lds_
                     r0 = wq0[b0][f];
                     r1 = wq1[b0][f];
                 }
-#if MCS_EXP_BAND_PART & 1   // (timing experiment: no bilinear arithmetic -- wrong values)
-                pls[f] = (r0.x ^ r1.y) & M;
-                phs[f] = (r0.y ^ r1.x) & M;
-#else
                 uint32_t t[4];
 #pragma unroll
                 for (int c = 0; c < 4; c++) t[c] = c < CN ? mb_tap2<CN>(r0, r1, wa, wb, c, dd) : 0u;
@@ -1724,7 +1673,6 @@ __device__ __forceinline__ void mb_bands_body(const KMbBandArgs &a, int bi, lds_
                 if constexpr (CN >= 4) phs[f] = __builtin_amdgcn_perm(t[3], t[1], 0x0c060c02u);
                 else if constexpr (CN == 2 || CN == 3) phs[f] = (t[1] >> 16) & 0xffu;
                 else phs[f] = 0u;
-#endif
             }
             // the previous row's finished entries (after this row's window wait), then the loads:
             // windows of row r + A (its descriptor arrived a row ago), descriptor of row r + A + 1
@@ -1782,9 +1730,6 @@ __device__ __forceinline__ void mb_bands(const KMbBandArgs &a, int bi, lds_u8 *r
 {
     if constexpr (AL) {
         const int lds = __builtin_amdgcn_readfirstlane(a.bands[bi].pad_) & 1;
-#ifdef MCS_EXP_BAND_SKIP   // (timing experiments only: 1 = skip the global-window bands, 2 = the LDS ones)
-        if (MCS_EXP_BAND_SKIP == (lds ? 2 : 1)) return;
-#endif
         if (lds) mb_bands_body<CN, FR, BR, 2>(a, bi, ring, pr);
         else mb_bands_body<CN, FR, BR, 1>(a, bi, ring, pr);
     } else {
@@ -1826,9 +1771,6 @@ __device__ __forceinline__ void mb_blend_tile(const KMbArgs &a, const MbGeo &G, 
     auto ir = [&](int cx, int cy) {   // the R1 region (g1, m1, d1, r1)
         return (int)__umul24((unsigned)ix2<IN>(cy, G.YR, kMbNRY), kMbNRX) + ix2<IN>(cx, G.XR, kMbNRX);
     };
-#if defined(MCS_MB_BL_SKIP) && MCS_MB_BL_SKIP >= 3
-    return;
-#endif
     const int n_r1 = t_d2[kMbN2X * kMbN2Y + 1];
     const uint16_t *t_r1 =
         reinterpret_cast<const uint16_t *>(t_d2 + kMbN2X * kMbN2Y + kMbTabCounts) + kMbTilePx;
@@ -1849,9 +1791,6 @@ __device__ __forceinline__ void mb_blend_tile(const KMbArgs &a, const MbGeo &G, 
             L.b2[k][e] = den ? num[k] / ((double)den * 65536.0) : 0.0;
     }
     __syncthreads();
-#if defined(MCS_MB_BL_SKIP) && MCS_MB_BL_SKIP >= 2
-    return;
-#endif
     // R1 = B1 + up(B2), B1 = sum m1 (16384 g1 - E(g2)) / (sum m1 * 4194304)
     // (the list is grouped by parity class, mb_prep: the zero-weight third taps of odd
     // coordinates are skipped by whole waves)
@@ -1910,9 +1849,6 @@ __device__ __forceinline__ void mb_blend_tile(const KMbArgs &a, const MbGeo &G, 
         }
     }
     __syncthreads();
-#if defined(MCS_MB_BL_SKIP) && MCS_MB_BL_SKIP >= 1
-    return;
-#endif
     // R0 = L0_owner / 16384 + up(R1) over the tile's own pixels; L0 = 16384 g0 - E(g1), g0 = the
     // owner sample already in the mosaic
 #pragma unroll

@@ -571,13 +571,7 @@ int band_lds_tables(const Api *A, mcs_plan *p, std::vector<mcs::MbBand> &bands, 
         const int w = slot == 0 ? p->kp.cam0_w : p->kp.st[slot - 1].src_w;
         const int h = slot == 0 ? p->kp.cam0_h : p->kp.st[slot - 1].src_h;
         const int64_t pitch = (int64_t)w * C, fb = pitch * h;
-#ifdef MCS_BAND_DIAG   // (variant builds only: why bands keep the global form)
-        static int why[6];
-        auto diag = [&](int k) { why[k]++; fprintf(stderr, "band_lds %zu/%zu: pitch %d invalid %d rows %d span %d sched %d lds %d\n", i, nb, why[0], why[1], why[2], why[3], why[4], why[5]); };
-#else
-        auto diag = [](int) {};
-#endif
-        if (pitch % 4 || pitch < SP) { diag(0); continue; }
+        if (pitch % 4 || pitch < SP) continue;
         uint64_t *d = desc.data() + i * DR * L;
         int y0 = INT32_MAX, y1 = -1;
         bool ok = true;
@@ -589,7 +583,7 @@ int band_lds_tables(const Api *A, mcs_plan *p, std::vector<mcs::MbBand> &bands, 
             y0 = std::min(y0, ya);
             y1 = std::max(y1, yb);
         }
-        if (!ok || y1 - y0 + 1 > 4 * (NG - 2)) { diag(ok ? 2 : 1); continue; }
+        if (!ok || y1 - y0 + 1 > 4 * (NG - 2)) continue;
         const int nr = y1 - y0 + 1;
         std::vector<int64_t> lo(nr, INT64_MAX), hi(nr, -1), bs(nr, 0);
         std::vector<int> glo(R, INT32_MAX), ghi(R, -1);
@@ -612,11 +606,11 @@ int band_lds_tables(const Api *A, mcs_plan *p, std::vector<mcs::MbBand> &bands, 
             bs[y] = std::min(hi[y] < 0 ? 0 : lo[y] & ~(int64_t)15, room);
             ok = bs[y] >= 0 && (hi[y] < 0 || hi[y] - bs[y] <= SP);
         }
-        if (!ok) { diag(3); continue; }
+        if (!ok) continue;
         for (int r = 0; r < R && ok; r++)
             ok = issue(ghi[r]) <= r - mcs::kMbLdsGLead && issue(glo[r] + K / 4) >= r;
-        if (!ok) { diag(4); continue; }
-        diag(5);
+        if (!ok) continue;
+       
         // group table: lane l loads chunk l % 16 of row 4g + l / 16; chunks no sample of the row
         // reads, rows no sample reads and rows past the band: an offset past the frame (the
         // kernel's buffer load fetches nothing for them)
@@ -1210,21 +1204,6 @@ int launch_mb_levels(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KMb
         const int form = band_form(p, b.P);
         const int kind = p->n_bands_in == 0 ? 1 : (p->n_bands > p->n_bands_in ? 2 : 0);
         if (kind == 1) b.band0 = 0;
-#ifdef MCS_MB_BAND_SPLIT   // (variant builds: interior and edge bands as two launches)
-        if (kind == 2) {
-            b.band0 = 0;
-            b.nb = p->n_bands_in;
-            int rc = launch_args(A, k->mb_bands[p->fd.channels][form][0],
-                                 xcd_grid((int64_t)b.nb * gy), 1, mcs::kMbBandLanes, 1, &b,
-                                 sizeof(b), s);
-            if (rc) return rc;
-            b.band0 = p->n_bands_in;
-            b.nb = p->n_bands - p->n_bands_in;
-            return launch_args(A, k->mb_bands[p->fd.channels][form][1],
-                               xcd_grid((int64_t)b.nb * gy), 1, mcs::kMbBandLanes, 1, &b,
-                               sizeof(b), s);
-        }
-#endif
         return launch_args(A, k->mb_bands[p->fd.channels][form][kind],
                            xcd_grid((int64_t)p->n_bands * gy), 1, mcs::kMbBandLanes, 1, &b,
                            sizeof(b), s);
@@ -1272,14 +1251,6 @@ int launch_mb_blend(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KMbA
 // n_frames captures that share one frame stride.  Work that does not read the mosaic -- the
 // direct-gather tiles and the first multi-band chunk's level pyramids -- runs on two side streams,
 // concurrently with the HBM-bound streaming kernel.
-// Timing decomposition of the multi-band launch (variant builds only, tools/build_variant.py;
-// never the product): 1 = band pass and blend serially after the streaming kernel on the
-// caller's stream (standalone kernel times in a trace), 2 = no blend, 3 = no band pass, 4 = neither
-// (2-4 write wrong pixels).
-#ifndef MCS_EXP_MB
-#define MCS_EXP_MB 0
-#endif
-
 // Capture ranges per large-footprint tile (mcs_stream_big).  Same-box C4 A/B over 1 / 2 / 4 / 8
 // parts (profiles/r06_big_parts_ab.txt): the paste launch gains with more parts (0.734 -> 0.720
 // ms at 8), the multi-band launch loses (1.297 -> 1.349 ms: the extra blocks take CUs from the
@@ -1297,38 +1268,6 @@ int big_parts(bool multiband)
 int launch_pair(const Api *A, const mcs_plan *p, const Kernels *k, mcs::KParams &P, int n_frames,
                 hipStream_t s)
 {
-#if MCS_EXP_MB
-    if (p->blend == MCS_BLEND_MULTIBAND && p->n_blend > 0) {
-        mcs::KMbArgs m;
-        mb_args(p, P, m);
-        mcs::KStreamArgs args;
-        args.P = P;
-        const bool b32 = stream_base(p, P, n_frames, &args.P.base);
-        args.tiles = p->d_tiles;
-        args.desc = p->d_desc;
-        args.desc4 = p->d_desc4;
-        args.spans = p->d_spans;
-        args.n_frames = n_frames;
-        args.parts = 1;
-        args.pad2_ = 0;
-        args.order = p->d_order;
-        args.n_order = p->n_list;
-        size_t sz = sizeof(args);
-        void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, (void *)&args, HIP_LAUNCH_PARAM_BUFFER_SIZE,
-                       &sz, HIP_LAUNCH_PARAM_END};
-        HIP_TRY(A->hipModuleLaunchKernel(k->stream[p->fd.channels][b32 ? 1 : 0],
-                                         8u * (((unsigned)p->n_list + 7u) / 8u), 1, 1, mcs::kWave,
-                                         mcs::kWavesPerBlock, 1,
-                                         (unsigned)mcs::lds_stream_bytes(p->fd.channels), s,
-                                         nullptr, cfg));
-        const int nf = std::min(p->mb_chunk, n_frames);
-        int rc = MCS_OK;
-        if (MCS_EXP_MB == 1 || MCS_EXP_MB == 2) rc = launch_mb_levels(A, p, k, m, 0, nf, s);
-        if (rc == MCS_OK && (MCS_EXP_MB == 1 || MCS_EXP_MB == 3))
-            rc = launch_mb_blend(A, p, k, m, 0, nf, s);
-        return rc;
-    }
-#endif
     // multi-band: the sweep (strips) or the band pass + blend
     const bool sweep = p->blend == MCS_BLEND_MULTIBAND && p->n_strips > 0;
     const bool mb = !sweep && p->blend == MCS_BLEND_MULTIBAND && p->n_blend > 0;

@@ -290,12 +290,6 @@ __device__ __forceinline__ void tile_pixel(int bx, int by, int lane, int wave, i
 }
 
 
-// Footprint DMA per row over the span its windows read (1) or the camera box's full width (0:
-// variant builds, the round-4 form, for A/B timing).
-#ifndef MCS_ROW_SPANS
-#define MCS_ROW_SPANS 1
-#endif
-
 struct FootprintLds {
     int rmin[MCS_MAX_CAMS], rmax[MCS_MAX_CAMS], cmin[MCS_MAX_CAMS], cmax[MCS_MAX_CAMS];
 };
@@ -452,12 +446,6 @@ __device__ __forceinline__ void prepare_tile(const KParams &P, TileHdr *tiles, u
         // first chunk | chunk count (>= 1: a row no window reads still issues its one DMA
         // instruction, of one chunk, so every job counts in the streaming kernel's vmcnt waits)
         int lo = span_lo[tid], hi = span_hi[tid];
-#if !MCS_ROW_SPANS
-        // (variant builds: every row fetches its camera's whole box width, the round-4 form)
-        for (int k = 0; k < th.ncam; k++)
-            if (tid >= th.jobstart[k] && tid < th.jobstart[k + 1])
-                lo = 0, hi = 16 * ((th.stride[k] >> 16) & 0xff);
-#endif
         const int c0 = lo <= hi ? lo >> 4 : 0, c1 = lo <= hi ? (hi + 15) >> 4 : 1;
         spans[(int64_t)tile * kMaxTileJobs + tid] = (uint16_t)(c0 | (max(c1 - c0, 1) << 8));
     }
@@ -468,126 +456,23 @@ __device__ __forceinline__ void prepare_tile(const KParams &P, TileHdr *tiles, u
         o[i] = make_uint4(d[4 * i], d[4 * i + 1], d[4 * i + 2], d[4 * i + 3]);
 }
 
-// Cache policy of the footprint DMA (aux bits: 2 = nt; measured 12 % slower: vertically adjacent
-// tiles re-read footprint rows from L2) and of the mosaic stores (nontemporal: the mosaic is
-// written once and never re-read by this launch; same-box A/B paste 0.62 -> 0.60 ms, multi-band
-// 0.978 -> 0.951 ms).
-#ifndef MCS_DMA_AUX
-#define MCS_DMA_AUX 0
-#endif
-#ifndef MCS_STORE_NT
-#define MCS_STORE_NT 1
-#endif
-// Decomposition knobs (variant builds only, never the product): MCS_EXP_NOCOMPUTE stores a
-// constant instead of reading LDS windows (memory-only time), MCS_EXP_NODMA stages only the
-// first ring of captures (compute + stores), MCS_EXP_NOSTORE skips the mosaic stores.
-#ifndef MCS_EXP_NOCOMPUTE
-#define MCS_EXP_NOCOMPUTE 0
-#endif
-#ifndef MCS_EXP_NODMA
-#define MCS_EXP_NODMA 0
-#endif
-#ifndef MCS_EXP_NOSTORE
-#define MCS_EXP_NOSTORE 0
-#endif
-#ifndef MCS_NARROW_GLOBAL
-#define MCS_NARROW_GLOBAL 0
-#endif
-// The streaming loop: 1 = steady-state and tail loops, computed-jump waits, running offsets
-// (round 5); 0 = the round-4 loop (variant builds, A/B only).
-#ifndef MCS_STREAM_LOOP2
-#define MCS_STREAM_LOOP2 1
-#endif
+// Cache policy of the footprint DMA: default (aux 0; nontemporal measured 12 % slower: vertically
+// adjacent tiles re-read footprint rows from L2).  The mosaic stores are nontemporal: the mosaic
+// is written once and never re-read by this launch (same-box A/B paste 0.62 -> 0.60 ms,
+// multi-band 0.978 -> 0.951 ms).
+constexpr int kDmaAux = 0;
 
 
 // Block-uniform value read from LDS (broadcast read + readfirstlane -> SGPR).
 __device__ __forceinline__ int uni(const int &v) { return __builtin_amdgcn_readfirstlane(v); }
 
-// The LDS-DMA jobs of one wave: its footprint rows (j = wave, wave + 8, ...), resolved once per
-// block into scalar registers (compile-time indexed), so a capture costs one 32-bit add and one
-// LDS-DMA instruction per row.  Per row: the byte offset of its first 16-byte chunk in frame 0
-// and one packed word, LDS offset (bits 0-15) | 16-byte chunks (16-23).  Every chunk lies inside
-// its camera frame (TileHdr::last_shift).
+// The LDS-DMA jobs of one wave, resolved once per block.  Every chunk lies inside its camera frame
+// (TileHdr::last_shift).
 //   BUF (every byte of every capture of every used camera within 4 GiB of P.base): offsets from
 //   P.base, read through one buffer resource (buffer_load_dwordx4 ... offen lds), the capture's
 //   offset f * fstride in the instruction's scalar offset -- no per-row 64-bit address math;
 //   otherwise 64-bit frame-0 addresses for global_load_lds_dwordx4.
-template <bool BUF, int NJ>
-struct WaveJobs {
-    typedef typename std::conditional<BUF, uint32_t, const uint8_t *>::type src_t;
-    src_t src[NJ];
-    uint32_t w[NJ];
-    int n;
-};
-
-template <int CN, bool BUF, int NJ>
-__device__ __forceinline__ WaveJobs<BUF, NJ> wave_jobs(const KParams &P, const TileHdr &h, int wave,
-                                                       const uint16_t *spans, int lane)
-{
-    static_assert(NJ * kWavesPerBlock <= kMaxTileJobs, "row spans per tile");
-    WaveJobs<BUF, NJ> J;
-    // the wave's rows' spans: lane jj holds job wave + 8 jj's (read back lane by lane below)
-    const uint32_t sp_v = lane < NJ ? (uint32_t)spans[wave + lane * kWavesPerBlock] : 0u;
-    const int njobs = uni(h.njobs);
-    J.n = 0;
-#pragma unroll
-    for (int jj = 0; jj < NJ; jj++) {
-        const int j = wave + jj * kWavesPerBlock;
-        J.src[jj] = 0;
-        J.w[jj] = 0;
-        if (j < njobs) {
-            int k = 0;
-            while (k < kTileCams - 1 && j >= uni(h.jobstart[k + 1])) k++;
-            const int c = uni(h.cam[k]);
-            const int row = j - uni(h.jobstart[k]);
-            const int stride = uni(h.stride[k]);
-            const int64_t pitch = (int64_t)P.cam_w[c] * CN;
-            const int r = uni(h.rmin[k]) + row;
-            const int e = r == P.cam_h[c] - 1 ? (uni(h.last_shift) >> (8 * k)) & 255 : 0;
-            // only the row's span of the box: chunks [lo, lo + n) of its LDS row
-            const uint32_t sp = (uint32_t)__builtin_amdgcn_readlane((int)sp_v, jj);
-            const int lo16 = 16 * (int)(sp & 0xffu);
-            const uint32_t nch = (sp >> 8) & 0xffu;
-            const int64_t in_frame = (int64_t)r * pitch + uni(h.cal[k]) - e + lo16;
-            if constexpr (BUF)
-                J.src[jj] = (uint32_t)((uint64_t)(uintptr_t)P.cams[c] -
-                                       (uint64_t)(uintptr_t)P.base + (uint64_t)in_frame);
-            else
-                J.src[jj] = P.cams[c] + in_frame;
-            J.w[jj] = (uint32_t)(uni(h.base[k]) + row * (stride & 0xffff) + lo16) | (nch << 16);
-            J.n = jj + 1;
-        }
-    }
-    return J;
-}
-
-// Issues capture f's footprint rows into `slot`: one LDS-DMA wave instruction per row (lane =
-// 16-byte chunk).  foff = f * fstride (fits 32 bits in BUF mode).
-template <bool BUF, int NJ>
-__device__ __forceinline__ void stage_capture(const WaveJobs<BUF, NJ> &J,
-                                              __amdgpu_buffer_rsrc_t rs, uint8_t *slot,
-                                              int64_t foff, int lane)
-{
-#pragma unroll
-    for (int jj = 0; jj < NJ; jj++) {
-        if (jj < J.n) {
-            const uint32_t w = J.w[jj];
-            // LDS destination: wave-uniform row base (M0); the hardware adds 16 * lane
-            if (lane < (int)(w >> 16)) {
-                if constexpr (BUF)
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                        rs, ((lds_u8 *)slot) + (w & 0xffffu), 16, J.src[jj] + 16 * lane,
-                        (int)(uint32_t)foff, 0, MCS_DMA_AUX);
-                else
-                    __builtin_amdgcn_global_load_lds(J.src[jj] + foff + 16 * lane,
-                                                     ((lds_u8 *)slot) + (w & 0xffffu), 16, 0,
-                                                     MCS_DMA_AUX);
-            }
-        }
-    }
-}
-
-// DMA jobs as 1 KiB LDS windows (MCS_DMA_WINDOWS=1): a camera's footprint rows lie in LDS at a
+// Jobs are 1 KiB LDS windows: a camera's footprint rows lie in LDS at a
 // uniform pitch (a multiple of 128 B), so the 64 lanes of one LDS-DMA instruction -- lane L writes
 // 16 bytes at M0 + 16 L -- can cover 1 KiB of consecutive rows: lane L takes row
 // (16 L + 1024 w) / pitch, chunk ((16 L + 1024 w) % pitch) / 16, and is enabled only where that
@@ -595,9 +480,6 @@ __device__ __forceinline__ void stage_capture(const WaveJobs<BUF, NJ> &J,
 // instruction instead of 1, a 256-B pitch 4: half the DMA instructions per capture or fewer, and
 // the same bytes.  Every window issues its instruction (a window no span reaches enables lane 0,
 // whose 16 bytes land outside every span: no pixel reads them), so the counted vmcnt waits hold.
-#ifndef MCS_DMA_WINDOWS
-#define MCS_DMA_WINDOWS 1
-#endif
 constexpr int kDmaWindow = 16 * kWave;     // bytes of LDS one window job fills
 
 template <bool BUF, int NJ>
@@ -678,10 +560,10 @@ __device__ __forceinline__ void stage_windows_from(const WaveWins<BUF, NJ> &J,
             if constexpr (BUF)
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, ((lds_u8 *)slot) + J.lds[JJ], 16,
                                                          J.src[JJ], (int)(uint32_t)foff, 0,
-                                                         MCS_DMA_AUX);
+                                                         kDmaAux);
             else
                 __builtin_amdgcn_global_load_lds(J.src[JJ] + foff, ((lds_u8 *)slot) + J.lds[JJ],
-                                                 16, 0, MCS_DMA_AUX);
+                                                 16, 0, kDmaAux);
         }
         stage_windows_from<JJ + 1, BUF, NJ>(J, rs, slot, foff);
     }
@@ -694,35 +576,12 @@ __device__ __forceinline__ void stage_windows(const WaveWins<BUF, NJ> &J,
     stage_windows_from<0, BUF, NJ>(J, rs, slot, foff);
 }
 
-// s_waitcnt vmcnt(n) + lgkmcnt(0) for a block-uniform run-time n (n clamped to 15 by the caller;
-// waiting for fewer outstanding operations is always safe).
-__device__ __forceinline__ void wait_vmcnt_le(int n)
-{
-    switch (n) {
-    case 0: asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory"); break;
-    case 5: asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory"); break;
-    case 7: asm volatile("s_waitcnt vmcnt(7) lgkmcnt(0)" ::: "memory"); break;
-    case 8: asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory"); break;
-    case 9: asm volatile("s_waitcnt vmcnt(9) lgkmcnt(0)" ::: "memory"); break;
-    case 10: asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)" ::: "memory"); break;
-    case 11: asm volatile("s_waitcnt vmcnt(11) lgkmcnt(0)" ::: "memory"); break;
-    case 12: asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)" ::: "memory"); break;
-    case 13: asm volatile("s_waitcnt vmcnt(13) lgkmcnt(0)" ::: "memory"); break;
-    case 14: asm volatile("s_waitcnt vmcnt(14) lgkmcnt(0)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(15) lgkmcnt(0)" ::: "memory"); break;
-    }
-}
-
-// The same wait as a computed jump: `entry` = 8 n + 12 selects entry n of a table of
+// s_waitcnt vmcnt(n) + lgkmcnt(0) for a block-uniform run-time n (0 <= n <= 15; waiting for fewer
+// outstanding operations is always safe), as a computed jump: `entry` = 8 n + 12 selects entry n of a table of
 // `s_waitcnt vmcnt(n) lgkmcnt(0); s_branch end` pairs (8 bytes each) that starts 12 bytes past
 // the s_getpc_b64 result (the address of the instruction after it: s_add_u32, s_addc_u32 and
 // s_setpc_b64 are 4 bytes each).  5 scalar instructions per wait instead of the switch's compare
-// tree (~25); vcc is the 64-bit temporary.
+// tree of a switch (~25); vcc is the 64-bit temporary.
 __device__ __forceinline__ uint32_t vmcnt_entry(int n) { return 8u * (uint32_t)n + 12u; }
 __device__ __forceinline__ void wait_vmcnt_jump(uint32_t entry)
 {
@@ -832,17 +691,10 @@ __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *til
             d[p * kDescWords + 2] = d2;
         }
     }
-#if MCS_DMA_WINDOWS
     const WaveWins<BUF, NJ> J =
         wave_windows<CN, BUF, NJ>(P, h, wave, spans + (int64_t)tile * kMaxTileJobs, lane);
 #define MCS_STAGE(slot, foff) stage_windows<BUF, NJ>(J, rs, (slot) - sizeof(TileHdr), (foff))
     const int njobs = J.total;   // DMA instructions per capture of the block
-#else
-    const WaveJobs<BUF, NJ> J =
-        wave_jobs<CN, BUF, NJ>(P, h, wave, spans + (int64_t)tile * kMaxTileJobs, lane);
-#define MCS_STAGE(slot, foff) stage_capture<BUF, NJ>(J, rs, (slot), (foff), lane)
-    const int njobs = uni(h.njobs);
-#endif
     // (BUF: raw buffer over [P.base, P.base + 4 GiB); no range clamping needed, every chunk is
     // inside a frame)
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
@@ -857,7 +709,6 @@ __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *til
         MCS_STAGE(ring0 + q * buf_bytes, (int64_t)(f_beg + q) * fstride);
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-#if MCS_STREAM_LOOP2
     // Capture f's pixels from its ring slot at LDS offset `sf`, stored to the mosaic at byte
     // offset `of` = f * out_fstride.  Every lane computes (a lane past the mosaic edge holds zero
     // descriptors and reads slot byte 0); only the stores are per lane.  A wave whose lanes all
@@ -866,13 +717,6 @@ __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *til
         __builtin_amdgcn_ballot_w64(live && wide) == __builtin_amdgcn_read_exec();
     auto emit = [&](uint32_t sf, int64_t of) __attribute__((always_inline)) {
         const uint8_t *b = ring0 + sf;
-#if MCS_EXP_NOCOMPUTE
-        OutWords w;
-        w.w0 = d[0] ^ (uint32_t)of;
-        w.w1 = d[1];
-        w.w2 = d[2];
-        w.w3 = d[3];
-#else
         uint32_t rr[kPx * CN];
         uint32_t raw[kPx][6];
 #pragma unroll
@@ -895,18 +739,10 @@ __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *til
                 rr[p * CN + k] = blend<CN>(r0, r1, d[p * kDescWords + 1], d[p * kDescWords + 2], k);
         }
         const OutWords w = pack_words<CN>(rr);
-#endif
-        if (MCS_EXP_NOSTORE) return;
         uint32_t *o32 = reinterpret_cast<uint32_t *>(dst + of);
         if (all_wide) {
 #pragma unroll
-            for (int i = 0; i < CN; i++) {
-#if MCS_STORE_NT
-                __builtin_nontemporal_store(w.at(i), &o32[i]);
-#else
-                o32[i] = w.at(i);
-#endif
-            }
+            for (int i = 0; i < CN; i++) __builtin_nontemporal_store(w.at(i), &o32[i]);
         } else if (live) {
             if (wide) {
 #pragma unroll
@@ -939,7 +775,7 @@ __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *til
     const uint32_t wait_steady = vmcnt_entry(waitn), wait_all = vmcnt_entry(0);
     for (int i = 0; i < n; i++) {
         const bool steady = i < n_steady;
-        if (steady && !MCS_EXP_NODMA) MCS_STAGE(ring0 + sa, fa);
+        if (steady) MCS_STAGE(ring0 + sa, fa);
         emit(sf, of);
         wait_vmcnt_jump(steady ? wait_steady : wait_all);
         __builtin_amdgcn_s_barrier();
@@ -950,82 +786,6 @@ __device__ __forceinline__ void stream_tile(const KParams &P, const TileHdr *til
         fa += fstride;
         of += P.out_fstride;
     }
-#else
-    // (variant builds: the round-4 loop -- per-iteration staging test, run-time wait switch)
-    int slot_f = 0, slot_a = ring - 1;     // slots of capture f and of capture f + ring - 1
-    for (int f = f_beg; f < f_end; f++) {
-        const int ahead = f + ring - 1;
-        const bool full = ahead < f_end && !MCS_EXP_NODMA;
-        if (full) MCS_STAGE(ring0 + slot_a * buf_bytes, (int64_t)ahead * fstride);
-        const uint8_t *b = ring0 + slot_f * buf_bytes;
-        if (live && !MCS_EXP_NOSTORE) {
-#if MCS_EXP_NOCOMPUTE
-            OutWords w;
-            w.w0 = d[0] ^ (uint32_t)f;
-            w.w1 = d[1];
-            w.w2 = d[2];
-            w.w3 = d[3];
-#else
-            uint32_t rr[kPx * CN];
-            // every LDS read of the 4 pixels issued before the first use (one latency per capture,
-            // not one per pixel)
-            uint32_t raw[kPx][6];
-#pragma unroll
-            for (int p = 0; p < kPx; p++) {
-                const uint32_t win = d[p * kDescWords];
-                const lds_u32 *w0 = (const lds_u32 *)(((const lds_u8 *)b) + ((win & 0xffffu) & ~3u));
-                const lds_u32 *w1 = (const lds_u32 *)(((const lds_u8 *)b) + ((win >> 16) & ~3u));
-                raw[p][0] = w0[0], raw[p][1] = w0[1], raw[p][2] = w0[2];
-                raw[p][3] = w1[0], raw[p][4] = w1[1], raw[p][5] = w1[2];
-            }
-#pragma unroll
-            for (int p = 0; p < kPx; p++) {
-                const uint32_t win = d[p * kDescWords], s0 = win & 3u, s1 = (win >> 16) & 3u;
-                const uint2 r0 = make_uint2(__builtin_amdgcn_alignbyte(raw[p][1], raw[p][0], s0),
-                                            __builtin_amdgcn_alignbyte(raw[p][2], raw[p][1], s0));
-                const uint2 r1 = make_uint2(__builtin_amdgcn_alignbyte(raw[p][4], raw[p][3], s1),
-                                            __builtin_amdgcn_alignbyte(raw[p][5], raw[p][4], s1));
-#pragma unroll
-                for (int k = 0; k < CN; k++)
-                    rr[p * CN + k] = blend<CN>(r0, r1, d[p * kDescWords + 1],
-                                               d[p * kDescWords + 2], k);
-            }
-            const OutWords w = pack_words<CN>(rr);
-#endif
-            uint8_t *o = dst + (int64_t)f * P.out_fstride;
-            if (wide) {
-                uint32_t *o32 = reinterpret_cast<uint32_t *>(o);
-#pragma unroll
-                for (int i = 0; i < CN; i++) {
-#if MCS_STORE_NT
-                    __builtin_nontemporal_store(w.at(i), &o32[i]);
-#else
-                    o32[i] = w.at(i);
-#endif
-                }
-            } else {
-#if MCS_NARROW_GLOBAL
-                // (variant builds: the round-4 form, 64-bit addresses -- 72 VGPRs)
-                for (int bb = 0; bb < npx * CN; bb++)
-                    o[bb] = (uint8_t)(w.at(bb >> 2) >> (8 * (bb & 3)));
-#else
-                // (a frame-edge lane: byte stores through a buffer resource over this capture's
-                // mosaic -- 32-bit offsets instead of a 64-bit address per byte: 61 VGPRs, was 72)
-                const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
-                    (void *)(P.out + (int64_t)f * P.out_fstride), 0, 0x7fffffff, 0x00020000);
-                const uint32_t lo = (uint32_t)(dst - P.out);
-                for (int bb = 0; bb < npx * CN; bb++)
-                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(w.at(bb >> 2) >> (8 * (bb & 3))),
-                                                         ro, lo + (uint32_t)bb, 0, 0);
-#endif
-            }
-        }
-        wait_vmcnt_le(full ? waitn : 0);
-        __builtin_amdgcn_s_barrier();
-        slot_f = slot_f + 1 == ring ? 0 : slot_f + 1;
-        slot_a = slot_a + 1 == ring ? 0 : slot_a + 1;
-    }
-#endif
 #undef MCS_STAGE
 }
 
@@ -1156,18 +916,8 @@ __device__ __forceinline__ void resize_px(const KResizeArgs &a)
     {                                                                                          \
         mcs::prepare_tile<CN, IN>(P, tiles, desc, desc4, fallback, big, spans);                \
     }
-#ifdef MCS_STREAM_WAVES_PER_EU   // experiment knob: occupancy target of the streaming kernel
-#define MCS_STREAM_ATTR __attribute__((amdgpu_waves_per_eu(MCS_STREAM_WAVES_PER_EU)))
-#else
-#define MCS_STREAM_ATTR
-#endif
-#ifdef MCS_MB_BL_WPE   // experiment knob: occupancy target of the multi-band blend kernel
-#define MCS_MB_BL_ATTR __attribute__((amdgpu_waves_per_eu(MCS_MB_BL_WPE)))
-#else
-#define MCS_MB_BL_ATTR
-#endif
 #define MCS_STREAM_ENTRY(CN, SUF, BUF)                                                         \
-    extern "C" __global__ __launch_bounds__(512) MCS_STREAM_ATTR void mcs_stream_c##CN##SUF(   \
+    extern "C" __global__ __launch_bounds__(512) void mcs_stream_c##CN##SUF(         \
         const mcs::KParams P, const mcs::TileHdr *tiles, const uint32_t *desc,                \
         const uint32_t *desc4, const uint16_t *spans, int n_frames, int parts,                \
         const int *order, int n_order)                                                         \
@@ -1307,21 +1057,21 @@ extern "C" __global__ __launch_bounds__(256) void mcs_blend_classify(const mcs::
     }                                                                                          \
     MCS_MB_BANDS_ENTRY(CN, , false)                                                            \
     MCS_MB_BANDS_ENTRY(CN, _a, true)                                                           \
-    extern "C" __global__ __launch_bounds__(MCS_MB_BL_THREADS) MCS_MB_BL_ATTR void             \
+    extern "C" __global__ __launch_bounds__(MCS_MB_BL_THREADS) void                            \
         mcs_mb_blend_c##CN##_s2(                                                               \
         const mcs::KMbArgs a)                                                                  \
     {                                                                                          \
         __shared__ mcs::MbBlLds<CN, 2> lds;                                                    \
         mcs::mb_blend<CN, 2>(a, lds);                                                          \
     }                                                                                          \
-    extern "C" __global__ __launch_bounds__(MCS_MB_BL_THREADS) MCS_MB_BL_ATTR void             \
+    extern "C" __global__ __launch_bounds__(MCS_MB_BL_THREADS) void                            \
         mcs_mb_blend_c##CN##_s4(                                                               \
         const mcs::KMbArgs a)                                                                  \
     {                                                                                          \
         __shared__ mcs::MbBlLds<CN, 4> lds;                                                    \
         mcs::mb_blend<CN, 4>(a, lds);                                                          \
     }                                                                                          \
-    extern "C" __global__ __launch_bounds__(MCS_MB_BL_THREADS) MCS_MB_BL_ATTR void             \
+    extern "C" __global__ __launch_bounds__(MCS_MB_BL_THREADS) void                            \
         mcs_mb_blend_c##CN##_s8(                                                               \
         const mcs::KMbArgs a)                                                                  \
     {                                                                                          \

@@ -412,11 +412,7 @@ constexpr int big_ring_bytes() { return kBigStreamLds - (int)sizeof(TileHdr); }
 // dwords ~3 apart (C = 3, 4 pixels per lane: a permutation of the 32 ds_read_b32 banks); where
 // the source row changes inside the lane group (a rotated map), the lanes past the change read
 // one pitch further -- conflict-free only when the pitch is a multiple of 128 bytes (32 banks).
-// MCS_STREAM_PITCH128=0: packed rows (pitch = bytes).
-#ifndef MCS_STREAM_PITCH128
-#define MCS_STREAM_PITCH128 1
-#endif
-constexpr int lds_row_pitch(int bytes) { return MCS_STREAM_PITCH128 ? (bytes + 127) & ~127 : bytes; }
+constexpr int lds_row_pitch(int bytes) { return (bytes + 127) & ~127; }
 
 
 // Seam-finder inputs (mcs_plan_find_seams): per point of the 2^k grid the distance owner's
