@@ -162,7 +162,9 @@ int mcs_plan_prepare(mcs_plan *plan, void *stream);
  * large-footprint streaming launch (16 rows per wave, 120 KiB ring), then per capture the
  * multi-band blend's computed ("mixed") pixels and R1 entries, then per capture the bytes the
  * LDS-path tiles' footprint DMAs read (each row's span in 16-byte chunks) and the bytes of their
- * footprint boxes (every row at the box width).  Entries past 15 read 0. */
+ * footprint boxes (every row at the box width); stats[16..19] = the multi-band sweep's strips
+ * (MCS_MB_SWEEP=1 plans; 0 otherwise), the mosaic pixels they write per capture, threads per
+ * sweep workgroup, and the rows of its precomputed sample descriptors.  Entries past 19 read 0. */
 int mcs_plan_stats(const mcs_plan *plan, int64_t *stats, int n);
 
 /* Blend mode of the plan (MCS_BLEND_*; default NONE = the reference's paste).  Changing it drops
