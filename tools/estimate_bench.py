@@ -156,6 +156,7 @@ def main():
         for key in tot:
             tot[key] += t[key]
     elapsed = time.perf_counter() - t0
+    captures = args.steps
     errs = [pair_error(h, T, W, Hh) if h is not None else None for (h, *_), T in zip(res, truth)]
     line = {
         "metric": "rig homography estimations/sec (C3: 4-cam 1080p, ORB + BF Hamming kNN-2 + "
