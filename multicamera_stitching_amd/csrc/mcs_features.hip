@@ -455,7 +455,7 @@ constexpr int kOrbSX = kOrbTX + 2, kOrbSY = kOrbTY + 2;                         
 
 extern "C" __global__ __launch_bounds__(256) void mcs_orb_level(const mcs::KOrbPyrArgs p)
 {
-    __shared__ uint8_t img[kOrbLY * kOrbLX];
+    __shared__ __attribute__((aligned(16))) uint8_t img[kOrbLY * kOrbLX];
     __shared__ uint16_t hb[(kOrbTY + 6) * kOrbTX];
     __shared__ uint8_t sc[kOrbSY * kOrbSX];
     __shared__ int sx[kOrbTX * kOrbTY];
@@ -471,9 +471,16 @@ extern "C" __global__ __launch_bounds__(256) void mcs_orb_level(const mcs::KOrbP
     if (tid == 0) ns = 0, nf = 0, nc = 0;
     if (x0 >= kOrbHalo && y0 >= kOrbHalo && x0 + kOrbTX + kOrbHalo <= w &&
         y0 + kOrbTY + kOrbHalo <= h) {   // interior tile: no reflection
+        // (dword loads: a staged row is 18 dwords; the level rows start at any byte, and gfx950
+        // global loads take unaligned dwords)
         const uint8_t *src = im + (int64_t)(y0 - kOrbHalo) * w + (x0 - kOrbHalo);
-        for (int i = tid; i < kOrbLY * kOrbLX; i += 256)
-            img[i] = src[(i / kOrbLX) * w + i % kOrbLX];
+        constexpr int DW = kOrbLX / 4;
+        static_assert(kOrbLX % 4 == 0, "ORB tile rows: whole dwords");
+        for (int i = tid; i < kOrbLY * DW; i += 256) {
+            uint32_t v;
+            __builtin_memcpy(&v, src + (int64_t)(i / DW) * w + 4 * (i % DW), 4);
+            reinterpret_cast<uint32_t *>(img)[i] = v;
+        }
     } else {
         for (int i = tid; i < kOrbLY * kOrbLX; i += 256) {
             const int yy = orb_refl(min(max(y0 - kOrbHalo + i / kOrbLX, -(h - 1)), 2 * h - 2), h);

@@ -78,9 +78,11 @@ struct OrbCand {
     double response;
 };
 // mcs_orb_level's tile: kOrbTileW x kOrbTileH pixels of a level per block (MCS_ORB_TILE_H: 16 or
-// 32 rows)
+// 32 rows).  32: the 4-pixel halo and the five barrier phases shared by twice the pixels (C3
+// resident estimate + stitch 2,860-2,865 -> 2,963-2,984 captures/s with the dword staging, same
+// box, three alternations: profiles/r06_orb_tile_ab.txt)
 #ifndef MCS_ORB_TILE_H
-#define MCS_ORB_TILE_H 16
+#define MCS_ORB_TILE_H 32
 #endif
 constexpr int kOrbTileW = 64, kOrbTileH = MCS_ORB_TILE_H;
 // All levels of one frame in one launch (mcs_orb_level): grid (bstart[nlevels]) blocks of 256
