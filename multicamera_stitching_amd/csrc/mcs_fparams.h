@@ -77,12 +77,13 @@ struct OrbCand {
     int x, y;
     double response;
 };
-// mcs_orb_level's tile: kOrbTileW x kOrbTileH pixels of a level per block (MCS_ORB_TILE_H: 16 or
-// 32 rows).  32: the 4-pixel halo and the five barrier phases shared by twice the pixels (C3
-// resident estimate + stitch 2,860-2,865 -> 2,963-2,984 captures/s with the dword staging, same
-// box, three alternations: profiles/r06_orb_tile_ab.txt)
+// mcs_orb_level's tile: kOrbTileW x kOrbTileH pixels of a level per block (MCS_ORB_TILE_H: 16, 32
+// or 64 rows).  64: the 4-pixel halo and the five barrier phases shared by four times the pixels
+// of round 5's 64 x 16 tile, 52 KB of LDS, 3 blocks per CU (C3 resident estimate + stitch, same
+// boxes: 16 rows 2,860-2,865, 32 rows 2,957-2,984, 64 rows 3,131-3,236 captures/s;
+// profiles/r06_orb_tile_ab.txt)
 #ifndef MCS_ORB_TILE_H
-#define MCS_ORB_TILE_H 32
+#define MCS_ORB_TILE_H 64
 #endif
 constexpr int kOrbTileW = 64, kOrbTileH = MCS_ORB_TILE_H;
 // All levels of one frame in one launch (mcs_orb_level): grid (bstart[nlevels]) blocks of 256
