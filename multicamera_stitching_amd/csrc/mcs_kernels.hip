@@ -128,6 +128,8 @@ __device__ __forceinline__ int place_cols(int sx, int sw, uint32_t wl, uint32_t 
 // byte column of each window's first tap) and the packed u16 weight pairs seen from them.
 struct Geo {
     int cam, r0, c0, r1, c1;
+    int cw, ch;                  // the camera's frame size
+    const uint8_t *frame;        // its frame 0 (P.cams[cam])
     uint32_t w0, w1;
     int fx, fy;                  // the bilinear fraction (1/32 px)
     bool plain;                  // all four taps in the image (or fy = 0 and both row-0 taps):
@@ -140,29 +142,53 @@ __device__ __forceinline__ Geo describe_geo(const KParams &P, int x, int y)
     Geo g;
     const int s = pixel_stage<INTERP>(P, x, y);
     int sw, sh, X, Y;
+    g.cam = 0;
+    g.cw = P.cam_w[0];
+    g.ch = P.cam_h[0];
+    g.frame = P.cams[0];
     if (s == -2) {               // no camera: all weights 0 (the border value)
-        g.cam = 0;
         sw = P.cam0_w;
         sh = P.cam0_h;
         X = Y = -(1 << 20);
     } else if (s < 0) {          // camera 0 pasted whole: a copy (weights 32768, 0, 0, 0)
-        g.cam = 0;
         sw = P.cam0_w;
         sh = P.cam0_h;
         X = (x + P.cam0_offx) << 5;
         Y = (y + P.cam0_offy) << 5;
     } else {
-        const KStage &S = P.st[s];
-        g.cam = S.cam;
-        sw = S.src_w;
-        sh = S.src_h;
-        stage_map<INTERP>(P, S, x, y, X, Y);
-        if (INTERP == MCS_INTER_NEAREST) {   // remapNearest: a copy of (X, Y) or the border value
-            X = sat_i16(X);
-            Y = sat_i16(Y);
-            const bool in = (unsigned)X < (unsigned)sw && (unsigned)Y < (unsigned)sh;
-            X = in ? X * 32 : -(1 << 20);
-            Y = in ? Y * 32 : -(1 << 20);
+        sw = sh = X = Y = 0;
+    }
+    // The stages of the wave's pixels one at a time, each with its parameters read by scalar loads:
+    // P.st or P.cams indexed by a per-lane stage are vector loads from the kernel arguments (~40 per
+    // wave in the direct stitch).  (P is always a kernel argument here, i.e. in the constant
+    // address space, which is what makes the uniform-address reads scalar.)
+    typedef __attribute__((address_space(4))) const KParams ckp;
+    const ckp *P4 = (const ckp *)&P;
+    bool pending = s >= 0;
+    for (uint64_t m = __builtin_amdgcn_ballot_w64(pending); m != 0;
+         m = __builtin_amdgcn_ballot_w64(pending)) {
+        const int s0 = __builtin_amdgcn_readlane(s, (int)__builtin_ctzll(m));
+        // (read before the branch: inside it the compiler would address them by the lane's own s,
+        // equal to s0 there, with vector loads)
+        const KStage S = P4->st[s0];
+        const int cw = P4->cam_w[S.cam], ch = P4->cam_h[S.cam];
+        const uint8_t *frame = P4->cams[S.cam];
+        if (pending && s == s0) {
+            g.cam = S.cam;
+            g.cw = cw;
+            g.ch = ch;
+            g.frame = frame;
+            sw = S.src_w;
+            sh = S.src_h;
+            stage_map<INTERP>(P, S, x, y, X, Y);
+            if (INTERP == MCS_INTER_NEAREST) {   // remapNearest: a copy of (X, Y) or the border
+                X = sat_i16(X);
+                Y = sat_i16(Y);
+                const bool in = (unsigned)X < (unsigned)sw && (unsigned)Y < (unsigned)sh;
+                X = in ? X * 32 : -(1 << 20);
+                Y = in ? Y * 32 : -(1 << 20);
+            }
+            pending = false;
         }
     }
     const int sx = sat_i16(X >> 5), sy = sat_i16(Y >> 5), fx = X & 31, fy = Y & 31;
@@ -196,12 +222,12 @@ __device__ __forceinline__ Desc<OFF32> describe(const KParams &P, int x, int y)
 {
     const Geo g = describe_geo<CN, INTERP>(P, x, y);
     Desc<OFF32> d;
-    const int64_t pitch = (int64_t)P.cam_w[g.cam] * CN, fbytes = pitch * P.cam_h[g.cam];
+    const int64_t pitch = (int64_t)g.cw * CN, fbytes = pitch * g.ch;
     const int64_t o0 = (int64_t)g.r0 * pitch + g.c0, o1 = (int64_t)g.r1 * pitch + g.c1;
     // an 8-byte window must end inside the frame: move it left, remember by how much
     const int64_t sh0 = o0 + 8 > fbytes ? o0 + 8 - fbytes : 0;
     const int64_t sh1 = o1 + 8 > fbytes ? o1 + 8 - fbytes : 0;
-    const uint64_t cam_off = (uint64_t)(uintptr_t)P.cams[g.cam] - (uint64_t)(uintptr_t)P.base;
+    const uint64_t cam_off = (uint64_t)(uintptr_t)g.frame - (uint64_t)(uintptr_t)P.base;
     d.off0 = (typename Desc<OFF32>::off_t)(cam_off + (uint64_t)(o0 - sh0));
     d.off1 = (typename Desc<OFF32>::off_t)(cam_off + (uint64_t)(o1 - sh1));
     d.w0 = g.w0;
