@@ -456,7 +456,7 @@ constexpr int kOrbSX = kOrbTX + 2, kOrbSY = kOrbTY + 2;                         
 extern "C" __global__ __launch_bounds__(256) void mcs_orb_level(const mcs::KOrbPyrArgs p)
 {
     __shared__ __attribute__((aligned(16))) uint8_t img[kOrbLY * kOrbLX];
-    __shared__ uint16_t hb[(kOrbTY + 6) * kOrbTX];
+    __shared__ __attribute__((aligned(16))) uint16_t hb[(kOrbTY + 6) * kOrbTX];
     __shared__ uint8_t sc[kOrbSY * kOrbSX];
     __shared__ int sx[kOrbTX * kOrbTY];
     __shared__ uint16_t fl[kOrbSY * kOrbSX], fc[kOrbSY * kOrbSX];
@@ -489,13 +489,30 @@ extern "C" __global__ __launch_bounds__(256) void mcs_orb_level(const mcs::KOrbP
         }
     }
     __syncthreads();
-    // blur: horizontal over rows y0 - 3 .. y0 + 18, then vertical
-    for (int i = tid; i < (kOrbTY + 6) * kOrbTX; i += 256) {
-        const uint8_t *r = img + (i / kOrbTX + 1) * kOrbLX + i % kOrbTX + 1;
-        int s = 0;
+    // blur: horizontal over rows y0 - 3 .. y0 + kOrbTY + 2, then vertical; 4 columns per thread
+    // (the horizontal pass reads its 10 bytes as 4 dwords + v_alignbyte and writes 4 u16 at once)
+    typedef __attribute__((address_space(3))) const uint32_t lu32;
+    typedef __attribute__((address_space(3))) const uint8_t lu8;
+    typedef __attribute__((address_space(3))) uint2 lu2;
+    constexpr int Q = kOrbTX / 4;
+    for (int i = tid; i < (kOrbTY + 6) * Q; i += 256) {
+        const int row = i / Q, c4 = 4 * (i - row * Q);
+        const int a = (row + 1) * kOrbLX + c4 + 1;   // the first tap of the 4 outputs
+        const lu32 *d = (const lu32 *)((lu8 *)img + (a & ~3));
+        const uint32_t sh = (uint32_t)a & 3u, x0 = d[0], x1 = d[1], x2 = d[2], x3 = d[3];
+        const uint32_t b[3] = {__builtin_amdgcn_alignbyte(x1, x0, sh),
+                               __builtin_amdgcn_alignbyte(x2, x1, sh),
+                               __builtin_amdgcn_alignbyte(x3, x2, sh)};
+        uint32_t o[4];
 #pragma unroll
-        for (int t = 0; t < 7; t++) s += mcs::kOrbBlur[t] * r[t];
-        hb[i] = (uint16_t)s;
+        for (int j = 0; j < 4; j++) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int t = 0; t < 7; t++)
+                v += (uint32_t)mcs::kOrbBlur[t] * ((b[(j + t) >> 2] >> (8 * ((j + t) & 3))) & 255u);
+            o[j] = v;
+        }
+        *(lu2 *)(hb + row * kOrbTX + c4) = make_uint2(o[0] | (o[1] << 16), o[2] | (o[3] << 16));
     }
     // FAST on the tile and a one-pixel ring (positions x0 - 1 .., y0 - 1 ..), in three compacted
     // stages so that every stage runs on full waves: the cardinal pre-test everywhere, the
@@ -527,14 +544,27 @@ extern "C" __global__ __launch_bounds__(256) void mcs_orb_level(const mcs::KOrbP
         sc[i] = (uint8_t)mcs::orb_fast_score(at(i), kOrbLX);
     }
     uint8_t *blur = p.blur + cam * p.stride + p.off[l];
-    for (int i = tid; i < kOrbTY * kOrbTX; i += 256) {
-        const int yy = y0 + i / kOrbTX, xx = x0 + i % kOrbTX;
+    for (int i = tid; i < kOrbTY * Q; i += 256) {
+        const int row = i / Q, c4 = 4 * (i - row * Q);
+        const int yy = y0 + row, xx = x0 + c4;
         if (yy >= h || xx >= w) continue;
-        const uint16_t *c = hb + (i / kOrbTX) * kOrbTX + i % kOrbTX;
-        int s = 0;
+        uint32_t sv[4] = {32768u, 32768u, 32768u, 32768u};
 #pragma unroll
-        for (int t = 0; t < 7; t++) s += mcs::kOrbBlur[t] * (int)c[t * kOrbTX];
-        blur[(int64_t)yy * w + xx] = (uint8_t)((s + 32768) >> 16);
+        for (int t = 0; t < 7; t++) {
+            const uint2 v = *(const lu2 *)(hb + (row + t) * kOrbTX + c4);
+            sv[0] += (uint32_t)mcs::kOrbBlur[t] * (v.x & 0xffffu);
+            sv[1] += (uint32_t)mcs::kOrbBlur[t] * (v.x >> 16);
+            sv[2] += (uint32_t)mcs::kOrbBlur[t] * (v.y & 0xffffu);
+            sv[3] += (uint32_t)mcs::kOrbBlur[t] * (v.y >> 16);
+        }
+        uint8_t *o = blur + (int64_t)yy * w + xx;
+        if (xx + 4 <= w) {   // (an unaligned dword store: level rows start at any byte)
+            const uint32_t word = (sv[0] >> 16) | ((sv[1] >> 16) << 8) | ((sv[2] >> 16) << 16) |
+                                  ((sv[3] >> 16) << 24);
+            __builtin_memcpy(o, &word, 4);
+        } else {
+            for (int j = 0; j < w - xx; j++) o[j] = (uint8_t)(sv[j] >> 16);
+        }
     }
     __syncthreads();
     // 3x3 NMS of the tile's pixels; survivors (packed y << 16 | x) compacted in LDS
