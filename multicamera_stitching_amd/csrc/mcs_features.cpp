@@ -525,7 +525,7 @@ unsigned mcs::feat::pyramid_args(const OrbGeom &g, uint8_t *lvl, KOrbBuildArgs &
     }
     a.lds_w = mw;
     a.lds_h = mh;
-    if (2 * (size_t)mw * mh > 64 * 1024) return 0;
+    if (2 * (size_t)mw * mh + 16 > 64 * 1024) return 0;   // (+16: mcs_orb_pyramid reads 8 bytes past a row)
     return (unsigned)(a.gx * gy);
 }
 
@@ -654,7 +654,7 @@ int orb_detect(const uint8_t *image, bool on_device, int w, int h, int channels,
         void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &ba, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz,
                        HIP_LAUNCH_PARAM_END};
         e = A->hipModuleLaunchKernel(k->orb_pyramid, pyr_blocks, 1, 1, 256, 1, 1,
-                                     (unsigned)(2 * ba.lds_w * ba.lds_h), s, nullptr, cfg);
+                                     (unsigned)(2 * ba.lds_w * ba.lds_h + 16), s, nullptr, cfg);
     } else {
         for (int l = 1; l < nlevels && e == hipSuccess && rc == MCS_OK; l++)
             rc = mcs_resize_linear_device(buf + o_lvl + off[l - 1], lw[l - 1], lh[l - 1],

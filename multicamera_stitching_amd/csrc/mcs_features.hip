@@ -781,32 +781,65 @@ extern "C" __global__ __launch_bounds__(256) void mcs_orb_pyramid(const mcs::KOr
         y1[l - 1] = min(max(s + 1, 0), sh - 1) + 1;
     }
     uint8_t *buf[2] = {pyr_lds, pyr_lds + a.lds_w * a.lds_h};
-    for (int l = 1; l <= L; l++) {
+    typedef __attribute__((address_space(3))) const uint32_t lu32;
+    typedef __attribute__((address_space(3))) uint8_t lu8;
+    // 8 bytes of a source row from byte o: level 0 by an unaligned global dwordx2, the LDS regions
+    // by three aligned dword reads + v_alignbyte (the LDS block has 16 bytes of slack past them)
+    auto row8_global = [](const uint8_t *q, int o) {
+        uint2 v;
+        __builtin_memcpy(&v, q + o, 8);
+        return v;
+    };
+    auto row8_lds = [](const uint8_t *q, int o) {
+        const uint32_t a8 = (uint32_t)(uintptr_t)((const lu8 *)q) + (uint32_t)o;
+        const lu32 *d = (const lu32 *)(uintptr_t)(a8 & ~3u);
+        const uint32_t sh = a8 & 3u, x0 = d[0], x1 = d[1], x2 = d[2];
+        return make_uint2(__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh));
+    };
+    // one level's region, 4 horizontally adjacent pixels per thread: their source columns lie
+    // within 8 bytes of the first's (every level step is below 2x), so each source row is read once
+    auto level = [&](int l, const uint8_t *src, int spitch, int sx0, int sy0, auto row8) {
         const int rw = x1[l] - x0[l], rh = y1[l] - y0[l];
         const int sw = a.w[l - 1], sh = a.h[l - 1];
-        // source: level 0 in global memory, else the previous region in LDS
-        const uint8_t *src = l == 1 ? lvl + a.off[0] : buf[(l - 1) & 1];
-        const int spitch = l == 1 ? sw : x1[l - 1] - x0[l - 1];
-        const int sx0 = l == 1 ? 0 : x0[l - 1], sy0 = l == 1 ? 0 : y0[l - 1];
-        uint8_t *dst = buf[l & 1];
+        lu8 *dst = (lu8 *)buf[l & 1];
         uint8_t *out = lvl + a.off[l];
-        for (int i = tid; i < rw * rh; i += 256) {
-            const int x = x0[l] + i % rw, y = y0[l] + i / rw;
-            int s, a0, a1, sy, b0, b1;
-            pyr_axis(x, a.sx[l], sw, true, s, a0, a1);
+        const int gw = (rw + 3) >> 2;
+        for (int i = tid; i < gw * rh; i += 256) {
+            const int gy = i / gw, gx = i - gy * gw;
+            const int y = y0[l] + gy, xs = x0[l] + 4 * gx, n = min(4, x1[l] - xs);
+            int sy, b0, b1;
             pyr_axis(y, a.sy[l], sh, false, sy, b0, b1);
             const int r0 = min(max(sy, 0), sh - 1), r1 = min(max(sy + 1, 0), sh - 1);
-            const uint8_t *p0 = src + (int64_t)(r0 - sy0) * spitch + (s - sx0);
-            const uint8_t *p1 = src + (int64_t)(r1 - sy0) * spitch + (s - sx0);
-            const bool one = s >= sw - 1;
-            const int d0 = one ? p0[0] * 2048 : p0[0] * a0 + p0[1] * a1;
-            const int d1 = one ? p1[0] * 2048 : p1[0] * a0 + p1[1] * a1;
-            const uint8_t v = (uint8_t)((((b0 * (d0 >> 4)) >> 16) + ((b1 * (d1 >> 4)) >> 16) + 2) >> 2);
-            if (l < L) dst[i] = v;
-            out[(int64_t)y * a.w[l] + x] = v;
+            int sc[4], c0[4], c1[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) pyr_axis(min(xs + j, x1[l] - 1), a.sx[l], sw, true, sc[j], c0[j], c1[j]);
+            const int o = sc[0] - sx0;
+            const uint2 w0 = row8(src + (int64_t)(r0 - sy0) * spitch, o);
+            const uint2 w1 = row8(src + (int64_t)(r1 - sy0) * spitch, o);
+            auto byte_at = [](uint2 w, int k) {
+                return (int)(((k < 4 ? w.x : w.y) >> (8 * (k & 3))) & 255u);
+            };
+            uint32_t word = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int k = sc[j] - sc[0];
+                const bool one = sc[j] >= sw - 1;
+                const int d0 = one ? byte_at(w0, k) * 2048 : byte_at(w0, k) * c0[j] + byte_at(w0, k + 1) * c1[j];
+                const int d1 = one ? byte_at(w1, k) * 2048 : byte_at(w1, k) * c0[j] + byte_at(w1, k + 1) * c1[j];
+                const uint32_t v = (uint32_t)((((b0 * (d0 >> 4)) >> 16) + ((b1 * (d1 >> 4)) >> 16) + 2) >> 2) & 255u;
+                word |= v << (8 * j);
+                if (l < L && j < n) dst[gy * rw + 4 * gx + j] = (uint8_t)v;
+            }
+            uint8_t *po = out + (int64_t)y * a.w[l] + xs;
+            if (n == 4) __builtin_memcpy(po, &word, 4);   // (an unaligned dword store)
+            else
+                for (int j = 0; j < n; j++) po[j] = (uint8_t)(word >> (8 * j));
         }
         __syncthreads();
-    }
+    };
+    level(1, lvl + a.off[0], a.w[0], 0, 0, row8_global);
+    for (int l = 2; l <= L; l++)
+        level(l, buf[(l - 1) & 1], x1[l - 1] - x0[l - 1], x0[l - 1], y0[l - 1], row8_lds);
 }
 
 // ---- A rig capture on the device (mcs_rig.cpp; KRigArgs) ---------------------------------------

@@ -426,7 +426,7 @@ int enqueue_chain(mcs_rig_job *j, const mcs::rt::Api *A, const mcs::feat::Featur
     if (rc == MCS_OK && L > 1) {
         if (d.pyr_blocks > 0) {
             rc = launch(A, k->orb_pyramid, d.pyr_blocks, C, 256, &d.ba, sizeof(d.ba), s, 1,
-                        (unsigned)(2 * d.ba.lds_w * d.ba.lds_h));
+                        (unsigned)(2 * d.ba.lds_w * d.ba.lds_h + 16));
         } else {
             for (int l = 1; l < L && rc == MCS_OK; l++)
                 rc = mcs_resize_linear_device(d.ga.gray + g.off[l - 1], g.lw[l - 1], g.lh[l - 1],
