@@ -793,7 +793,8 @@ def companion_lines():
     """The 1-GPU companion lines beside C2, C4 and C5 (which every N measures in-process): C3
     (per-capture estimation + stitch through the rig jobs, frames uploaded every capture,
     tools/estimate_bench.py), the Hamming matcher's pairs/s (tools/match_bench.py) and the C4
-    graph-cut seams per plan (tools/seam_bench.py)."""
+    graph-cut seams per plan (tools/seam_bench.py); C3 again with the frames resident in HBM
+    (the GPU-bound rate of the same estimate + stitch chain)."""
     return {
         "c3_estimate_and_stitch": _child_line(
             ["tools/estimate_bench.py", "--stitch", "--pipelined", "--overlap", "--depth", "4",
@@ -801,6 +802,12 @@ def companion_lines():
             ("metric", "value", "unit", "ms_per_step", "stitched_mpix_per_s", "config",
              "latency_ms_upload_to_homographies", "h2d_gb_per_s", "h2d_link_ceiling_gb_per_s",
              "frac_of_h2d_link", "max_reproj_err_px_vs_truth", "max_abs_diff_vs_cpu_render")),
+        "c3_estimate_and_stitch_resident": _child_line(
+            ["tools/estimate_bench.py", "--stitch", "--pipelined", "--overlap", "--resident",
+             "--depth", "4", "--steps", "400", "--warmup", "20", "--no-cpu-baseline"], 300,
+            ("metric", "value", "unit", "ms_per_step", "stitched_mpix_per_s",
+             "frames_resident_in_hbm", "max_reproj_err_px_vs_truth",
+             "max_abs_diff_vs_cpu_render")),
         "hamming_matcher": _child_line(["tools/match_bench.py"], 200,
                                        ("metric", "unit", "sizes", "ops_per_pair",
                                         "peak_lane_ops_per_s")),
