@@ -678,8 +678,30 @@ extern "C" __global__ __launch_bounds__(1024) void mcs_orb_select(const mcs::KOr
     }
 }
 
-// grid (n), block 64: one wave per keypoint -- orientation moments (lane v sums row v of the
-// disk, wave reduction), then 4 rBRIEF pairs per lane packed into the 32 descriptor bytes.
+// The orientation disk (rows v = 0 .. kOrbHalfPatch, |u| <= kOrbUmax[v]) as a flat list of
+// (v, u) entries, (v << 8) | (u & 255); an entry of row v >= 1 stands for the pixels (u, v) and
+// (u, -v).  Dealt over the wave's 64 lanes (~6 entries each) instead of one row per lane.
+struct OrbMomTab {
+    int16_t e[512];
+    int n;
+};
+constexpr OrbMomTab orb_mom_tab()
+{
+    OrbMomTab t{};
+    int i = 0;
+    for (int u = -mcs::kOrbHalfPatch; u <= mcs::kOrbHalfPatch; u++) t.e[i++] = (int16_t)(u & 255);
+    for (int v = 1; v <= mcs::kOrbHalfPatch; v++)
+        for (int u = -mcs::kOrbUmax[v]; u <= mcs::kOrbUmax[v]; u++)
+            t.e[i++] = (int16_t)((v << 8) | (u & 255));
+    t.n = i;
+    return t;
+}
+__constant__ OrbMomTab kOrbMom = orb_mom_tab();
+static_assert(orb_mom_tab().n <= 512, "ORB orientation disk entries");
+
+// grid (n), block 64: one wave per keypoint -- orientation moments (the disk's entries dealt over
+// the lanes, integer sums, wave reduction), then 4 rBRIEF pairs per lane packed into the 32
+// descriptor bytes.
 extern "C" __global__ __launch_bounds__(64) void mcs_orb_describe(const mcs::KOrbDescArgs a)
 {
     using namespace mcs;
@@ -692,19 +714,14 @@ extern "C" __global__ __launch_bounds__(64) void mcs_orb_describe(const mcs::KOr
     const int64_t co = cam * a.stride;
     const uint8_t *p = a.img[lvl] + co + (int64_t)y * w + x;
     long long m10 = 0, m01 = 0;
-    if (lane <= kOrbHalfPatch) {
-        const int v = lane;
+    for (int i = lane; i < kOrbMom.n; i += 64) {
+        const int e = kOrbMom.e[i], v = e >> 8, u = (int)(int8_t)(e & 255);
         if (v == 0) {
-            for (int u = -kOrbHalfPatch; u <= kOrbHalfPatch; u++) m10 += u * (int)p[u];
+            m10 += u * (int)p[u];
         } else {
-            long long vs = 0;
-            const int d = kOrbUmax[v];
-            for (int u = -d; u <= d; u++) {
-                const int q = p[u + v * w], r = p[u - v * w];
-                vs += q - r;
-                m10 += (long long)u * (q + r);
-            }
-            m01 = v * vs;
+            const int q = p[u + v * w], r = p[u - v * w];
+            m01 += (long long)(v * (q - r));
+            m10 += (long long)(u * (q + r));
         }
     }
     for (int off = 32; off > 0; off >>= 1) {
