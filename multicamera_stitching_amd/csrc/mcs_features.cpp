@@ -662,7 +662,7 @@ int orb_detect(const uint8_t *image, bool on_device, int w, int h, int channels,
                                           0, 1, 1, device, s);
     }
     if (e == hipSuccess && rc == MCS_OK) {
-        // blur, FAST, NMS and Harris of every level: one launch (mcs_orb_level, 64 x 16 tiles)
+        // blur, FAST, NMS and Harris of every level: one launch (mcs_orb_level, kOrbTileW x kOrbTileH tiles)
         mcs::KOrbPyrArgs pa;
         std::memset(&pa, 0, sizeof(pa));
         pa.img = buf + o_lvl;
@@ -680,7 +680,8 @@ int orb_detect(const uint8_t *image, bool on_device, int w, int h, int channels,
             pa.bstart[l + 1] = pa.bstart[l] + (lw[l] + mcs::kOrbTileW - 1) / mcs::kOrbTileW *
                                             ((lh[l] + mcs::kOrbTileH - 1) / mcs::kOrbTileH);
         }
-        rc = launch(A, k->orb_level, (unsigned)pa.bstart[nlevels], 1, 256, &pa, sizeof(pa), s);
+        rc = launch(A, k->orb_level, (unsigned)pa.bstart[nlevels], 1, mcs::kOrbLevelThreads, &pa,
+                    sizeof(pa), s);
     }
     // Device ranking (mcs_orb_select) and description, then ONE copy back of counts,
     // keypoints, descriptors, orientations and responses.  A level with more than kOrbSelMax

@@ -453,7 +453,7 @@ constexpr int kOrbTX = mcs::kOrbTileW, kOrbTY = mcs::kOrbTileH, kOrbHalo = 4;
 constexpr int kOrbLX = kOrbTX + 2 * kOrbHalo, kOrbLY = kOrbTY + 2 * kOrbHalo;   // 72 x 24
 constexpr int kOrbSX = kOrbTX + 2, kOrbSY = kOrbTY + 2;                         // score ring
 
-extern "C" __global__ __launch_bounds__(256) void mcs_orb_level(const mcs::KOrbPyrArgs p)
+extern "C" __global__ __launch_bounds__(mcs::kOrbLevelThreads) void mcs_orb_level(const mcs::KOrbPyrArgs p)
 {
     __shared__ __attribute__((aligned(16))) uint8_t img[kOrbLY * kOrbLX];
     __shared__ __attribute__((aligned(16))) uint16_t hb[(kOrbTY + 6) * kOrbTX];
@@ -482,13 +482,13 @@ extern "C" __global__ __launch_bounds__(256) void mcs_orb_level(const mcs::KOrbP
         const uint8_t *src = im + (int64_t)(y0 - kOrbHalo) * w + (x0 - kOrbHalo);
         constexpr int DW = kOrbLX / 4;
         static_assert(kOrbLX % 4 == 0, "ORB tile rows: whole dwords");
-        for (int i = tid; i < kOrbLY * DW; i += 256) {
+        for (int i = tid; i < kOrbLY * DW; i += mcs::kOrbLevelThreads) {
             uint32_t v;
             __builtin_memcpy(&v, src + (int64_t)(i / DW) * w + 4 * (i % DW), 4);
             reinterpret_cast<uint32_t *>(img)[i] = v;
         }
     } else {
-        for (int i = tid; i < kOrbLY * kOrbLX; i += 256) {
+        for (int i = tid; i < kOrbLY * kOrbLX; i += mcs::kOrbLevelThreads) {
             const int yy = orb_refl(min(max(y0 - kOrbHalo + i / kOrbLX, -(h - 1)), 2 * h - 2), h);
             const int xx = orb_refl(min(max(x0 - kOrbHalo + i % kOrbLX, -(w - 1)), 2 * w - 2), w);
             img[i] = im[(int64_t)yy * w + xx];
@@ -501,7 +501,7 @@ extern "C" __global__ __launch_bounds__(256) void mcs_orb_level(const mcs::KOrbP
     typedef __attribute__((address_space(3))) const uint8_t lu8;
     typedef __attribute__((address_space(3))) uint2 lu2;
     constexpr int Q = kOrbTX / 4;
-    for (int i = tid; i < (kOrbTY + 6) * Q; i += 256) {
+    for (int i = tid; i < (kOrbTY + 6) * Q; i += mcs::kOrbLevelThreads) {
         const int row = i / Q, c4 = 4 * (i - row * Q);
         const int a = (row + 1) * kOrbLX + c4 + 1;   // the first tap of the 4 outputs
         const lu32 *d = (const lu32 *)((lu8 *)img + (a & ~3));
@@ -532,7 +532,7 @@ extern "C" __global__ __launch_bounds__(256) void mcs_orb_level(const mcs::KOrbP
         list[__shfl(base, leader) + __popcll(act & ((1ull << lane) - 1ull))] = (uint16_t)i;
     };
     auto at = [&](int i) { return img + (i / kOrbSX + kOrbHalo - 1) * kOrbLX + i % kOrbSX + kOrbHalo - 1; };
-    for (int i = tid; i < kOrbSY * kOrbSX; i += 256) {
+    for (int i = tid; i < kOrbSY * kOrbSX; i += mcs::kOrbLevelThreads) {
         const int yy = y0 - 1 + i / kOrbSX, xx = x0 - 1 + i % kOrbSX;
         sc[i] = 0;
         if (xx >= lo && yy >= lo && xx < w - lo && yy < h - lo &&
@@ -540,17 +540,17 @@ extern "C" __global__ __launch_bounds__(256) void mcs_orb_level(const mcs::KOrbP
             append(&nc, fc, i);
     }
     __syncthreads();
-    for (int j = tid; j < nc; j += 256) {
+    for (int j = tid; j < nc; j += mcs::kOrbLevelThreads) {
         const int i = fc[j];
         if (mcs::orb_fast_test(at(i), kOrbLX, p.threshold)) append(&nf, fl, i);
     }
     __syncthreads();
-    for (int j = tid; j < nf; j += 256) {
+    for (int j = tid; j < nf; j += mcs::kOrbLevelThreads) {
         const int i = fl[j];
         sc[i] = (uint8_t)mcs::orb_fast_score(at(i), kOrbLX);
     }
     uint8_t *blur = p.blur + cam * p.stride + p.off[l];
-    for (int i = tid; i < kOrbTY * Q; i += 256) {
+    for (int i = tid; i < kOrbTY * Q; i += mcs::kOrbLevelThreads) {
         const int row = i / Q, c4 = 4 * (i - row * Q);
         const int yy = y0 + row, xx = x0 + c4;
         if (yy >= h || xx >= w) continue;
@@ -575,7 +575,7 @@ extern "C" __global__ __launch_bounds__(256) void mcs_orb_level(const mcs::KOrbP
     __syncthreads();
     // 3x3 NMS of the tile's pixels; survivors (packed y << 16 | x) compacted in LDS
     const int e = mcs::kOrbEdge;
-    for (int i = tid; i < kOrbTY * kOrbTX; i += 256) {
+    for (int i = tid; i < kOrbTY * kOrbTX; i += mcs::kOrbLevelThreads) {
         const int yy = y0 + i / kOrbTX, xx = x0 + i % kOrbTX;
         bool keep = xx >= e && yy >= e && xx < w - e && yy < h - e;
         if (keep) {
@@ -598,7 +598,7 @@ extern "C" __global__ __launch_bounds__(256) void mcs_orb_level(const mcs::KOrbP
     }
     __syncthreads();
     const int n = ns;
-    for (int j0 = 0; j0 < n; j0 += 256) {
+    for (int j0 = 0; j0 < n; j0 += mcs::kOrbLevelThreads) {
         const int j = j0 + tid;
         if (j >= n) break;
         const int i = sx[j];

@@ -86,6 +86,11 @@ struct OrbCand {
 #define MCS_ORB_TILE_H 64
 #endif
 constexpr int kOrbTileW = 64, kOrbTileH = MCS_ORB_TILE_H;
+// threads of an mcs_orb_level block (8 waves: with 4 blocks of 36 KB per CU, 32 waves in flight)
+#ifndef MCS_ORB_LEVEL_THREADS
+#define MCS_ORB_LEVEL_THREADS 512
+#endif
+constexpr int kOrbLevelThreads = MCS_ORB_LEVEL_THREADS;
 // All levels of one frame in one launch (mcs_orb_level): grid (bstart[nlevels]) blocks of 256
 // threads, level l owning blocks [bstart[l], bstart[l + 1]), one block per 64 x 16 tile (row-major
 // over the level).  Level buffers are the bases + off[l] (pixels) and cand + coff[l].

@@ -436,7 +436,8 @@ int enqueue_chain(mcs_rig_job *j, const mcs::rt::Api *A, const mcs::feat::Featur
         }
     }
     if (rc == MCS_OK)
-        rc = launch(A, k->orb_level, (unsigned)d.pa.bstart[L], C, 256, &d.pa, sizeof(d.pa), s);
+        rc = launch(A, k->orb_level, (unsigned)d.pa.bstart[L], C, mcs::kOrbLevelThreads, &d.pa,
+                    sizeof(d.pa), s);
     if (rc == MCS_OK)
         rc = launch(A, k->orb_select, (unsigned)L, C, mcs::kOrbSelThreads, &d.sa, sizeof(d.sa), s);
     if (rc == MCS_OK && g.n_bound > 0)
