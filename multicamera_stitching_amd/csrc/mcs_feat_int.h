@@ -22,7 +22,7 @@ struct FeatureKernels {
     hipFunction_t orb_select = nullptr;
     hipFunction_t l2_prep = nullptr, l2_i8 = nullptr, l2_f32 = nullptr, l2_finalize = nullptr;
     hipFunction_t rig_knn2 = nullptr, rig_match = nullptr, rig_ransac = nullptr,
-                  rig_best = nullptr;
+                  rig_best = nullptr, rig_hyp = nullptr;
     hipFunction_t seam_init = nullptr, seam_hinit = nullptr, seam_relabel = nullptr,
                   seam_push = nullptr, seam_active = nullptr, seam_label = nullptr,
                   seam_relabel_lds = nullptr;

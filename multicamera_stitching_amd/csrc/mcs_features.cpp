@@ -123,6 +123,7 @@ int mcs::feat::feature_kernels(const Api *A, int device, const FeatureKernels **
                    {"mcs_l2_knn2_f32", &k.l2_f32},    {"mcs_l2_knn2_finalize", &k.l2_finalize},
                    {"mcs_rig_knn2", &k.rig_knn2},     {"mcs_rig_match", &k.rig_match},
                    {"mcs_rig_ransac", &k.rig_ransac}, {"mcs_rig_best", &k.rig_best},
+                   {"mcs_rig_hyp", &k.rig_hyp},
                    {"mcs_seam_flow_init", &k.seam_init}, {"mcs_seam_flow_hinit", &k.seam_hinit},
                    {"mcs_seam_flow_relabel", &k.seam_relabel},
                    {"mcs_seam_flow_push", &k.seam_push},

@@ -934,17 +934,62 @@ extern "C" __global__ __launch_bounds__(1024) void mcs_rig_match(const mcs::KRig
 
 // grid (iters, pairs), block kRansacBlock: pair p's hypotheses (none -- scores -1 -- with 4 or
 // fewer matches: the reference needs more than 4 to call findHomography).
+// The rig's RANSAC in two launches: mcs_rig_hyp solves the hypotheses, one per lane (grid
+// (ceil(iters / 64), pairs), block 64: the 4-point solves of 64 hypotheses side by side instead
+// of each on thread 0 of its own block while the other 255 wait), mcs_rig_ransac scores them,
+// one block per hypothesis.  Same functions, same operands: the same models and scores as
+// ransac_block.
+extern "C" __global__ __launch_bounds__(64) void mcs_rig_hyp(const mcs::KRigArgs a)
+{
+    using namespace mcs;
+    const int p = blockIdx.y, k = blockIdx.x * 64 + threadIdx.x, n = a.info[4 * p];
+    if (k >= a.iters || n <= 4) return;
+    const double *pts = a.pts + (int64_t)4 * p * a.kstride;
+    double *hyps = a.hyps + (int64_t)8 * p * a.iters;
+    int idx[4];
+    double sp[8], dp[8], hh[8];
+    bool ok = rs_subset(a.seed, (uint32_t)k, (uint32_t)n, idx);
+    if (ok) {
+        for (int m = 0; m < 4; m++) {
+            sp[2 * m] = pts[4 * idx[m]], sp[2 * m + 1] = pts[4 * idx[m] + 1];
+            dp[2 * m] = pts[4 * idx[m] + 2], dp[2 * m + 1] = pts[4 * idx[m] + 3];
+        }
+        ok = rs_model4(sp, dp, hh);
+    }
+    for (int j = 0; j < 8; j++) hyps[(int64_t)k * 8 + j] = ok ? hh[j] : __builtin_nan("");
+    a.scores[(int64_t)p * a.iters + k] = ok ? 0 : -1;   // (validity, for mcs_rig_ransac)
+}
+
+// grid (iters, pairs), block kRansacBlock: the inliers of hypothesis blockIdx.x (mcs_rig_hyp's
+// model; its score slot holds -1 for a rejected one, which keeps it).
 extern "C" __global__ __launch_bounds__(256) void mcs_rig_ransac(const mcs::KRigArgs a)
 {
     using namespace mcs;
-    const int p = blockIdx.y, k = blockIdx.x, n = a.info[4 * p];
+    const int p = blockIdx.y, k = blockIdx.x, n = a.info[4 * p], tid = threadIdx.x;
     int32_t *scores = a.scores + (int64_t)p * a.iters;
+    __shared__ int wsum[kRansacBlock / 64];
     if (n <= 4) {
-        if (threadIdx.x == 0) scores[k] = -1;
+        if (tid == 0) scores[k] = -1;
         return;
     }
-    ransac_block(a.pts + (int64_t)4 * p * a.kstride, a.hyps + (int64_t)8 * p * a.iters, scores, n,
-                 a.seed, a.t2, k);
+    if (scores[k] < 0) return;   // (block-uniform: rejected by mcs_rig_hyp, score stays -1)
+    const double *hk = a.hyps + (int64_t)8 * p * a.iters + (int64_t)8 * k;
+    double h[8];
+    for (int j = 0; j < 8; j++) h[j] = hk[j];
+    const double *pts = a.pts + (int64_t)4 * p * a.kstride;
+    int c = 0;
+    for (int i = tid; i < n; i += kRansacBlock) {
+        const double *q = pts + 4 * (int64_t)i;
+        c += rs_inlier(h, q[0], q[1], q[2], q[3], a.t2) ? 1 : 0;
+    }
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off, 64);
+    if ((tid & 63) == 0) wsum[tid >> 6] = c;
+    __syncthreads();
+    if (tid == 0) {
+        int t = 0;
+        for (int w = 0; w < kRansacBlock / 64; w++) t += wsum[w];
+        scores[k] = t;
+    }
 }
 
 // grid (pairs), block 1024: pair p's best hypothesis -- the first of the highest score, as the

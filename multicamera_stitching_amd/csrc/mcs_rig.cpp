@@ -447,6 +447,9 @@ int enqueue_chain(mcs_rig_job *j, const mcs::rt::Api *A, const mcs::feat::Featur
                     sizeof(d.ra), s, (unsigned)P);
     if (rc == MCS_OK) rc = launch(A, k->rig_match, (unsigned)P, 1, 1024, &d.ra, sizeof(d.ra), s);
     if (rc == MCS_OK)
+        rc = launch(A, k->rig_hyp, (unsigned)((j->iters + 63) / 64), (unsigned)P, 64, &d.ra,
+                    sizeof(d.ra), s);
+    if (rc == MCS_OK)
         rc = launch(A, k->rig_ransac, (unsigned)j->iters, (unsigned)P, mcs::kRansacBlock, &d.ra,
                     sizeof(d.ra), s);
     if (rc == MCS_OK) rc = launch(A, k->rig_best, (unsigned)P, 1, 1024, &d.ra, sizeof(d.ra), s);
