@@ -1,10 +1,10 @@
-# Round 6: C3 A/B of the main build against variants/$1.so: GPU ORB / estimate tests on main,
+# Round 6: C3 A/B of the main build against variants/$1.so: GPU ORB / estimate / RANSAC tests on main,
 # per-kernel times of the C3 serial run (rocprofv3 --stats) for both, then C3 resident estimate +
 # stitch lines alternating three times.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; mkdir -p gpurun_out
 R="$GRAFT_REPO_ROOT"; V=$1
-timeout -k 10 600 python -u -m pytest tests/test_gpu_orb.py tests/test_gpu_estimate.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_c3ab.log 2>&1 || { tail -30 gpurun_out/pytest_c3ab.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_gpu_orb.py tests/test_gpu_estimate.py tests/test_gpu_ransac.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_c3ab.log 2>&1 || { tail -30 gpurun_out/pytest_c3ab.log; exit 1; }
 tail -1 gpurun_out/pytest_c3ab.log
 for v in main $V; do
   if [ "$v" = main ]; then unset MCS_LIBRARY; else export MCS_LIBRARY="$R/variants/$v.so"; fi
